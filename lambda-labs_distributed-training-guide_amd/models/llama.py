@@ -1,0 +1,267 @@
+"""Llama-family causal LM (Llama-2/3/3.1/3.2, GQA, llama3 RoPE scaling, tied embeddings).
+
+Owned by this repo instead of HF transformers so the layout fits the kernels:
+  * fused QKV weight [(nq + 2 nkv) * d, H] and fused gate|up weight [2 I, H] (one hipBLASLt
+    GEMM each; attention reads q/k/v straight out of the fused output);
+  * the residual add is fused into the following RMSNorm (`add_rms_norm`);
+  * RoPE is applied inside the attention autograd node (in place on the QKV activation);
+  * lm_head + cross entropy are fused and chunked (no [T, V] logits in memory);
+  * activations are 2-D token-major [B*S, H]; packed sequences (position ids restarting at
+    EOS, 00-rime) go through varlen attention via cu_seqlens.
+Tensor parallelism (Megatron column/row + sequence parallel + vocab-parallel embedding and
+loss) is built in: pass `tp_group` and every weight is the local shard.
+
+State-dict names follow HF (`model.layers.N.self_attn.qkv_proj.weight`, ...); `hf_compat`
+converts to/from HF's split q/k/v and gate/up tensors.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .. import ops
+from ..parallel import tp_comm
+from .config import LlamaConfig
+
+
+@dataclasses.dataclass
+class CausalLMOutput:
+    loss: Optional[torch.Tensor] = None
+    logits: Optional[torch.Tensor] = None
+
+
+class Weight(nn.Module):
+    """Parameter holder (no forward); keeps HF-like `<name>.weight` state-dict keys."""
+
+    def __init__(self, *shape, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(*shape, device=device, dtype=dtype))
+
+
+class TPInfo:
+    def __init__(self, group=None):
+        self.group = group
+        self.size = dist.get_world_size(group) if group is not None else 1
+        self.rank = dist.get_rank(group) if group is not None else 0
+
+    @property
+    def enabled(self):
+        return self.size > 1
+
+
+class RunCtx:
+    """Per-forward runtime data shared by all layers."""
+
+    __slots__ = ("cos", "sin", "pos", "cu_seqlens", "max_seqlen")
+
+    def __init__(self, cos, sin, pos, cu_seqlens, max_seqlen):
+        self.cos, self.sin, self.pos, self.cu_seqlens, self.max_seqlen = cos, sin, pos, cu_seqlens, max_seqlen
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, cfg: LlamaConfig, tp: TPInfo, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        assert cfg.num_attention_heads % tp.size == 0 and cfg.num_key_value_heads % tp.size == 0, \
+            "tensor-parallel degree must divide the number of query and key/value heads"
+        self.nq = cfg.num_attention_heads // tp.size
+        self.nkv = cfg.num_key_value_heads // tp.size
+        self.d = cfg.head_dim
+        h = cfg.hidden_size
+        self.qkv_proj = Weight((self.nq + 2 * self.nkv) * self.d, h, device=device, dtype=dtype)
+        self.o_proj = Weight(h, self.nq * self.d, device=device, dtype=dtype)
+
+    def forward(self, x, rc: RunCtx):
+        qkv = ops.linear(x, self.qkv_proj.weight)
+        o = ops.attention(qkv, self.nq, self.nkv, self.d, rc.cu_seqlens, rc.max_seqlen, rc.cos, rc.sin, rc.pos)
+        return ops.linear(o, self.o_proj.weight)
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, cfg: LlamaConfig, tp: TPInfo, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        assert cfg.intermediate_size % tp.size == 0
+        self.inter = cfg.intermediate_size // tp.size
+        self.gate_up_proj = Weight(2 * self.inter, cfg.hidden_size, device=device, dtype=dtype)
+        self.down_proj = Weight(cfg.hidden_size, self.inter, device=device, dtype=dtype)
+
+    def forward(self, x):
+        gu = ops.linear(x, self.gate_up_proj.weight)
+        return ops.linear(ops.swiglu(gu), self.down_proj.weight)
+
+
+class LlamaDecoderLayer(nn.Module):
+    def __init__(self, cfg: LlamaConfig, tp: TPInfo, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.eps = cfg.rms_norm_eps
+        self.tp = tp
+        self.input_layernorm = Weight(cfg.hidden_size, device=device, dtype=dtype)
+        self.post_attention_layernorm = Weight(cfg.hidden_size, device=device, dtype=dtype)
+        self.self_attn = LlamaAttention(cfg, tp, device, dtype)
+        self.mlp = LlamaMLP(cfg, tp, device, dtype)
+        for p in (self.input_layernorm.weight, self.post_attention_layernorm.weight):
+            p._dtg_sequence_parallel = tp.enabled  # replicated over TP; grads need a TP all-reduce
+
+    def forward(self, x, res, rc: RunCtx):
+        """x: previous sub-block output (or embeddings), res: residual stream (None at layer 0).
+        Returns (mlp output, residual stream); the residual add is fused into the next norm."""
+        g = self.tp.group if self.tp.enabled else None
+        if res is None:
+            n, res = ops.rms_norm(x, self.input_layernorm.weight, self.eps), x
+        else:
+            n, res = ops.add_rms_norm(x, res, self.input_layernorm.weight, self.eps)
+        if g is not None:
+            n = tp_comm.gather_seq(n, g)
+        a = self.self_attn(n, rc)
+        if g is not None:
+            a = tp_comm.scatter_seq(a, g)
+        n2, res = ops.add_rms_norm(a, res, self.post_attention_layernorm.weight, self.eps)
+        if g is not None:
+            n2 = tp_comm.gather_seq(n2, g)
+        m = self.mlp(n2)
+        if g is not None:
+            m = tp_comm.scatter_seq(m, g)
+        return m, res
+
+
+class _VocabParallelEmbedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, w, vstart):
+        local = ids - vstart
+        mask = (local < 0) | (local >= w.shape[0])
+        local = local.masked_fill(mask, 0)
+        out = torch.nn.functional.embedding(local, w)
+        out.masked_fill_(mask[:, None], 0)
+        ctx.save_for_backward(local, mask)
+        ctx.w = w
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        local, mask = ctx.saved_tensors
+        dy = dy.masked_fill(mask[:, None], 0)
+        from ..ops.grad_routing import route_embedding_grad
+
+        return None, route_embedding_grad(ctx.w, local, dy.contiguous(), ctx.w.shape[0]), None
+
+
+class LlamaForCausalLM(nn.Module):
+    def __init__(self, cfg: LlamaConfig, tp_group=None, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.config = cfg
+        self.tp = TPInfo(tp_group)
+        tp = self.tp
+        assert cfg.vocab_size % tp.size == 0 or not tp.enabled, "vocab must divide by the TP degree"
+        self.vocab_local = cfg.vocab_size // tp.size
+        self.vocab_start = tp.rank * self.vocab_local
+        self.embed_tokens = Weight(self.vocab_local, cfg.hidden_size, device=device, dtype=dtype)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg, tp, device, dtype) for _ in range(cfg.num_hidden_layers)])
+        self.norm = Weight(cfg.hidden_size, device=device, dtype=dtype)
+        self.norm.weight._dtg_sequence_parallel = tp.enabled
+        self.lm_head = None if cfg.tie_word_embeddings else Weight(self.vocab_local, cfg.hidden_size, device=device, dtype=dtype)
+        if cfg.tie_word_embeddings:
+            self.embed_tokens.weight._dtg_uses = 2  # embedding + lm_head gradient contributions
+        self._rope = None
+        self._dense_cache = {}
+
+    # ---------------------------------------------------------------- init
+    @torch.no_grad()
+    def init_weights(self, std: Optional[float] = None):
+        std = self.config.initializer_range if std is None else std
+        for name, p in self.named_parameters():
+            if p.device.type == "meta":
+                continue
+            if name.endswith("layernorm.weight") or name == "norm.weight":
+                p.fill_(1.0)
+            else:
+                p.normal_(0.0, std)
+
+    def lm_head_weight(self):
+        return self.embed_tokens.weight if self.lm_head is None else self.lm_head.weight
+
+    # ---------------------------------------------------------------- runtime
+    def _rope_tables(self, need: int, device):
+        if self._rope is None or self._rope[0].shape[0] < need or self._rope[0].device != device:
+            n = max(need, 4096)
+            n = (n + 4095) // 4096 * 4096
+            c = self.config
+            self._rope = ops.rope_tables(c.head_dim, c.rope_theta, n, c.rope_scaling, device=device)
+        return self._rope
+
+    def _dense_meta(self, B, S, device):
+        key = (B, S, str(device))
+        v = self._dense_cache.get(key)
+        if v is None:
+            pos = torch.arange(S, device=device, dtype=torch.long).repeat(B)
+            cu = torch.arange(0, (B + 1) * S, S, device=device, dtype=torch.int32)
+            v = (pos, cu)
+            self._dense_cache = {key: v}
+        return v
+
+    def forward(self, input_ids, labels=None, position_ids=None, cu_seqlens=None, max_seqlen=None,
+                num_valid=None, return_logits=False, attention_mask=None):
+        """HF-compatible call: model(input_ids=[B,S], labels=[B,S], position_ids=[B,S]?).
+
+        Packed sequences: pass position_ids (restarting at 0 per document) and ideally
+        cu_seqlens (int32 [ndocs+1]) + max_seqlen from the collator (else derived, 1 sync).
+        `num_valid` (host int) = number of non-ignored shifted labels (avoids a sync)."""
+        B, S = input_ids.shape
+        T = B * S
+        dev = input_ids.device
+        ids = input_ids.reshape(-1)
+        if position_ids is None:
+            pos, cu = self._dense_meta(B, S, dev)
+            max_seqlen = S
+        else:
+            pos = position_ids.reshape(-1).to(torch.long)
+            if cu_seqlens is None:
+                starts = torch.nonzero(pos == 0).flatten()
+                row_starts = torch.arange(0, T, S, device=dev)
+                starts = torch.unique(torch.cat([starts, row_starts]))
+                cu = torch.cat([starts, torch.tensor([T], device=dev)]).to(torch.int32)
+                max_seqlen = int((cu[1:] - cu[:-1]).max().item())
+            else:
+                cu = cu_seqlens.to(device=dev, dtype=torch.int32)
+                if max_seqlen is None:
+                    max_seqlen = int((cu[1:] - cu[:-1]).max().item())
+        cos, sin = self._rope_tables(S, dev)
+        rc = RunCtx(cos, sin, pos, cu, int(max_seqlen))
+        tp = self.tp
+        if tp.enabled:
+            x = _VocabParallelEmbedding.apply(ids, self.embed_tokens.weight, self.vocab_start)
+            x = tp_comm.scatter_seq(x, tp.group)
+        else:
+            x = ops.embedding(ids, self.embed_tokens.weight)
+        res = None
+        for layer in self.layers:
+            x, res = layer(x, res, rc)
+        h, _ = ops.add_rms_norm(x, res, self.norm.weight, self.config.rms_norm_eps)
+        if tp.enabled:
+            h = tp_comm.gather_seq(h, tp.group)
+        out = CausalLMOutput()
+        w = self.lm_head_weight()
+        if labels is not None:
+            shifted = torch.full_like(labels, -100)
+            shifted[:, :-1] = labels[:, 1:]
+            shifted = shifted.reshape(-1)
+            if num_valid is None:
+                num_valid = int((shifted != -100).sum().item())
+            if tp.enabled:
+                out.loss = ops.vocab_parallel_fused_linear_cross_entropy(
+                    h, w, shifted, self.vocab_start, tp.group, num_valid=num_valid)
+            else:
+                out.loss = ops.fused_linear_cross_entropy(h, w, shifted, num_valid=num_valid)
+        if return_logits or labels is None:
+            logits = ops.linear(h, w)
+            if tp.enabled:
+                logits = tp_comm.gather_seq(logits.t().contiguous(), tp.group).t()
+            out.logits = logits.view(B, S, -1)
+        return out
+
+
+def count_valid_labels(labels: torch.Tensor, ignore_index: int = -100) -> int:
+    """Host-side count of shifted labels that contribute to the loss (call on the CPU batch)."""
+    return int((labels[:, 1:] != ignore_index).sum())

@@ -1,0 +1,187 @@
+"""CPU implementations of the `dtg` operators (plain PyTorch, f32 math).
+
+They define the numerics the gfx950 kernels are tested against (tests compare a HIP kernel
+with these on the same inputs) and they run the CPU plumbing configuration (GPT-2 / tiny
+Llama on the build box).  Registered for the CPU dispatch key only.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ._schema import LIB
+
+_LOG2E = 1.4426950408889634
+
+
+def rmsnorm_fwd(x, w, eps):
+    xf = x.float()
+    rstd = torch.rsqrt(xf.pow(2).mean(-1) + eps)
+    n = (xf * rstd[:, None]).to(x.dtype)
+    y = (w.float() * n.float()).to(x.dtype)
+    return y, rstd
+
+
+def add_rmsnorm_fwd(x, res, w, eps):
+    h = (x.float() + res.float()).to(x.dtype)
+    y, rstd = rmsnorm_fwd(h, w, eps)
+    return y, h, rstd
+
+
+def rmsnorm_bwd(dy, x, w, rstd, dres):
+    xf, dyf, wf = x.float(), dy.float(), w.float()
+    n = xf * rstd[:, None]
+    g = dyf * wf
+    dot = (g * n).mean(-1, keepdim=True)
+    dx = rstd[:, None] * (g - n * dot)
+    if dres is not None:
+        dx = dx + dres.float()
+    dw = (dyf * n.to(x.dtype).float()).sum(0)
+    return dx.to(x.dtype), dw.to(w.dtype)
+
+
+def rope_(qkv, cos, sin, pos, nheads, head_dim, inverse):
+    T = qkv.shape[0]
+    half = head_dim // 2
+    view = qkv[:, : nheads * head_dim].reshape(T, nheads, head_dim)
+    x1 = view[..., :half].float()
+    x2 = view[..., half:].float()
+    c = cos[pos][:, None, :]
+    s = sin[pos][:, None, :]
+    if inverse:
+        s = -s
+    o1 = x1 * c - x2 * s
+    o2 = x2 * c + x1 * s
+    qkv[:, : nheads * head_dim] = torch.cat([o1, o2], dim=-1).to(qkv.dtype).reshape(T, nheads * head_dim)
+
+
+def swiglu_fwd(gu):
+    inter = gu.shape[1] // 2
+    g, u = gu[:, :inter].float(), gu[:, inter:].float()
+    return (F.silu(g) * u).to(gu.dtype)
+
+
+def swiglu_bwd(dh, gu):
+    inter = gu.shape[1] // 2
+    g, u, d = gu[:, :inter].float(), gu[:, inter:].float(), dh.float()
+    s = torch.sigmoid(g)
+    du = d * g * s
+    dg = d * u * s * (1 + g * (1 - s))
+    return torch.cat([dg, du], dim=1).to(gu.dtype)
+
+
+def ce_fwd_bwd_(logits, labels, ignore_index, grad_scale, compute_grad):
+    x = logits.float()
+    lse = torch.logsumexp(x, dim=-1)
+    valid = labels != ignore_index
+    safe = torch.where(valid, labels, torch.zeros_like(labels))
+    xl = x.gather(1, safe[:, None])[:, 0]
+    loss = torch.where(valid, lse - xl, torch.zeros_like(lse))
+    if compute_grad:
+        g = torch.exp(x - lse[:, None])
+        g.scatter_add_(1, safe[:, None], -torch.ones_like(g[:, :1]))
+        g = g * grad_scale
+        g[~valid] = 0
+        logits.copy_(g.to(logits.dtype))
+    return loss
+
+
+def ce_stats(logits, labels, vocab_start):
+    x = logits.float()
+    m = x.max(-1).values
+    s = torch.exp(x - m[:, None]).sum(-1)
+    local = labels - vocab_start
+    inside = (local >= 0) & (local < x.shape[1])
+    xl = x.gather(1, local.clamp(0, x.shape[1] - 1)[:, None])[:, 0]
+    return m, s, torch.where(inside, xl, torch.zeros_like(xl))
+
+
+def ce_grad_(logits, labels, lse, vocab_start, ignore_index, grad_scale):
+    x = logits.float()
+    g = torch.exp(x - lse[:, None])
+    local = labels - vocab_start
+    inside = (local >= 0) & (local < x.shape[1])
+    onehot = torch.zeros_like(g)
+    rows = torch.nonzero(inside).flatten()
+    onehot[rows, local[rows]] = 1.0
+    g = (g - onehot) * grad_scale
+    g[labels == ignore_index] = 0
+    logits.copy_(g.to(logits.dtype))
+
+
+def adamw_(p, master, g, m, v, lr, beta1, beta2, eps, wd, step, grad_scale):
+    pf = master if master is not None else p.float()
+    gf = g.float() * grad_scale
+    mf, vf = m.float(), v.float()
+    pf = pf * (1 - lr * wd)
+    mf = mf + (gf - mf) * (1 - beta1)
+    vf = vf * beta2 + (1 - beta2) * gf * gf
+    bc1 = 1 - beta1**step
+    bc2 = math.sqrt(1 - beta2**step)
+    pf = pf - (lr / bc1) * mf / (vf.sqrt() / bc2 + eps)
+    m.copy_(mf)
+    v.copy_(vf)
+    if master is not None:
+        master.copy_(pf)
+    p.copy_(pf)
+
+
+def _attn_ref(q, k, v, cu_seqlens, scale, causal):
+    """Per-sequence f32 attention; returns o (bf16/in dtype) and lse [Hq, T] (natural log)."""
+    T, hq, d = q.shape
+    hkv = k.shape[1]
+    rep = hq // hkv
+    o = torch.zeros(T, hq, d, dtype=torch.float32)
+    lse = torch.full((hq, T), float("-inf"), dtype=torch.float32)
+    cu = cu_seqlens.tolist()
+    for i in range(len(cu) - 1):
+        a, b = cu[i], cu[i + 1]
+        if b <= a:
+            continue
+        qs = q[a:b].float().transpose(0, 1)  # [hq, s, d]
+        ks = k[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        vs = v[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        sc = qs @ ks.transpose(1, 2) * scale
+        if causal:
+            n = b - a
+            mask = torch.ones(n, n, dtype=torch.bool).triu(1)
+            sc = sc.masked_fill(mask, float("-inf"))
+        l_ = torch.logsumexp(sc, -1)
+        p = torch.exp(sc - l_[..., None])
+        o[a:b] = (p @ vs).transpose(0, 1)
+        lse[:, a:b] = l_
+    return o, lse
+
+
+def flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal):
+    o, lse = _attn_ref(q, k, v, cu_seqlens, scale, causal)
+    return o.to(q.dtype), lse
+
+
+def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal):
+    with torch.enable_grad():
+        qf = q.detach().float().requires_grad_()
+        kf = k.detach().float().requires_grad_()
+        vf = v.detach().float().requires_grad_()
+        of, _ = _attn_ref(qf, kf, vf, cu_seqlens, scale, causal)
+        dq, dk, dv = torch.autograd.grad(of, (qf, kf, vf), dout.float())
+    return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
+
+
+def flash_attn_bwd_qkv(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal):
+    T = qkv.shape[0]
+    d = head_dim
+    q = qkv[:, : nq * d].reshape(T, nq, d)
+    k = qkv[:, nq * d : (nq + nkv) * d].reshape(T, nkv, d)
+    v = qkv[:, (nq + nkv) * d :].reshape(T, nkv, d)
+    dq, dk, dv = flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal)
+    return torch.cat([dq.reshape(T, -1), dk.reshape(T, -1), dv.reshape(T, -1)], dim=1)
+
+
+for _name, _fn in list(globals().items()):
+    if _name in (
+        "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
+        "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "flash_attn_fwd", "flash_attn_bwd",
+        "flash_attn_bwd_qkv",
+    ):
+        LIB.impl(_name, _fn, "CPU")

@@ -1,0 +1,32 @@
+"""Operator schemas of the `dtg` library.
+
+Schemas are declared once here; implementations register against them:
+  * CUDA (= HIP on ROCm): the gfx950 kernels in csrc/kernels/*.hip (`_C.so`)
+  * CPU: fp32 PyTorch reference implementations in `dtg.ops._cpu` (tests, CPU plumbing runs)
+PyTorch's dispatcher picks the implementation from the tensors' device.
+"""
+import torch
+
+LIB = torch.library.Library("dtg", "DEF")
+
+_DEFS = [
+    "rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)",
+    "add_rmsnorm_fwd(Tensor x, Tensor residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)",
+    "rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres) -> (Tensor, Tensor)",
+    "rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, Tensor pos, int nheads, int head_dim, bool inverse) -> ()",
+    "swiglu_fwd(Tensor gu) -> Tensor",
+    "swiglu_bwd(Tensor dh, Tensor gu) -> Tensor",
+    "ce_fwd_bwd_(Tensor(a!) logits, Tensor labels, int ignore_index, float grad_scale, bool compute_grad) -> Tensor",
+    "ce_stats(Tensor logits, Tensor labels, int vocab_start) -> (Tensor, Tensor, Tensor)",
+    "ce_grad_(Tensor(a!) logits, Tensor labels, Tensor lse, int vocab_start, int ignore_index, float grad_scale) -> ()",
+    "adamw_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!) m, Tensor(d!) v, float lr, float beta1, "
+    "float beta2, float eps, float wd, int step, float grad_scale) -> ()",
+    "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> (Tensor, Tensor)",
+    "flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor cu_seqlens, "
+    "int max_seqlen, float scale, bool causal) -> (Tensor, Tensor, Tensor)",
+    "flash_attn_bwd_qkv(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
+    "Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> Tensor",
+]
+
+for _d in _DEFS:
+    LIB.define(_d)

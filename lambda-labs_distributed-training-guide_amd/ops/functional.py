@@ -1,0 +1,330 @@
+"""Autograd functions for the decoder hot path.
+
+Each function is a thin torch.autograd.Function over `torch.ops.dtg.*` (HIP on GPU, f32
+reference on CPU) or hipBLASLt GEMMs (`torch.mm`).  Activations stay 2-D token-major
+[T, features] end to end, so no transposes/copies appear between kernels.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from .grad_routing import route_embedding_grad, route_param_grad, route_weight_grad_mm
+
+ops = torch.ops.dtg
+
+
+# --------------------------------------------------------------------------------------------
+# Linear (hipBLASLt) with direct weight-gradient routing
+# --------------------------------------------------------------------------------------------
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return torch.mm(x, w.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
+        dw = route_weight_grad_mm(w, dy, x) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+def linear(x, w, b=None):
+    """y = x @ w^T (+ b); x is [T, in]."""
+    if b is None:
+        return _Linear.apply(x, w)
+    return _LinearBias.apply(x, w, b)
+
+
+class _LinearBias(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w, b)
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b = ctx.saved_tensors
+        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
+        dw = route_weight_grad_mm(w, dy, x) if ctx.needs_input_grad[1] else None
+        db = route_param_grad(b, dy.sum(0)) if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+# --------------------------------------------------------------------------------------------
+# RMSNorm and fused residual-add + RMSNorm
+# --------------------------------------------------------------------------------------------
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        y, rstd = ops.rmsnorm_fwd(x, w, eps)
+        ctx.save_for_backward(x, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dx, dw = ops.rmsnorm_bwd(dy, x, w, rstd, None)
+        return dx, route_param_grad(w, dw), None
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, w, eps):
+        y, h, rstd = ops.add_rmsnorm_fwd(x, res, w, eps)
+        ctx.save_for_backward(h, w, rstd)
+        return y, h
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        h, w, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(h)
+        dx, dw = ops.rmsnorm_bwd(dy, h, w, rstd, dh)
+        return dx, dx, route_param_grad(w, dw), None
+
+
+def rms_norm(x, w, eps):
+    return _RMSNorm.apply(x, w, eps)
+
+
+def add_rms_norm(x, res, w, eps):
+    """Returns (rmsnorm(x + res), x + res)."""
+    return _AddRMSNorm.apply(x, res, w, eps)
+
+
+# --------------------------------------------------------------------------------------------
+# Rotary tables
+# --------------------------------------------------------------------------------------------
+def _llama3_inv_freq(inv_freq, scaling):
+    factor = scaling["factor"]
+    low = scaling.get("low_freq_factor", 1.0)
+    high = scaling.get("high_freq_factor", 4.0)
+    old_ctx = scaling["original_max_position_embeddings"]
+    low_wl = old_ctx / low
+    high_wl = old_ctx / high
+    wavelen = 2 * math.pi / inv_freq
+    out = torch.where(wavelen > low_wl, inv_freq / factor, inv_freq)
+    smooth = (old_ctx / wavelen - low) / (high - low)
+    smoothed = (1 - smooth) * out / factor + smooth * out
+    is_medium = (wavelen >= high_wl) & (wavelen <= low_wl)
+    return torch.where(is_medium, smoothed, out)
+
+
+def rope_tables(head_dim, theta, max_pos, scaling=None, device=None):
+    """cos/sin [max_pos, head_dim/2] f32 (HF LlamaRotaryEmbedding semantics, incl. llama3 scaling)."""
+    inv_freq = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.int64).float() / head_dim))
+    attn_factor = 1.0
+    if scaling is not None:
+        kind = scaling.get("rope_type", scaling.get("type"))
+        if kind == "llama3":
+            inv_freq = _llama3_inv_freq(inv_freq, scaling)
+        elif kind in (None, "default"):
+            pass
+        else:
+            raise NotImplementedError(f"rope scaling {kind}")
+    t = torch.arange(max_pos, dtype=torch.float32)
+    freqs = torch.outer(t, inv_freq)
+    cos = (freqs.cos() * attn_factor).contiguous()
+    sin = (freqs.sin() * attn_factor).contiguous()
+    if device is not None:
+        cos, sin = cos.to(device), sin.to(device)
+    return cos, sin
+
+
+# --------------------------------------------------------------------------------------------
+# Attention (RoPE fused into the same autograd node; fused QKV in, fused dQKV out)
+# --------------------------------------------------------------------------------------------
+class _AttentionQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, pos, cu_seqlens, max_seqlen, nq, nkv, head_dim, scale, causal, rope):
+        T = qkv.shape[0]
+        d = head_dim
+        if rope:
+            ops.rope_(qkv, cos, sin, pos, nq + nkv, d, False)
+        q = qkv.as_strided((T, nq, d), (qkv.stride(0), d, 1), qkv.storage_offset())
+        k = qkv.as_strided((T, nkv, d), (qkv.stride(0), d, 1), qkv.storage_offset() + nq * d)
+        v = qkv.as_strided((T, nkv, d), (qkv.stride(0), d, 1), qkv.storage_offset() + (nq + nkv) * d)
+        o, lse = ops.flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal)
+        ctx.save_for_backward(qkv, o, lse, cu_seqlens, cos, sin, pos)
+        ctx.meta = (max_seqlen, nq, nkv, d, scale, causal, rope)
+        return o.view(T, nq * d)
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, cu, cos, sin, pos = ctx.saved_tensors
+        max_seqlen, nq, nkv, d, scale, causal, rope = ctx.meta
+        T = qkv.shape[0]
+        dqkv = ops.flash_attn_bwd_qkv(do.contiguous().view(T, nq, d), qkv, nq, nkv, d, o, lse, cu, max_seqlen, scale, causal)
+        if rope:
+            ops.rope_(dqkv, cos, sin, pos, nq + nkv, d, True)
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
+
+
+def attention(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos=None, sin=None, pos=None, causal=True, scale=None):
+    """Causal (varlen) GQA attention on a fused [T, (nq+2nkv)*d] QKV activation -> [T, nq*d].
+
+    If cos/sin/pos are given, RoPE is applied to q and k first (in place on qkv)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(head_dim)
+    rope = cos is not None
+    if not rope:
+        cos = sin = torch.empty(0, device=qkv.device)
+        pos = torch.empty(0, dtype=torch.long, device=qkv.device)
+    return _AttentionQKV.apply(qkv, cos, sin, pos, cu_seqlens, int(max_seqlen), nq, nkv, head_dim, float(scale), causal, rope)
+
+
+# --------------------------------------------------------------------------------------------
+# SwiGLU
+# --------------------------------------------------------------------------------------------
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        ctx.save_for_backward(gu)
+        return ops.swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (gu,) = ctx.saved_tensors
+        return ops.swiglu_bwd(dh.contiguous(), gu)
+
+
+def swiglu(gu):
+    return _SwiGLU.apply(gu)
+
+
+# --------------------------------------------------------------------------------------------
+# Embedding
+# --------------------------------------------------------------------------------------------
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, w):
+        ctx.save_for_backward(ids)
+        ctx.w = w
+        return F.embedding(ids, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        w = ctx.w
+        return None, route_embedding_grad(w, ids, dy.contiguous(), w.shape[0])
+
+
+def embedding(ids, w):
+    return _Embedding.apply(ids, w)
+
+
+# --------------------------------------------------------------------------------------------
+# Fused lm_head + causal-LM cross entropy (chunked; logits never materialised whole)
+# --------------------------------------------------------------------------------------------
+def _default_chunk(vocab, hidden_rows):
+    # ~1 GiB of bf16 logits per chunk; at least 1024 rows.
+    return max(1024, min(hidden_rows, (1 << 29) // max(vocab, 1)))
+
+
+class _FusedLinearCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, w, labels, ignore_index, num_valid, chunk):
+        T = h.shape[0]
+        need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        scale = 1.0 / max(num_valid, 1)
+        loss_sum = torch.zeros((), dtype=torch.float32, device=h.device)
+        dh = torch.empty_like(h) if need else None
+        dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if (need and ctx.needs_input_grad[1]) else None
+        for s in range(0, T, chunk):
+            e = min(T, s + chunk)
+            logits = torch.mm(h[s:e], w.t())
+            rows = ops.ce_fwd_bwd_(logits, labels[s:e], ignore_index, scale, need)
+            loss_sum += rows.sum()
+            if need:
+                torch.mm(logits, w, out=dh[s:e])
+                if dw is not None:
+                    # f32 accumulate inside the GEMM, one bf16 rounding per chunk
+                    if s == 0:
+                        torch.mm(logits.t(), h[s:e], out=dw)
+                    else:
+                        dw.addmm_(logits.t(), h[s:e])
+        ctx.save_for_backward(dh, dw)
+        ctx.w = w
+        return loss_sum * scale
+
+    @staticmethod
+    def backward(ctx, go):
+        dh, dw = ctx.saved_tensors
+        w = ctx.w
+        gdh = (dh * go.to(dh.dtype)) if ctx.needs_input_grad[0] else None
+        gdw = route_param_grad(w, dw * go.to(dw.dtype)) if dw is not None else None
+        return gdh, gdw, None, None, None, None
+
+
+def fused_linear_cross_entropy(h, w, labels, ignore_index=-100, num_valid=None, chunk=None):
+    """mean CE of softmax(h @ w^T) vs labels over rows with label != ignore_index.
+
+    `labels` are already shifted (label of row i = token i+1).  `num_valid` (host int) avoids a
+    device sync; if None it is computed (one sync)."""
+    if num_valid is None:
+        num_valid = int((labels != ignore_index).sum().item())
+    if chunk is None:
+        chunk = _default_chunk(w.shape[0], h.shape[0])
+    return _FusedLinearCE.apply(h, w, labels, ignore_index, int(num_valid), int(chunk))
+
+
+class _VocabParallelFusedLinearCE(torch.autograd.Function):
+    """lm_head sharded over the vocabulary across `group` (tensor parallel); h is replicated.
+
+    Per chunk: local logits -> (max, sum-exp, target logit) -> all-reduces over the TP group
+    -> global log-sum-exp -> local softmax gradient in place.  The returned
+    dh is this rank's vocab-shard PARTIAL; the caller's TP-region entry (sequence all-gather,
+    whose backward is a reduce-scatter) sums it across ranks."""
+
+    @staticmethod
+    def forward(ctx, h, w, labels, ignore_index, num_valid, chunk, vocab_start, group):
+        T = h.shape[0]
+        need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        scale = 1.0 / max(num_valid, 1)
+        loss_sum = torch.zeros((), dtype=torch.float32, device=h.device)
+        dh = torch.empty_like(h) if need else None
+        dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if need else None
+        for s in range(0, T, chunk):
+            e = min(T, s + chunk)
+            lab = labels[s:e]
+            logits = torch.mm(h[s:e], w.t())
+            m, sx, xl = ops.ce_stats(logits, lab, vocab_start)
+            gm = m.clone()
+            dist.all_reduce(gm, op=dist.ReduceOp.MAX, group=group)
+            sx = sx * torch.exp(m - gm)
+            stats = torch.stack([sx, xl])
+            dist.all_reduce(stats, group=group)
+            lse = gm + torch.log(stats[0])
+            valid = lab != ignore_index
+            loss_sum += torch.where(valid, lse - stats[1], torch.zeros_like(lse)).sum()
+            if need:
+                ops.ce_grad_(logits, lab, lse.contiguous(), vocab_start, ignore_index, scale)
+                torch.mm(logits, w, out=dh[s:e])
+                if s == 0:
+                    torch.mm(logits.t(), h[s:e], out=dw)
+                else:
+                    dw.addmm_(logits.t(), h[s:e])
+        ctx.save_for_backward(dh, dw)
+        ctx.w = w
+        return loss_sum * scale
+
+    @staticmethod
+    def backward(ctx, go):
+        dh, dw = ctx.saved_tensors
+        gdh = dh * go.to(dh.dtype)
+        gdw = route_param_grad(ctx.w, dw * go.to(dw.dtype))
+        return gdh, gdw, None, None, None, None, None, None
+
+
+def vocab_parallel_fused_linear_cross_entropy(h, w_local, labels, vocab_start, group, ignore_index=-100,
+                                              num_valid=None, chunk=None):
+    if num_valid is None:
+        num_valid = int((labels != ignore_index).sum().item())
+    if chunk is None:
+        chunk = _default_chunk(w_local.shape[0], h.shape[0])
+    return _VocabParallelFusedLinearCE.apply(h, w_local, labels, ignore_index, int(num_valid), int(chunk),
+                                             int(vocab_start), group)

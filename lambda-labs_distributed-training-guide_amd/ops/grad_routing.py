@@ -1,0 +1,65 @@
+"""Weight-gradient routing shared by all `dtg` autograd functions.
+
+A parameter managed by a parallel engine carries `main_grad` (a view into the engine's flat
+gradient buffer) and `_dtg_notify` (the engine's "this gradient is final for this backward"
+callback, used to launch bucketed all-reduce / reduce-scatter while backward continues).
+Functions compute a weight gradient straight into `main_grad` -- the first contribution of a
+step writes (`out=`), later ones (tied embeddings, gradient accumulation) add -- and return
+None to autograd.  Parameters without `main_grad` get an ordinary gradient.
+"""
+import torch
+
+
+def _fresh(param) -> bool:
+    return not getattr(param, "_dtg_grad_written", False)
+
+
+def _mark(param):
+    param._dtg_grad_written = True
+    cb = getattr(param, "_dtg_notify", None)
+    if cb is not None:
+        cb(param)
+
+
+def route_param_grad(param, grad):
+    """Add `grad` into param.main_grad if present; otherwise return it for autograd."""
+    mg = getattr(param, "main_grad", None)
+    if mg is None:
+        return grad
+    if _fresh(param):
+        mg.copy_(grad.view_as(mg))
+    else:
+        mg.add_(grad.view_as(mg))
+    _mark(param)
+    return None
+
+
+def route_weight_grad_mm(param, a, b):
+    """Weight gradient a^T @ b (a: [T, out], b: [T, in]) into main_grad without a temporary."""
+    mg = getattr(param, "main_grad", None)
+    if mg is None:
+        return a.t() @ b
+    if _fresh(param):
+        torch.mm(a.t(), b, out=mg)
+    else:
+        mg.addmm_(a.t(), b)
+    _mark(param)
+    return None
+
+
+def route_embedding_grad(param, ids, dy, num_weights):
+    mg = getattr(param, "main_grad", None)
+    if mg is None:
+        g = torch.zeros(num_weights, dy.shape[-1], dtype=dy.dtype, device=dy.device)
+        g.index_add_(0, ids, dy)
+        return g
+    if _fresh(param):
+        mg.zero_()
+    mg.index_add_(0, ids, dy)
+    _mark(param)
+    return None
+
+
+def reset_grad_state(params):
+    for p in params:
+        p._dtg_grad_written = False

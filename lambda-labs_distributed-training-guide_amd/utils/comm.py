@@ -1,0 +1,72 @@
+"""Collective primitives over torch.distributed (RCCL on MI355X, gloo on CPU).
+
+Thin helpers that pick the native collective where the backend has it: RCCL implements
+`all_gather_into_tensor` / `reduce_scatter_tensor` directly; gloo (CPU tests) lacks
+reduce-scatter, so it is expressed as all-reduce + local slice there.  These helpers are used
+by the TP/SP functions and the DDP/ZeRO/FSDP engines.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def backend_of(group=None) -> str:
+    return dist.get_backend(group)
+
+
+def world(group=None) -> int:
+    return dist.get_world_size(group) if dist.is_initialized() else 1
+
+
+def rank(group=None) -> int:
+    return dist.get_rank(group) if dist.is_initialized() else 0
+
+
+def all_gather_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
+    n = world(group)
+    if n == 1:
+        return x
+    out = torch.empty((x.shape[0] * n,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=group)
+    return out
+
+
+def reduce_scatter_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
+    n = world(group)
+    if n == 1:
+        return x
+    assert x.shape[0] % n == 0, f"dim 0 ({x.shape[0]}) must divide by group size {n}"
+    chunk = x.shape[0] // n
+    if backend_of(group) == "gloo":
+        y = x.clone()
+        dist.all_reduce(y, group=group)
+        r = rank(group)
+        return y[r * chunk:(r + 1) * chunk].contiguous()
+    out = torch.empty((chunk,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, x, group=group)
+    return out
+
+
+def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group=None, async_op=False):
+    """Flat all-gather: out.numel() == shard.numel() * world."""
+    return dist.all_gather_into_tensor(out, shard, group=group, async_op=async_op)
+
+
+class _DoneWork:
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group=None, async_op=False):
+    """Flat sum reduce-scatter of `full` into this rank's `out` chunk."""
+    if backend_of(group) == "gloo":
+        dist.all_reduce(full, group=group)
+        r = rank(group)
+        n = out.numel()
+        out.copy_(full.view(-1)[r * n:(r + 1) * n].view_as(out))
+        return _DoneWork() if async_op else None
+    return dist.reduce_scatter_tensor(out, full, group=group, async_op=async_op)

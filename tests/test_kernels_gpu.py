@@ -1,0 +1,214 @@
+"""T6: every gfx950 HIP kernel against the f32 PyTorch reference of the same op (CPU impl).
+
+Inputs are generated once on the CPU, the kernel runs on cuda:0, the reference on the CPU, and
+outputs are compared in f32 with bf16-appropriate tolerances.
+"""
+import math
+
+import pytest
+import torch
+
+import dtg  # noqa: F401
+from dtg import ops
+from dtg.ops import _native
+
+pytestmark = pytest.mark.gpu
+dops = torch.ops.dtg
+
+
+def _close(a, b, atol, rtol=0.0, name=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{name}: {bad} elems off, max err {err.max().item():.4g}"
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def test_native_loaded(cuda):
+    assert _native.LOADED, "gfx950 extension must be loaded on a GPU box"
+
+
+@pytest.mark.parametrize("T,H", [(257, 4096), (64, 3072), (33, 128), (8, 16384)])
+def test_rmsnorm(cuda, T, H):
+    torch.manual_seed(0)
+    x = torch.randn(T, H).bfloat16()
+    r = torch.randn(T, H).bfloat16()
+    w = (1 + 0.1 * torch.randn(H)).bfloat16()
+    dy = torch.randn(T, H).bfloat16()
+    dres = torch.randn(T, H).bfloat16()
+    y_ref, rstd_ref = dops.rmsnorm_fwd(x, w, 1e-5)
+    y, rstd = dops.rmsnorm_fwd(x.to(cuda), w.to(cuda), 1e-5)
+    _close(y, y_ref, 2e-2, 1e-2, "rmsnorm y")
+    _close(rstd, rstd_ref, 1e-4, 1e-4, "rstd")
+    y2_ref, h_ref, _ = dops.add_rmsnorm_fwd(x, r, w, 1e-5)
+    y2, h, rstd2 = dops.add_rmsnorm_fwd(x.to(cuda), r.to(cuda), w.to(cuda), 1e-5)
+    _close(h, h_ref, 0, 0, "residual sum")
+    _close(y2, y2_ref, 2e-2, 1e-2, "add_rmsnorm y")
+    dx_ref, dw_ref = dops.rmsnorm_bwd(dy, x, w, rstd_ref, dres)
+    dx, dw = dops.rmsnorm_bwd(dy.to(cuda), x.to(cuda), w.to(cuda), rstd, dres.to(cuda))
+    _close(dx, dx_ref, 3e-2, 2e-2, "dx")
+    assert _rel(dw, dw_ref) < 1e-2
+
+
+@pytest.mark.parametrize("D,nh", [(128, 40), (64, 6)])
+def test_rope(cuda, D, nh):
+    torch.manual_seed(0)
+    T = 300
+    cols = nh * D + 2 * D  # an extra (v-like) head region the kernel must not touch
+    qkv = torch.randn(T, cols).bfloat16()
+    cos, sin = ops.rope_tables(D, 500000.0, 4096, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                                    "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    pos = torch.randint(0, 4096, (T,))
+    ref = qkv.clone()
+    dops.rope_(ref, cos, sin, pos, nh, D, False)
+    g = qkv.to(cuda)
+    dops.rope_(g, cos.to(cuda), sin.to(cuda), pos.to(cuda), nh, D, False)
+    _close(g, ref, 2e-2, 1e-2, "rope")
+    dops.rope_(g, cos.to(cuda), sin.to(cuda), pos.to(cuda), nh, D, True)
+    _close(g, qkv, 3e-2, 2e-2, "rope inverse")
+
+
+def test_swiglu(cuda):
+    torch.manual_seed(0)
+    T, I = 77, 1792
+    gu = (2 * torch.randn(T, 2 * I)).bfloat16()
+    dh = torch.randn(T, I).bfloat16()
+    _close(dops.swiglu_fwd(gu.to(cuda)), dops.swiglu_fwd(gu), 2e-2, 1e-2, "swiglu")
+    _close(dops.swiglu_bwd(dh.to(cuda), gu.to(cuda)), dops.swiglu_bwd(dh, gu), 3e-2, 2e-2, "swiglu bwd")
+
+
+@pytest.mark.parametrize("V", [50257, 1000, 128256, 156939])
+def test_cross_entropy(cuda, V):
+    torch.manual_seed(0)
+    t = 37
+    full = (3 * torch.randn(t, V + 3)).bfloat16()
+    logits = full[:, 1:V + 1]  # misaligned rows exercise the scalar head/tail
+    labels = torch.randint(0, V, (t,))
+    labels[3] = -100
+    labels[10] = -100
+    ref = logits.clone()
+    loss_ref = dops.ce_fwd_bwd_(ref, labels, -100, 0.25, True)
+    gl = logits.to(cuda)
+    loss = dops.ce_fwd_bwd_(gl, labels.to(cuda), -100, 0.25, True)
+    _close(loss, loss_ref, 2e-3, 1e-3, "ce loss")
+    _close(gl, ref, 2e-4, 2e-2, "ce grad")
+    # vocab-parallel pieces: two shards combined on the host equal the fused result
+    half = V // 2
+    lg = logits.to(cuda)
+    m0, s0, x0 = dops.ce_stats(lg[:, :half], labels.to(cuda), 0)
+    m1, s1, x1 = dops.ce_stats(lg[:, half:], labels.to(cuda), half)
+    gm = torch.maximum(m0, m1)
+    lse = gm + torch.log(s0 * torch.exp(m0 - gm) + s1 * torch.exp(m1 - gm))
+    valid = labels.to(cuda) != -100
+    loss_vp = torch.where(valid, lse - (x0 + x1), torch.zeros_like(lse))
+    _close(loss_vp, loss_ref, 2e-3, 1e-3, "vocab-parallel loss")
+    a, b = lg[:, :half].clone(), lg[:, half:].clone()
+    dops.ce_grad_(a, labels.to(cuda), lse.contiguous(), 0, -100, 0.25)
+    dops.ce_grad_(b, labels.to(cuda), lse.contiguous(), half, -100, 0.25)
+    _close(torch.cat([a, b], 1), ref, 2e-4, 2e-2, "vocab-parallel grad")
+
+
+@pytest.mark.parametrize("state_dtype,master", [(torch.bfloat16, False), (torch.float32, False), (torch.float32, True)])
+@pytest.mark.parametrize("n", [1 << 20, 1001])
+def test_adamw(cuda, state_dtype, master, n):
+    torch.manual_seed(0)
+    p = torch.randn(n).bfloat16()
+    g = torch.randn(n).bfloat16()
+    m = (0.1 * torch.randn(n)).to(state_dtype)
+    v = (0.01 * torch.rand(n)).to(state_dtype)
+    mw = p.float() if master else None
+    P = [t.clone() if t is not None else None for t in (p, g, m, v, mw)]
+    G = [t.to(cuda) if t is not None else None for t in (p, g, m, v, mw)]
+    for step in (1, 2, 3):
+        dops.adamw_(P[0], P[4], P[1], P[2], P[3], 1e-3, 0.9, 0.999, 1e-8, 0.01, step, 0.5)
+        dops.adamw_(G[0], G[4], G[1], G[2], G[3], 1e-3, 0.9, 0.999, 1e-8, 0.01, step, 0.5)
+    _close(G[0], P[0], 1e-2, 1e-2, "param")
+    _close(G[2], P[2], 1e-3, 1e-2, "exp_avg")
+    _close(G[3], P[3], 1e-5, 1e-2, "exp_avg_sq")
+    # match torch's own fused AdamW (the reference's optimizer) on bf16 params/states
+    if state_dtype == torch.bfloat16 and not master:
+        tp = torch.nn.Parameter(p.clone().to(cuda))
+        opt = torch.optim.AdamW([tp], lr=1e-3, fused=True)
+        pm = p.clone().to(cuda)
+        mm = torch.zeros(n, dtype=torch.bfloat16, device=cuda)
+        vv = torch.zeros(n, dtype=torch.bfloat16, device=cuda)
+        for step in (1, 2, 3):
+            tp.grad = g.to(cuda)
+            opt.step()
+            dops.adamw_(pm, None, g.to(cuda), mm, vv, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, 1.0)
+        assert (tp.detach().float() - pm.float()).abs().max().item() <= 2 * 2**-7 * tp.detach().float().abs().max().item()
+
+
+def _attn_case(cuda, seqlens, hq, hkv, D, causal, stride_extra=0):
+    torch.manual_seed(0)
+    T = sum(seqlens)
+    cu = torch.tensor([0] + list(torch.tensor(seqlens).cumsum(0).tolist()), dtype=torch.int32)
+    cols = (hq + 2 * hkv) * D + stride_extra
+    qkv = torch.randn(T, cols).bfloat16()
+    q = qkv[:, : hq * D].view(T, hq, D)
+    k = qkv[:, hq * D:(hq + hkv) * D].view(T, hkv, D)
+    v = qkv[:, (hq + hkv) * D:(hq + 2 * hkv) * D].view(T, hkv, D)
+    scale = 1 / math.sqrt(D)
+    o_ref, lse_ref = dops.flash_attn_fwd(q, k, v, cu, max(seqlens), scale, causal)
+    g = qkv.to(cuda)
+    gq = g[:, : hq * D].view(T, hq, D)
+    gk = g[:, hq * D:(hq + hkv) * D].view(T, hkv, D)
+    gv = g[:, (hq + hkv) * D:(hq + 2 * hkv) * D].view(T, hkv, D)
+    o, lse = dops.flash_attn_fwd(gq, gk, gv, cu.to(cuda), max(seqlens), scale, causal)
+    _close(o, o_ref, 2e-2, 2e-2, "attn out")
+    _close(lse, lse_ref, 2e-3, 1e-3, "lse")
+    do = torch.randn(T, hq, D).bfloat16()
+    dq_ref, dk_ref, dv_ref = dops.flash_attn_bwd(do, q, k, v, o_ref, lse_ref, cu, max(seqlens), scale, causal)
+    dq, dk, dv = dops.flash_attn_bwd(do.to(cuda), gq, gk, gv, o, lse, cu.to(cuda), max(seqlens), scale, causal)
+    for a, b, n in ((dq, dq_ref, "dq"), (dk, dk_ref, "dk"), (dv, dv_ref, "dv")):
+        assert _rel(a, b) < 2e-2, f"{n} rel err {_rel(a, b)}"
+    return qkv, cu
+
+
+@pytest.mark.parametrize("seqlens", [[1024], [100, 257, 667], [64, 1, 129, 130]])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attn_d128_gqa(cuda, seqlens, causal):
+    _attn_case(cuda, seqlens, hq=8, hkv=2, D=128, causal=causal, stride_extra=8)
+
+
+@pytest.mark.parametrize("seqlens", [[512, 300]])
+def test_flash_attn_d64_mha(cuda, seqlens):
+    _attn_case(cuda, seqlens, hq=4, hkv=4, D=64, causal=True)
+
+
+def test_flash_attn_bwd_qkv_fused(cuda):
+    torch.manual_seed(0)
+    T, hq, hkv, D = 384, 4, 1, 128
+    cu = torch.tensor([0, 200, 384], dtype=torch.int32)
+    qkv = torch.randn(T, (hq + 2 * hkv) * D).bfloat16()
+    do = torch.randn(T, hq, D).bfloat16()
+    scale = 1 / math.sqrt(D)
+    views = lambda t: (t[:, : hq * D].view(T, hq, D), t[:, hq * D:(hq + hkv) * D].view(T, hkv, D), t[:, (hq + hkv) * D:].view(T, hkv, D))
+    g = qkv.to(cuda)
+    o, lse = dops.flash_attn_fwd(*views(g), cu.to(cuda), 200, scale, True)
+    ref = torch.cat([t.reshape(T, -1) for t in dops.flash_attn_bwd(do.to(cuda), *views(g), o, lse, cu.to(cuda), 200, scale, True)], 1)
+    fused = dops.flash_attn_bwd_qkv(do.to(cuda), g, hq, hkv, D, o, lse, cu.to(cuda), 200, scale, True)
+    _close(fused, ref, 0, 0, "fused dqkv layout")
+
+
+def test_llama_tiny_gpu_matches_cpu(cuda):
+    from dtg.models import build_model
+
+    torch.manual_seed(0)
+    cpu = build_model("llama-tiny-d128", device="cpu", dtype=torch.float32)
+    gpu = build_model("llama-tiny-d128", device=cuda)
+    gpu.load_state_dict({k: v.bfloat16() for k, v in cpu.state_dict().items()})
+    ids = torch.randint(0, 1000, (2, 256))
+    lc = cpu(input_ids=ids, labels=ids).loss
+    lg = gpu(input_ids=ids.to(cuda), labels=ids.to(cuda)).loss
+    assert abs(lc.item() - lg.item()) < 0.05
+    lg.backward()
+    gn = torch.stack([p.grad.float().norm() for p in gpu.parameters()]).norm().item()
+    lc.backward()
+    cn = torch.stack([p.grad.float().norm() for p in cpu.parameters()]).norm().item()
+    assert abs(gn - cn) / cn < 0.05
