@@ -111,7 +111,7 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
     DTG_CHECK(master->scalar_type() == at::kFloat && master->numel() == n && master->is_contiguous(),
               "adamw_: master must be contiguous f32");
   if (n == 0) return;
-  c10::hip::HIPGuard gd(p.device());
+  const c10::DeviceGuard gd(p.device());
   AdamHyper h;
   h.lr = lr;
   h.beta1 = beta1;

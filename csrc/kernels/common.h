@@ -12,7 +12,7 @@
 
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 namespace dtg {

@@ -61,16 +61,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int rowA, int rowB, 
   const int colbase = col0 + 16 * (g & 1);
   const int ch = (colbase >> 3) + (p >> 1);
   const int half = 8 * (p & 1);
-  i16x4 a = tr_read(tile + off<W>(rowA + q, ch) + half);
-  i16x4 b = tr_read(tile + off<W>(rowB + q, ch) + half);
-  i16x4 lo = a, hi = b;
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    r[j] = __builtin_bit_cast(__bf16, lo[j]);
-    r[4 + j] = __builtin_bit_cast(__bf16, hi[j]);
-  }
-  return r;
+  const i16x4 a = tr_read(tile + off<W>(rowA + q, ch) + half);
+  const i16x4 b = tr_read(tile + off<W>(rowB + q, ch) + half);
+  // Whole-vector concatenation: per-element extraction of the tr-read result miscompiles on
+  // ROCm 7.2 (hipcc duplicates the low dword; caught by tests/native/probe_fragments.hip).
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const i16x8 ab = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, ab);
 }
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -521,7 +518,7 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   DTG_CHECK(D == 64 || D == 128, "flash_attn: head_dim must be 64 or 128");
   DTG_CHECK(cu_seqlens.scalar_type() == at::kInt && cu_seqlens.is_cuda() && cu_seqlens.is_contiguous(),
             "flash_attn: cu_seqlens must be int32 on the GPU");
-  c10::hip::HIPGuard g(q.device());
+  const c10::DeviceGuard g(q.device());
   auto o = at::empty({T, hq, D}, q.options());
   auto lse = at::empty({hq, T}, q.options().dtype(at::kFloat));
   const int nseq = cu_seqlens.numel() - 1;
@@ -562,7 +559,7 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   DTG_CHECK(D == 64 || D == 128, "flash_attn: head_dim must be 64 or 128");
   DTG_CHECK(cu_seqlens.scalar_type() == at::kInt && cu_seqlens.is_cuda() && cu_seqlens.is_contiguous(),
             "flash_attn: cu_seqlens must be int32 on the GPU");
-  c10::hip::HIPGuard g(q.device());
+  const c10::DeviceGuard g(q.device());
   auto opts = q.options();
   const int nseq = cu_seqlens.numel() - 1;
   // Rows outside every sequence (none in practice) keep zero gradients.

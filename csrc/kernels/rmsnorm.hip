@@ -169,7 +169,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Te
   DTG_CHECK_CUDA_BF16(w);
   const int T = x.size(0), H = x.size(1);
   DTG_CHECK(H % 8 == 0 && w.numel() == H && w.is_contiguous(), "rmsnorm: bad weight/hidden");
-  c10::hip::HIPGuard g(x.device());
+  const c10::DeviceGuard g(x.device());
   auto y = at::empty({T, H}, x.options());
   auto rstd = at::empty({T}, x.options().dtype(at::kFloat));
   if (T == 0) return {y, rstd};
@@ -190,7 +190,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> add_rmsnorm_fwd(const at::Tensor&
   const int T = x.size(0), H = x.size(1);
   DTG_CHECK(res.size(0) == T && res.size(1) == H, "add_rmsnorm: shape mismatch");
   DTG_CHECK(H % 8 == 0 && w.numel() == H && w.is_contiguous(), "rmsnorm: bad weight/hidden");
-  c10::hip::HIPGuard g(x.device());
+  const c10::DeviceGuard g(x.device());
   auto y = at::empty({T, H}, x.options());
   auto h = at::empty({T, H}, x.options());
   auto rstd = at::empty({T}, x.options().dtype(at::kFloat));
@@ -212,7 +212,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy_, const at::
   const int T = x.size(0), H = x.size(1);
   DTG_CHECK(dy.size(0) == T && dy.size(1) == H, "rmsnorm_bwd: dy shape");
   DTG_CHECK(rstd.scalar_type() == at::kFloat && rstd.numel() == T, "rmsnorm_bwd: rstd");
-  c10::hip::HIPGuard g(x.device());
+  const c10::DeviceGuard g(x.device());
   auto dx = at::empty({T, H}, x.options());
   auto dw = at::empty({H}, w.options());
   if (T == 0) { dw.zero_(); return {dx, dw}; }

@@ -64,7 +64,7 @@ void rope_(const at::Tensor& qkv, const at::Tensor& cos_t, const at::Tensor& sin
             "rope: position ids must be int64 [T]");
   const int64_t T = qkv.size(0);
   if (T == 0) return;
-  c10::hip::HIPGuard g(qkv.device());
+  const c10::DeviceGuard g(qkv.device());
   const int threads = 256;
   if (head_dim == 128) {
     const int64_t total = T * nheads * (64 / 8);

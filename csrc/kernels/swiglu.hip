@@ -54,7 +54,7 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
             "swiglu: gu must be [T, 2I] with I % 8 == 0");
   const int64_t T = gu.size(0);
   const int I = gu.size(1) / 2;
-  c10::hip::HIPGuard g(gu.device());
+  const c10::DeviceGuard g(gu.device());
   auto h = at::empty({T, I}, gu.options());
   const int64_t n = T * (I / 8);
   if (n == 0) return h;
@@ -71,7 +71,7 @@ at::Tensor swiglu_bwd(const at::Tensor& dh_, const at::Tensor& gu) {
   const int64_t T = gu.size(0);
   const int I = gu.size(1) / 2;
   DTG_CHECK(dh.size(0) == T && dh.size(1) == I, "swiglu_bwd: shape mismatch");
-  c10::hip::HIPGuard g(gu.device());
+  const c10::DeviceGuard g(gu.device());
   auto dgu = at::empty({T, 2 * I}, gu.options());
   const int64_t n = T * (I / 8);
   if (n == 0) return dgu;

@@ -160,7 +160,7 @@ static void check_logits(const at::Tensor& logits, const at::Tensor& labels) {
 at::Tensor ce_fwd_bwd_(const at::Tensor& logits, const at::Tensor& labels, int64_t ignore_index,
                        double grad_scale, bool compute_grad) {
   check_logits(logits, labels);
-  c10::hip::HIPGuard g(logits.device());
+  const c10::DeviceGuard g(logits.device());
   const int64_t t = logits.size(0);
   auto loss = at::empty({t}, logits.options().dtype(at::kFloat));
   if (t == 0) return loss;
@@ -175,7 +175,7 @@ at::Tensor ce_fwd_bwd_(const at::Tensor& logits, const at::Tensor& labels, int64
 std::tuple<at::Tensor, at::Tensor, at::Tensor> ce_stats(const at::Tensor& logits,
                                                         const at::Tensor& labels, int64_t vstart) {
   check_logits(logits, labels);
-  c10::hip::HIPGuard g(logits.device());
+  const c10::DeviceGuard g(logits.device());
   const int64_t t = logits.size(0);
   auto opts = logits.options().dtype(at::kFloat);
   auto m = at::empty({t}, opts), s = at::empty({t}, opts), xl = at::empty({t}, opts);
@@ -193,7 +193,7 @@ void ce_grad_(const at::Tensor& logits, const at::Tensor& labels, const at::Tens
   check_logits(logits, labels);
   DTG_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == logits.size(0),
             "ce_grad_: lse must be f32 [t]");
-  c10::hip::HIPGuard g(logits.device());
+  const c10::DeviceGuard g(logits.device());
   const int64_t t = logits.size(0);
   if (t == 0) return;
   ce_grad_kernel<<<t, kCeThreads, 0, stream()>>>(bf16_mut(logits), logits.stride(0), logits.size(1),

@@ -1,0 +1,49 @@
+"""HF text pipeline: tokenize -> group into seq_length blocks -> labels.
+
+Semantics follow the reference's `_load_and_preprocess_data`: tokenize the `text` column (or the
+first column), concatenate and chunk into `seq_length` blocks (dropping the remainder), labels =
+input_ids, and `seq_length = args.seq_length or tokenizer.model_max_length` clamped to
+min(1024, max_position_embeddings) when too long.  It needs the dataset and tokenizer to be
+available locally (HF cache or a path); on the offline GPU boxes the synthetic datasets are
+used instead (`--dataset-name synthetic` / `synthetic:packed`).
+"""
+from __future__ import annotations
+
+import os
+from itertools import chain
+
+
+def load_and_preprocess(dataset_name: str, tokenizer_name: str, seq_length, max_position_embeddings: int,
+                        num_proc: int | None = None):
+    import datasets
+    from transformers import AutoTokenizer
+
+    tok = AutoTokenizer.from_pretrained(tokenizer_name)
+    data = datasets.load_dataset(dataset_name, trust_remote_code=True)
+    split = data["train"]
+    column_names = split.column_names
+    text_column = "text" if "text" in column_names else column_names[0]
+    num_proc = num_proc or os.cpu_count()
+
+    def tokenize(ex):
+        return tok(ex[text_column])
+
+    tokenized = split.map(tokenize, batched=True, remove_columns=column_names, num_proc=num_proc,
+                          desc="Running tokenizer on dataset")
+    if seq_length is None:
+        seq_length = tok.model_max_length
+        if seq_length > max_position_embeddings:
+            seq_length = min(1024, max_position_embeddings)
+
+    def group_texts(examples):
+        concatenated = {k: list(chain(*examples[k])) for k in examples.keys()}
+        total = len(concatenated[list(examples.keys())[0]])
+        if total > seq_length:
+            total = (total // seq_length) * seq_length
+        result = {k: [t[i:i + seq_length] for i in range(0, total, seq_length)] for k, t in concatenated.items()}
+        result["labels"] = result["input_ids"].copy()
+        return result
+
+    grouped = tokenized.map(group_texts, batched=True, num_proc=num_proc, desc=f"Grouping texts in chunks of {seq_length}")
+    grouped = grouped.remove_columns([c for c in grouped.column_names if c not in ("input_ids", "labels")])
+    return grouped.with_format("torch"), seq_length
