@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--lr", type=float, default=3e-5)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
+    ap.add_argument("--tunableop", choices=["off", "use", "tune"], default="use",
+                    help="PyTorch TunableOp for the hipBLASLt GEMMs: 'use' loads the committed per-shape "
+                         "solution table (tunableop/), 'tune' benchmarks new shapes during warmup and writes it")
     return ap.parse_args()
 
 
@@ -48,6 +51,10 @@ def main():
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
 
+    if args.tunableop != "off" and torch.cuda.is_available():
+        from dtg.utils.gemm_tuning import enable_tunableop
+
+        enable_tunableop(tune=args.tunableop == "tune")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -101,6 +108,10 @@ def main():
         loss = step(args.warmup + i)
     sync()
     elapsed = time.perf_counter() - t0
+    if args.tunableop == "tune" and cuda and rank == 0:
+        from dtg.utils.gemm_tuning import save_tunableop
+
+        save_tunableop()
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)

@@ -128,14 +128,25 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
   }
 }
 
-// Column sums of an [nrows, H] f32 matrix -> bf16 [H]; one thread per column, coalesced rows.
-__global__ void colsum_to_bf16_kernel(const float* __restrict__ part, int nrows, int H,
-                                      uint16_t* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= H) return;
+// Column sums of an [nrows, H] f32 matrix -> bf16 [H].  A workgroup owns 32 columns; its 8
+// row-groups of 32 lanes read 128-B row segments (coalesced) and are combined through LDS,
+// so the reduction spreads over H/32 workgroups instead of H serial threads.
+__global__ __launch_bounds__(256) void colsum_to_bf16_kernel(const float* __restrict__ part, int nrows, int H,
+                                                             uint16_t* __restrict__ out) {
+  __shared__ float red[8][33];
+  const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + lane;
   float s = 0.f;
-  for (int r = 0; r < nrows; ++r) s += part[(int64_t)r * H + c];
-  out[c] = f2bf(s);
+  if (c < H)
+    for (int r = grp; r < nrows; r += 8) s += part[(int64_t)r * H + c];
+  red[grp][lane] = s;
+  __syncthreads();
+  if (grp == 0 && c < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][lane];
+    out[c] = f2bf(t);
+  }
 }
 
 static int pick_per(int H) {
@@ -240,8 +251,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy_, const at::
                               part.data_ptr<float>(), T, H, rpb));
   }
   DTG_LAUNCH_CHECK();
-  colsum_to_bf16_kernel<<<(H + 255) / 256, 256, 0, stream()>>>(part.data_ptr<float>(), nb, H,
-                                                               bf16_mut(dw));
+  colsum_to_bf16_kernel<<<(H + 31) / 32, 256, 0, stream()>>>(part.data_ptr<float>(), nb, H, bf16_mut(dw));
   DTG_LAUNCH_CHECK();
   return {dx, dw};
 }

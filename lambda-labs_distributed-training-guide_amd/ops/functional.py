@@ -10,6 +10,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
+from . import grad_routing as _gr
 from .grad_routing import route_embedding_grad, route_param_grad, route_weight_grad_mm
 
 ops = torch.ops.dtg
@@ -233,7 +234,10 @@ class _FusedLinearCE(torch.autograd.Function):
         scale = 1.0 / max(num_valid, 1)
         loss_sum = torch.zeros((), dtype=torch.float32, device=h.device)
         dh = torch.empty_like(h) if need else None
-        dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if (need and ctx.needs_input_grad[1]) else None
+        want_dw = need and ctx.needs_input_grad[1]
+        # direct: dW goes straight into w.main_grad now (engine-owned loss, grad_output == 1)
+        direct = want_dw and _gr.direct_loss_grad() and getattr(w, "main_grad", None) is not None
+        dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if (want_dw and not direct) else None
         for s in range(0, T, chunk):
             e = min(T, s + chunk)
             logits = torch.mm(h[s:e], w.t())
@@ -241,7 +245,9 @@ class _FusedLinearCE(torch.autograd.Function):
             loss_sum += rows.sum()
             if need:
                 torch.mm(logits, w, out=dh[s:e])
-                if dw is not None:
+                if direct:
+                    _gr.accumulate_mm_into_main_grad(w, logits, h[s:e])
+                elif dw is not None:
                     # f32 accumulate inside the GEMM, one bf16 rounding per chunk
                     if s == 0:
                         torch.mm(logits.t(), h[s:e], out=dw)
@@ -249,12 +255,16 @@ class _FusedLinearCE(torch.autograd.Function):
                         dw.addmm_(logits.t(), h[s:e])
         ctx.save_for_backward(dh, dw)
         ctx.w = w
+        ctx.direct = direct
         return loss_sum * scale
 
     @staticmethod
     def backward(ctx, go):
         dh, dw = ctx.saved_tensors
         w = ctx.w
+        if ctx.direct:
+            _gr.notify_param(w)
+            return dh, None, None, None, None, None
         gdh = (dh * go.to(dh.dtype)) if ctx.needs_input_grad[0] else None
         gdw = route_param_grad(w, dw * go.to(dw.dtype)) if dw is not None else None
         return gdh, gdw, None, None, None, None

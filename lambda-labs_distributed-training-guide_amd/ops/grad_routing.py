@@ -9,6 +9,21 @@ None to autograd.  Parameters without `main_grad` get an ordinary gradient.
 """
 import torch
 
+# When an engine owns the loss (it back-propagates the loss with an implicit gradient of 1 and
+# folds any scaling into the optimizer's grad_scale), the fused loss head writes the lm_head
+# weight gradient straight into main_grad during its forward pass and skips the grad_output
+# multiply in backward: no temporary [V, H] buffer and no extra passes over it.
+_DIRECT_LOSS_GRAD = False
+
+
+def set_direct_loss_grad(enabled: bool):
+    global _DIRECT_LOSS_GRAD
+    _DIRECT_LOSS_GRAD = bool(enabled)
+
+
+def direct_loss_grad() -> bool:
+    return _DIRECT_LOSS_GRAD
+
 
 def _fresh(param) -> bool:
     return not getattr(param, "_dtg_grad_written", False)
@@ -32,6 +47,23 @@ def route_param_grad(param, grad):
         mg.add_(grad.view_as(mg))
     _mark(param)
     return None
+
+
+def accumulate_mm_into_main_grad(param, a, b) -> bool:
+    """main_grad (+)= a^T @ b without notifying (used by the fused loss head's forward)."""
+    mg = getattr(param, "main_grad", None)
+    if mg is None:
+        return False
+    if _fresh(param):
+        torch.mm(a.t(), b, out=mg)
+        param._dtg_grad_written = True
+    else:
+        mg.addmm_(a.t(), b)
+    return True
+
+
+def notify_param(param):
+    _mark(param)
 
 
 def route_weight_grad_mm(param, a, b):

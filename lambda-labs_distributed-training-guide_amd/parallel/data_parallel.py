@@ -25,7 +25,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.adamw import adamw_step
-from ..ops.grad_routing import reset_grad_state
+from ..ops.grad_routing import reset_grad_state, set_direct_loss_grad
 from ..utils import comm
 from .flat import FlatSpace, rebind_parameters
 
@@ -46,7 +46,7 @@ class DataParallel:
         for n, p in named:
             p._dtg_name = n
         self.space = FlatSpace(named, dev, world=self.world if self.mode == "zero" else 1,
-                               bucket_bytes=bucket_mb << 20)
+                               bucket_bytes=bucket_mb << 20, dtype=named[0][1].dtype)
         self.params = rebind_parameters(model, self.space, copy_data=True, notify=self._on_grad)
         self._sync_enabled = True
         self._inflight = []
@@ -73,6 +73,9 @@ class DataParallel:
             self._shard_param_copy(self.master)
         self.step_count = 0
         self.accum_count = 0  # micro-batches accumulated since the last step
+        # The engine owns the loss: backward(loss) uses an implicit gradient of 1 and any
+        # scaling goes into AdamW's grad_scale, which lets the loss head write dW in place.
+        set_direct_loss_grad(True)
 
     # ------------------------------------------------------------------ grad sync
     @contextlib.contextmanager

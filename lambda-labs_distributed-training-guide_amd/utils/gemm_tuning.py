@@ -1,0 +1,31 @@
+"""hipBLASLt GEMM solution selection via PyTorch TunableOp.
+
+Plain library GEMMs (every Linear of the model) run through hipBLASLt.  Its default
+heuristic picks a reasonable but not always the fastest kernel for the Llama shapes, so the
+per-shape winners are measured once on an MI355X with TunableOp and committed as
+`tunableop/tunableop_results.csv`; later runs load that table (no tuning cost), and only tune
+shapes it does not contain when asked to (`tune=True`).
+"""
+import os
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+TABLE = os.path.join(ROOT, "tunableop", "tunableop_results.csv")
+
+
+def enable_tunableop(tune: bool = False, max_tuning_ms: int = 30, table: str = TABLE):
+    os.makedirs(os.path.dirname(table), exist_ok=True)
+    t = torch.cuda.tunable
+    t.enable(True)
+    t.set_filename(table, insert_device_ordinal=False)
+    t.tuning_enable(tune)
+    if tune:
+        t.set_max_tuning_duration(max_tuning_ms)
+        t.set_max_tuning_iterations(50)
+    if os.path.exists(table):
+        t.read_file(table)
+
+
+def save_tunableop(table: str = TABLE):
+    torch.cuda.tunable.write_file(table)
