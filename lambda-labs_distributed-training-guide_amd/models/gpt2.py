@@ -101,20 +101,23 @@ class GPT2LMHeadModel(nn.Module):
         return self.h
 
     @torch.no_grad()
-    def init_weights(self, std=None):
-        std = self.config.initializer_range if std is None else std
-        proj_std = std / math.sqrt(2 * self.config.n_layer)
+    def init_param(self, name: str, p: torch.Tensor):
+        """HF GPT-2 init: normal(0, 0.02), residual projections scaled by 1/sqrt(2 n_layer)."""
+        std = self.config.initializer_range
+        if ".ln_" in name or name.startswith("ln_f"):
+            p.fill_(1.0 if name.endswith("weight") else 0.0)
+        elif name.endswith("bias"):
+            p.zero_()
+        elif name.endswith("c_proj.weight") or name.endswith("mlp_proj.weight"):
+            p.normal_(0.0, std / math.sqrt(2 * self.config.n_layer))
+        else:
+            p.normal_(0.0, std)
+
+    @torch.no_grad()
+    def init_weights(self):
         for name, p in self.named_parameters():
-            if p.device.type == "meta":
-                continue
-            if ".ln_" in name or name.startswith("ln_f"):
-                p.fill_(1.0 if name.endswith("weight") else 0.0)
-            elif name.endswith("bias"):
-                p.zero_()
-            elif name.endswith("c_proj.weight") or name.endswith("mlp_proj.weight"):
-                p.normal_(0.0, proj_std)
-            else:
-                p.normal_(0.0, std)
+            if p.device.type != "meta":
+                self.init_param(name, p)
 
     def lm_head_weight(self):
         return self.wte.weight

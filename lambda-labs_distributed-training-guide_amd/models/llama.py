@@ -37,6 +37,8 @@ class CausalLMOutput:
 class Weight(nn.Module):
     """Parameter holder (no forward); keeps HF-like `<name>.weight` state-dict keys."""
 
+    _dtg_param_holder = True
+
     def __init__(self, *shape, device=None, dtype=torch.bfloat16):
         super().__init__()
         self.weight = nn.Parameter(torch.empty(*shape, device=device, dtype=dtype))
@@ -169,15 +171,18 @@ class LlamaForCausalLM(nn.Module):
 
     # ---------------------------------------------------------------- init
     @torch.no_grad()
-    def init_weights(self, std: Optional[float] = None):
-        std = self.config.initializer_range if std is None else std
+    def init_param(self, name: str, t: torch.Tensor):
+        """HF Llama init: normal(0, initializer_range) for matrices/embeddings, ones for norms."""
+        if name.endswith("layernorm.weight") or name == "norm.weight":
+            t.fill_(1.0)
+        else:
+            t.normal_(0.0, self.config.initializer_range)
+
+    @torch.no_grad()
+    def init_weights(self):
         for name, p in self.named_parameters():
-            if p.device.type == "meta":
-                continue
-            if name.endswith("layernorm.weight") or name == "norm.weight":
-                p.fill_(1.0)
-            else:
-                p.normal_(0.0, std)
+            if p.device.type != "meta":
+                self.init_param(name, p)
 
     def lm_head_weight(self):
         return self.embed_tokens.weight if self.lm_head is None else self.lm_head.weight

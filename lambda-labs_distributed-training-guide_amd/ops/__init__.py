@@ -11,6 +11,9 @@ from . import _cpu  # noqa: F401  (CPU implementations)
 from . import _native
 
 _native.load()
+if not _native.LOADED:  # CPU-only box without a build: host AdamW falls back to the f32 reference
+    _schema.LIB.impl("adamw_cpu_", lambda p, g, m, v, lr, b1, b2, eps, wd, step, gs: _cpu.adamw_(
+        p, None, g, m, v, lr, b1, b2, eps, wd, step, gs), "CPU")
 
 from .functional import (  # noqa: E402
     add_rms_norm,

@@ -11,3 +11,9 @@ def adamw_step(p, g, m, v, *, lr, step, beta1=0.9, beta2=0.999, eps=1e-8, weight
     gradient-accumulation division, clipping) so no separate scaling pass is needed."""
     torch.ops.dtg.adamw_(p, master, g, m, v, float(lr), float(beta1), float(beta2), float(eps),
                          float(weight_decay), int(step), float(grad_scale))
+
+
+def adamw_step_cpu(p, g, m, v, *, lr, step, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, grad_scale=1.0):
+    """Host AdamW on pinned CPU shards (FSDP CPU offload): native OpenMP C++ kernel."""
+    torch.ops.dtg.adamw_cpu_(p, g, m, v, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+                             int(step), float(grad_scale))

@@ -1,0 +1,511 @@
+"""Fully-sharded data parallel (ZeRO-3) engine over flat per-unit buffers.
+
+Design (MI355X-first, not a wrapper around torch FSDP):
+  * A *unit* is a group of modules whose parameters are gathered together: one per decoder
+    layer (`policy="transformer"`, the 405B chapter's transformer wrap + Embedding), or greedy
+    post-order groups of >= `min_num_params` (`policy="size"`, the `--numel-to-wrap` policy of
+    chapter 04).  Everything else belongs to the root unit.
+  * Each unit owns one flat bf16 buffer laid out like `FlatSpace` (padded to world*16), so its
+    all-gather is ONE `all_gather_into_tensor` (RCCL) into a full buffer whose storage is
+    resized to 0 after use (saved autograd views stay valid: the same storage is refilled by
+    the next gather); its gradient reduce-scatter is ONE `reduce_scatter_tensor`.
+  * Forward: pre-hook waits for the unit's gather, then prefetches the next unit's gather
+    (overlaps with compute); post-hook reshards (`reshard_after_forward`) and inserts a
+    pre-backward node on the outputs.  Backward: that node re-gathers the unit and prefetches
+    the previous one; once every parameter gradient of the unit is written (notification from
+    the kernels' gradient routing) the unit's reduce-scatter is launched asynchronously.
+  * All shards live in one flat "shard space" per rank: the fused AdamW runs once over it.
+  * Sharding for 288 GB HBM3E: default keeps params resharded after forward (ZeRO-3); with
+    `reshard_after_forward=False` the gathered units stay resident until backward (ZeRO-2-like
+    traffic, 2/3 of the all-gathers) when memory allows.
+  * `cpu_offload=True` keeps parameter shards, gradient shards and optimizer state in pinned
+    host memory and runs the native C++ AdamW on the CPU (chapter 05).
+  * Meta-device init: units are materialised one at a time on the GPU, initialised with the
+    same seed on every rank, and only the local shard is kept (peak = one unit).
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+from collections import deque
+from typing import Callable, Dict, Iterable, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops.adamw import adamw_step
+from ..ops.grad_routing import reset_grad_state, set_direct_loss_grad
+from ..utils import comm
+
+ALIGN = 16
+
+
+def _round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+def transformer_units(model: nn.Module) -> List[nn.Module]:
+    """One unit per decoder layer (the reference's transformer wrap policy); the embedding,
+    final norm and lm_head form the root unit, gathered for the whole step (they are needed at
+    both ends of forward and backward, so a separate embedding unit would only be re-gathered)."""
+    return list(model.layers)
+
+
+def _callable_unit(m: nn.Module) -> bool:
+    # parameter holders (models.llama.Weight) are never called, so forward hooks cannot gather
+    # them: their parameters belong to the enclosing unit instead.
+    return not getattr(m, "_dtg_param_holder", False)
+
+
+def size_based_units(model: nn.Module, min_num_params: int) -> List[nn.Module]:
+    """Post-order greedy wrap like torch's size_based_auto_wrap_policy: a module becomes a unit
+    when its not-yet-wrapped parameters number >= min_num_params."""
+    units: List[nn.Module] = []
+    wrapped = set()
+
+    def visit(m: nn.Module) -> int:
+        n = 0
+        for c in m.children():
+            n += visit(c)
+        own = sum(p.numel() for p in m.parameters(recurse=False) if id(p) not in wrapped)
+        n += own
+        if m is not model and n >= min_num_params and _callable_unit(m):
+            units.append(m)
+            for p in m.parameters():
+                wrapped.add(id(p))
+            return 0
+        return n
+
+    visit(model)
+    return units
+
+
+class _Unit:
+    def __init__(self, engine: "FullyShard", idx: int, module: nn.Module, named: Sequence, is_root: bool):
+        self.engine, self.idx, self.module, self.is_root = engine, idx, module, is_root
+        self.names = [n for n, _ in named]
+        self.params_src = [p for _, p in named]
+        self.shapes = [tuple(p.shape) for p in self.params_src]
+        W = engine.world
+        offs, cur = [], 0
+        for p in self.params_src:
+            offs.append(cur)
+            cur += _round_up(p.numel(), ALIGN)
+        self.offsets = offs
+        self.numel = _round_up(max(cur, 1), W * ALIGN)
+        self.shard_numel = self.numel // W
+        self.expected = sum(getattr(p, "_dtg_uses", 1) for p in self.params_src)
+        self.pending = self.expected
+        self.full: Optional[torch.Tensor] = None  # full param buffer (storage resized to 0 when sharded)
+        self.gathered = False
+        self.gather_work = None
+        self.full_grad: Optional[torch.Tensor] = None
+        self.params: List[nn.Parameter] = []
+        self.in_backward = False
+        self.rs_launched = False
+
+
+class _PreBackward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, unit, *xs):
+        ctx.unit = unit
+        ys = tuple(x.view_as(x) for x in xs)
+        return ys if len(ys) > 1 else ys[0]
+
+    @staticmethod
+    def backward(ctx, *gs):
+        ctx.unit.engine._pre_backward(ctx.unit)
+        return (None,) + gs
+
+
+class FullyShard:
+    def __init__(self, model: nn.Module, group=None, policy: str = "transformer", min_num_params: int = 100_000_000,
+                 device=None, reshard_after_forward: bool = True, cpu_offload: bool = False,
+                 state_dtype=torch.bfloat16, init_fn: Optional[Callable] = None, seed: int = 0,
+                 prefetch: bool = True, max_inflight_rs: int = 2):
+        self.module = model
+        self.group = group
+        self.world = comm.world(group) if dist.is_initialized() else 1
+        self.rank = comm.rank(group) if self.world > 1 else 0
+        self.mode = "fsdp"
+        self.reshard_after_forward = reshard_after_forward
+        self.cpu_offload = cpu_offload
+        self.prefetch = prefetch
+        self.max_inflight_rs = max_inflight_rs
+        p0 = next(model.parameters())
+        self.dtype = p0.dtype if p0.dtype.is_floating_point else torch.bfloat16
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+        self.device = torch.device(device)
+        # ---- units
+        mods = transformer_units(model) if policy == "transformer" else size_based_units(model, min_num_params)
+        seen = set()
+        unit_named = []
+        qual = {id(p): n for n, p in model.named_parameters()}
+        for m in mods:
+            named = [(qual[id(p)], p) for _, p in m.named_parameters() if id(p) not in seen and p.requires_grad]
+            for _, p in named:
+                seen.add(id(p))
+            if named:
+                unit_named.append((m, named))
+        root_named = [(n, p) for n, p in model.named_parameters() if id(p) not in seen and p.requires_grad]
+        self.units: List[_Unit] = []
+        for i, (m, named) in enumerate(unit_named):
+            self.units.append(_Unit(self, i, m, named, False))
+        self.root = _Unit(self, len(self.units), model, root_named, True) if root_named else None
+        all_units = self.units + ([self.root] if self.root is not None else [])
+        # ---- one shard space for all units (single fused AdamW launch)
+        total = sum(u.shard_numel for u in all_units)
+        home = torch.device("cpu") if cpu_offload else self.device
+        pin = cpu_offload and torch.cuda.is_available()
+        self.shard_params = torch.zeros(total, dtype=self.dtype, device=home, pin_memory=pin)
+        self.shard_grads = torch.zeros(total, dtype=self.dtype, device=home, pin_memory=pin)
+        self.exp_avg = torch.zeros(total, dtype=state_dtype, device=home)
+        self.exp_avg_sq = torch.zeros(total, dtype=state_dtype, device=home)
+        o = 0
+        for u in all_units:
+            u.shard_off = o
+            o += u.shard_numel
+        self.all_units = all_units
+        # ---- materialise params: full buffers per unit, shard extraction, param rebinding
+        where = {}
+        for mn, mm in model.named_modules():
+            for pn, p in mm._parameters.items():
+                if p is not None:
+                    where.setdefault(id(p), []).append((mm, pn))
+        init_fn = init_fn or getattr(model, "init_param", None) or _default_init(model)
+        for u in all_units:
+            full = torch.zeros(u.numel, dtype=self.dtype, device=self.device)
+            u.full = full
+            new = []
+            for i, src in enumerate(u.params_src):
+                n = math.prod(u.shapes[i])
+                view = full[u.offsets[i]:u.offsets[i] + n].view(u.shapes[i])
+                if src.device.type == "meta":
+                    torch.manual_seed(seed + 7919 * u.idx + i)
+                    init_fn(u.names[i], view)
+                else:
+                    with torch.no_grad():
+                        view.copy_(src.detach())
+                np_ = nn.Parameter(view, requires_grad=src.requires_grad)
+                for attr in ("_dtg_sequence_parallel", "_dtg_uses"):
+                    if hasattr(src, attr):
+                        setattr(np_, attr, getattr(src, attr))
+                np_._dtg_unit = u
+                np_._dtg_notify = self._on_grad
+                np_.register_post_accumulate_grad_hook(_post_accumulate)
+                for mm, pn in where.get(id(src), []):
+                    mm._parameters[pn] = np_
+                new.append(np_)
+            u.params = new
+            if self.world > 1 and all(p.device.type != "meta" for p in u.params_src):
+                # identical init on every rank is assumed; keep rank 0 authoritative (sync_module_states)
+                dist.broadcast(full, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+            my = full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel]
+            self.shard_params[u.shard_off:u.shard_off + u.shard_numel].copy_(my)
+            u.params_src = None
+            self._free_full(u)
+        # ---- hooks
+        for u in self.units:
+            u.module.register_forward_pre_hook(self._make_pre_forward(u))
+            u.module.register_forward_hook(self._make_post_forward(u))
+        model.register_forward_pre_hook(self._root_pre_forward)
+        if self.root is not None:
+            model.register_forward_hook(self._root_post_forward)
+        self._rs_inflight = deque()
+        self._order: List[_Unit] = []  # forward execution order (recorded on the first step)
+        self._record_order = True
+        self.step_count = 0
+        self.accum_count = 0
+        self._sync_enabled = True
+        self._first_micro = True
+        set_direct_loss_grad(True)
+
+    # ------------------------------------------------------------------ memory helpers
+    def _shard_view(self, u: _Unit, buf: torch.Tensor) -> torch.Tensor:
+        return buf[u.shard_off:u.shard_off + u.shard_numel]
+
+    def _free_full(self, u: _Unit):
+        if u.full is not None and u.full.untyped_storage().size() > 0:
+            u.full.untyped_storage().resize_(0)
+        u.gathered = False
+
+    def _alloc_full(self, u: _Unit):
+        st = u.full.untyped_storage()
+        if st.size() == 0:
+            st.resize_(u.numel * u.full.element_size())
+
+    # ------------------------------------------------------------------ gather / reshard
+    def _issue_gather(self, u: _Unit):
+        if u.gathered or u.gather_work is not None:
+            return
+        self._alloc_full(u)
+        shard = self._shard_view(u, self.shard_params)
+        if self.cpu_offload:
+            shard = shard.to(self.device, non_blocking=True)
+        with torch.autograd._unsafe_preserve_version_counter(u.full):
+            if self.world == 1:
+                u.full.copy_(shard)
+                u.gather_work = None
+                u.gathered = True
+                return
+            if comm.backend_of(self.group) == "gloo":
+                dist.all_gather_into_tensor(u.full, shard.contiguous(), group=self.group)
+                u.gathered = True
+                return
+            u.gather_work = dist.all_gather_into_tensor(u.full, shard, group=self.group, async_op=True)
+        u._gather_src = shard  # keep the (H2D) source alive until the gather completes
+
+    def _wait_gather(self, u: _Unit):
+        self._issue_gather(u)
+        if u.gather_work is not None:
+            u.gather_work.wait()
+            u.gather_work = None
+            u.gathered = True
+        u._gather_src = None
+
+    def _reshard(self, u: _Unit):
+        if u.gather_work is not None:
+            u.gather_work.wait()
+            u.gather_work = None
+        self._free_full(u)
+
+    # ------------------------------------------------------------------ forward hooks
+    def _root_pre_forward(self, module, args, kwargs=None):
+        if self.root is not None:
+            self._wait_gather(self.root)
+            self.root.in_backward = False
+            if torch.is_grad_enabled():
+                self._prepare_grads(self.root)
+        if self.prefetch and self._order and not self._record_order:
+            self._issue_gather(self._order[0])
+
+    def _root_post_forward(self, module, args, out):
+        self._record_order = False
+        return out
+
+    def _make_pre_forward(self, u: _Unit):
+        def hook(module, args):
+            self._wait_gather(u)
+            if u.in_backward:  # activation-checkpoint recompute inside backward
+                return None
+            if self._record_order:
+                self._order.append(u)
+            elif self.prefetch:
+                k = self._order.index(u) if u in self._order else -1
+                if 0 <= k < len(self._order) - 1:
+                    self._issue_gather(self._order[k + 1])
+            return None
+
+        return hook
+
+    def _make_post_forward(self, u: _Unit):
+        def hook(module, args, out):
+            if u.in_backward or not torch.is_grad_enabled():
+                return out
+            if self.reshard_after_forward:
+                self._reshard(u)
+            flat, rebuild = _flatten_out(out)
+            if not any(t.requires_grad for t in flat):
+                return out
+            new = _PreBackward.apply(u, *flat)
+            new = new if isinstance(new, tuple) else (new,)
+            return rebuild(list(new))
+
+        return hook
+
+    # ------------------------------------------------------------------ backward
+    def _pre_backward(self, u: _Unit):
+        if u.in_backward:
+            return
+        u.in_backward = True
+        self._wait_gather(u)
+        self._prepare_grads(u)
+        if self.prefetch and u in self._order:
+            k = self._order.index(u)
+            if k > 0:
+                self._issue_gather(self._order[k - 1])
+
+    def _prepare_grads(self, u: _Unit):
+        if u.full_grad is not None:
+            return
+        u.full_grad = torch.empty(u.numel, dtype=self.dtype, device=self.device)
+        for i, p in enumerate(u.params):
+            n = math.prod(u.shapes[i])
+            p.main_grad = u.full_grad[u.offsets[i]:u.offsets[i] + n].view(u.shapes[i])
+        u.pending = u.expected
+        u.rs_launched = False
+
+    def _on_grad(self, p):
+        u = p._dtg_unit
+        if getattr(p, "_dtg_sequence_parallel", False) and getattr(self, "tp_group", None) is not None:
+            dist.all_reduce(p.main_grad, group=self.tp_group)
+        u.pending -= 1
+        if u.pending == 0:
+            self._launch_rs(u)
+
+    def _launch_rs(self, u: _Unit):
+        if u.rs_launched:
+            return
+        u.rs_launched = True
+        # zero the padding / never-written params so the reduce-scatter sums only real grads
+        for i, p in enumerate(u.params):
+            if not getattr(p, "_dtg_grad_written", False):
+                p.main_grad.zero_()
+        end = u.offsets[-1] + math.prod(u.shapes[-1]) if u.params else 0
+        if end < u.numel:
+            u.full_grad[end:].zero_()
+        gs = self._shard_view(u, self.shard_grads)
+        first = self._first_micro
+        direct = not (self.cpu_offload or not first)  # reduce-scatter straight into the grad shard
+        out = gs if direct else torch.empty(u.shard_numel, dtype=self.dtype, device=self.device)
+        if self.world == 1:
+            out.copy_(u.full_grad)
+            work = None
+        else:
+            work = comm.reduce_scatter_into(out, u.full_grad, group=self.group, async_op=True)
+        self._rs_inflight.append((u, work, out, first, direct))
+        if not u.is_root and self.reshard_after_forward:
+            self._reshard(u)
+        while len(self._rs_inflight) > self.max_inflight_rs:
+            self._complete_rs(*self._rs_inflight.popleft())
+
+    def _complete_rs(self, u, work, out, first, direct):
+        if work is not None:
+            work.wait()
+        if not direct:
+            gs = self._shard_view(u, self.shard_grads)
+            if first:
+                gs.copy_(out)
+            else:
+                gs.add_(out.to(gs.device))
+        u.full_grad = None
+        for p in u.params:
+            p.main_grad = None
+
+    def finish_grad_sync(self):
+        for u in self.all_units:
+            if u.full_grad is not None and not u.rs_launched:
+                self._launch_rs(u)
+        while self._rs_inflight:
+            self._complete_rs(*self._rs_inflight.popleft())
+        # every unit is resharded: the optimizer updates the shards, so a full buffer kept from
+        # this step would be stale in the next forward
+        for u in self.all_units:
+            u.in_backward = False
+            self._reshard(u)
+        self._first_micro = False
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation: FSDP still reduce-scatters each micro-batch (memory stays
+        sharded) and accumulates into the gradient shard; this context only defers nothing
+        and exists for API parity with DataParallel."""
+        yield
+
+    def backward(self, loss):
+        loss.backward()
+        self.accum_count += 1
+        self.finish_grad_sync()
+
+    def zero_grad(self):
+        for u in self.all_units:
+            reset_grad_state(u.params)
+            u.pending = u.expected
+        self.accum_count = 0
+        self._first_micro = True
+
+    # ------------------------------------------------------------------ optimizer
+    def step(self, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, grad_scale=None):
+        self.step_count += 1
+        if grad_scale is None:
+            grad_scale = 1.0 / (self.world * max(1, self.accum_count))
+        if self.cpu_offload:
+            from ..ops.adamw import adamw_step_cpu
+
+            adamw_step_cpu(self.shard_params, self.shard_grads, self.exp_avg, self.exp_avg_sq, lr=lr,
+                           step=self.step_count, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
+                           grad_scale=grad_scale)
+        else:
+            adamw_step(self.shard_params, self.shard_grads, self.exp_avg, self.exp_avg_sq, lr=lr, step=self.step_count,
+                       beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale)
+
+    # ------------------------------------------------------------------ state
+    def optimizer_state(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "mode": "fsdp", "world": self.world, "rank": self.rank}
+
+    def load_optimizer_state(self, st):
+        assert st["world"] == self.world, "optimizer state layout mismatch"
+        self.step_count = int(st["step"])
+        self.exp_avg.copy_(st["exp_avg"])
+        self.exp_avg_sq.copy_(st["exp_avg_sq"])
+
+    def sharded_param_items(self):
+        """(unit, name, shard-local slice info) for sharded checkpoints: yields
+        (qualified_name, full_shape, flat_start_in_unit, numel, unit)."""
+        for u in self.all_units:
+            prefix = ""
+            for i, n in enumerate(u.names):
+                yield n, u.shapes[i], u.offsets[i], math.prod(u.shapes[i]), u
+
+    @torch.no_grad()
+    def full_state_dict(self, rank0_only: bool = True) -> Dict[str, torch.Tensor]:
+        """Gather every unit and return the full (CPU) state dict, names as in model.state_dict()."""
+        out = {}
+        qual = {id(p): n for n, p in self.module.named_parameters()}
+        for u in self.all_units:
+            self._wait_gather(u)
+            for p in u.params:
+                if (not rank0_only) or self.rank == 0:
+                    out[qual[id(p)]] = p.detach().cpu().clone()
+            self._reshard(u)
+        return out
+
+
+def _flatten_out(out):
+    if isinstance(out, torch.Tensor):
+        return [out], lambda xs: xs[0]
+    if isinstance(out, tuple) and all(isinstance(t, torch.Tensor) for t in out):
+        return list(out), lambda xs: tuple(xs)
+    if isinstance(out, tuple):
+        idx = [i for i, t in enumerate(out) if isinstance(t, torch.Tensor)]
+
+        def rebuild(xs):
+            lst = list(out)
+            for i, x in zip(idx, xs):
+                lst[i] = x
+            return tuple(lst)
+
+        return [out[i] for i in idx], rebuild
+    return [], lambda xs: out
+
+
+def _post_accumulate(p):
+    if p.grad is None:
+        return
+    from ..ops.grad_routing import route_param_grad
+
+    g = p.grad
+    p.grad = None
+    route_param_grad(p, g)
+
+
+def _default_init(model):
+    cfg = getattr(model, "config", None)
+    std = getattr(cfg, "initializer_range", 0.02)
+
+    def init(name, t):
+        with torch.no_grad():
+            if name.endswith("layernorm.weight") or name.endswith("norm.weight") or ".ln_" in name or name.startswith("ln_"):
+                if name.endswith("bias"):
+                    t.zero_()
+                else:
+                    t.fill_(1.0)
+            elif name.endswith("bias"):
+                t.zero_()
+            else:
+                t.normal_(0.0, std)
+
+    return init

@@ -1,0 +1,90 @@
+"""T2/T3: the FSDP (ZeRO-3) engine on gloo reproduces single-process training; policies,
+meta-device init, activation checkpointing and CPU offload."""
+import pytest
+import torch
+
+import dtg  # noqa: F401
+
+from _dist import run_distributed
+from test_engines_cpu import _batches, _train
+
+TOL = dict(atol=3e-4, rtol=1e-3)
+
+
+def _fsdp_train(rank, world, model_name, batches, policy, min_params, reshard, ac, offload):
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+    from dtg.parallel.checkpointing import apply_activation_checkpointing
+
+    torch.manual_seed(0)
+    model = build_model(model_name, device="cpu", dtype=torch.float32)
+    if ac:
+        apply_activation_checkpointing(model)
+    eng = FullyShard(model, policy=policy, min_num_params=min_params, reshard_after_forward=reshard,
+                     cpu_offload=offload, device="cpu")
+    opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
+    for ids in batches:
+        per = ids.shape[0] // world
+        mine = ids[rank * per:(rank + 1) * per]
+        opt.zero_grad()
+        out = model(input_ids=mine, labels=mine)
+        eng.backward(out.loss)
+        opt.step()
+    sd = eng.full_state_dict(rank0_only=False)
+    return sd, len(eng.units)
+
+
+@pytest.mark.parametrize("model_name,policy,min_params,reshard,ac", [
+    ("llama-tiny", "transformer", 0, True, False),
+    ("llama-tiny", "size", 100_000, True, False),
+    ("llama-tiny", "transformer", 0, False, True),
+    ("gpt2-tiny", "transformer", 0, True, True),
+])
+def test_fsdp_matches_single(model_name, policy, min_params, reshard, ac):
+    batches = _batches(512, 4, 32)
+    ref, _ = _train(model_name, "single", 0, 1, batches)
+    res = run_distributed(_fsdp_train, 2, model_name, batches, policy, min_params, reshard, ac, False)
+    for r in range(2):
+        sd, nunits = res[r]
+        assert nunits >= 1
+        for n in ref:
+            torch.testing.assert_close(sd[n], ref[n], **TOL, msg=f"rank {r} {n}")
+
+
+def test_fsdp_world1_cpu_offload_and_meta_init():
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+
+    batches = _batches(512, 2, 16)
+    ref, _ = _train("llama-tiny", "single", 0, 1, batches)
+    sd, _ = _fsdp_train(0, 1, "llama-tiny", batches, "transformer", 0, True, False, True)
+    for n in ref:
+        torch.testing.assert_close(sd[n], ref[n], **TOL, msg=n)
+    # meta-device construction: only shards are materialised, init is seeded per unit
+    with torch.device("meta"):
+        m = build_model("llama-tiny", dtype=torch.float32, init=False)
+    eng = FullyShard(m, device="cpu")
+    opt = FlatAdamW(eng, lr=1e-3)
+    ids = batches[0]
+    out = m(input_ids=ids, labels=ids)
+    eng.backward(out.loss)
+    opt.step()
+    assert torch.isfinite(out.loss) and abs(out.loss.item() - 6.24) < 0.5
+    full = eng.full_state_dict()
+    assert torch.allclose(full["layers.0.input_layernorm.weight"], torch.ones(256), atol=1e-2)
+    assert full["layers.0.self_attn.qkv_proj.weight"].std().item() == pytest.approx(0.02, rel=0.1)
+
+
+def test_size_policy_units():
+    from dtg.models import build_model
+    from dtg.parallel.fsdp import size_based_units, transformer_units
+
+    m = build_model("llama-tiny", device="meta", dtype=torch.float32, init=False)
+    assert len(transformer_units(m)) == m.config.num_hidden_layers
+    units = size_based_units(m, 100_000)
+    # mlp (393k) and self_attn (196k) exceed the threshold in every layer; Weight holders never
+    # become units (they are not called, so they could not be gathered by hooks)
+    assert len(units) == 2 * m.config.num_hidden_layers
+    assert all(not getattr(u, "_dtg_param_holder", False) for u in units)
