@@ -123,9 +123,10 @@ class FullyShard:
     def __init__(self, model: nn.Module, group=None, policy: str = "transformer", min_num_params: int = 100_000_000,
                  device=None, reshard_after_forward: bool = True, cpu_offload: bool = False,
                  state_dtype=torch.bfloat16, init_fn: Optional[Callable] = None, seed: int = 0,
-                 prefetch: bool = True, max_inflight_rs: int = 2):
+                 prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None):
         self.module = model
         self.group = group
+        self.tp_group = tp_group  # 2-D: sequence-parallel (replicated) grads are summed over TP first
         self.world = comm.world(group) if dist.is_initialized() else 1
         self.rank = comm.rank(group) if self.world > 1 else 0
         self.mode = "fsdp"
@@ -339,7 +340,7 @@ class FullyShard:
 
     def _on_grad(self, p):
         u = p._dtg_unit
-        if getattr(p, "_dtg_sequence_parallel", False) and getattr(self, "tp_group", None) is not None:
+        if getattr(p, "_dtg_sequence_parallel", False) and self.tp_group is not None:
             dist.all_reduce(p.main_grad, group=self.tp_group)
         u.pending -= 1
         if u.pending == 0:

@@ -1,0 +1,78 @@
+"""T2: tensor + sequence parallel (and 2-D dp x tp) on gloo == single-process Llama."""
+import pytest
+import torch
+
+import dtg  # noqa: F401
+
+from _dist import run_distributed
+from test_engines_cpu import _batches, _train
+
+TOL = dict(atol=3e-4, rtol=1e-3)
+
+
+def _tp_worker(rank, world, tp, model_name, batches, engine_mode, steps_loss_only=False):
+    import torch.distributed as dist
+
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+    from dtg.parallel.tensor_parallel import make_mesh, shard_full_state_dict
+
+    dp_group, tp_group, dp_rank, tp_rank, dp = make_mesh(tp)
+    cfg = resolve_config(model_name)
+    torch.manual_seed(0)
+    full = build_model(cfg, device="cpu", dtype=torch.float32)
+    model = build_model(cfg, device="cpu", dtype=torch.float32, tp_group=tp_group, init=False)
+    model.load_state_dict(shard_full_state_dict(full.state_dict(), cfg, tp_rank, tp))
+    if engine_mode == "fsdp":
+        from dtg.parallel.fsdp import FullyShard
+
+        eng = FullyShard(model, group=dp_group, tp_group=tp_group, device="cpu")
+    else:
+        eng = DataParallel(model, mode=engine_mode if dp > 1 else "single", group=dp_group, tp_group=tp_group,
+                           broadcast_from_rank0=False)
+    opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
+    losses = []
+    for ids in batches:
+        per = ids.shape[0] // dp
+        mine = ids[dp_rank * per:(dp_rank + 1) * per]
+        opt.zero_grad()
+        out = model(input_ids=mine, labels=mine)
+        eng.backward(out.loss)
+        opt.step()
+        losses.append(out.loss.item())
+    if engine_mode == "fsdp":
+        sd = eng.full_state_dict(rank0_only=False)
+        return sd, losses, tp_rank
+    return {n: p.detach().clone() for n, p in model.named_parameters()}, losses, tp_rank
+
+
+@pytest.mark.parametrize("world,tp,mode", [(2, 2, "ddp"), (4, 2, "zero"), (4, 2, "ddp"), (4, 2, "fsdp"), (2, 1, "fsdp")])
+def test_tp_sp_matches_single(world, tp, mode):
+    from dtg.models import resolve_config
+    from dtg.parallel.tensor_parallel import unshard_state_dicts
+
+    model_name = "llama-tiny-d128"  # tied embeddings + GQA (4 q / 2 kv heads), llama3 rope
+    cfg = resolve_config(model_name)
+    batches = _batches(cfg.vocab_size, 4, 32)
+    ref, ref_losses = _train(model_name, "single", 0, 1, batches)
+    res = run_distributed(_tp_worker, world, tp, model_name, batches, mode)
+    shards = [r[0] for r in sorted(res[:tp], key=lambda r: r[2])]
+    full = unshard_state_dicts(shards, cfg)
+    for n in ref:
+        torch.testing.assert_close(full[n], ref[n], **TOL, msg=n)
+    # every dp replica identical
+    for r in res[tp:]:
+        for n, v in r[0].items():
+            assert torch.equal(v, res[r[2]][0][n])
+
+
+def test_shard_unshard_roundtrip():
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.tensor_parallel import shard_full_state_dict, unshard_state_dicts
+
+    cfg = resolve_config("llama-tiny")
+    m = build_model(cfg, device="cpu", dtype=torch.float32)
+    sd = m.state_dict()
+    back = unshard_state_dicts([shard_full_state_dict(sd, cfg, r, 2) for r in range(2)], cfg)
+    for k in sd:
+        assert torch.equal(back[k], sd[k]), k
