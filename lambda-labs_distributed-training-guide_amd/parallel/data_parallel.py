@@ -160,17 +160,49 @@ class DataParallel:
                            self.exp_avg_sq[o:o + n], lr=lr, step=self.step_count, beta1=beta1, beta2=beta2,
                            eps=eps, weight_decay=weight_decay, grad_scale=grad_scale,
                            master=None if self.master is None else self.master[o:o + n])
-            works = []
-            for b, (s, e) in zip(self.space.buckets, self.shard_ranges):
-                works.append(comm.all_gather_into(self.space.param_buf[b.start:b.end],
-                                                  self.space.param_buf[s:e].clone() if comm.backend_of(self.group) == "gloo"
-                                                  else self.space.param_buf[s:e], group=self.group, async_op=True))
-            for w in works:
-                w.wait()
+            self._allgather_params()
         else:
             adamw_step(self.space.param_buf, self.space.grad_buf, self.exp_avg, self.exp_avg_sq, lr=lr,
                        step=self.step_count, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
                        grad_scale=grad_scale, master=self.master)
+
+    def _allgather_params(self):
+        """ZeRO: every rank updated its slice of each bucket; all-gather them in place."""
+        gloo = comm.backend_of(self.group) == "gloo"
+        works = []
+        for b, (s, e) in zip(self.space.buckets, self.shard_ranges):
+            src = self.space.param_buf[s:e]
+            works.append(comm.all_gather_into(self.space.param_buf[b.start:b.end], src.clone() if gloo else src,
+                                              group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+
+    def sync_params_after_load(self):
+        if self.mode == "zero":
+            self._allgather_params()
+
+    # ------------------------------------------------------------------ checkpoint layout
+    def ckpt_pieces(self):
+        """This rank's owned slices: (param_name, start_in_param, numel, param_view, state_index).
+
+        ddp/single own whole parameters (states indexed like the flat param buffer); zero owns
+        the r-th slice of every bucket (states indexed in the shard space)."""
+        sp = self.space
+        out = []
+        for i, name in enumerate(sp.names):
+            off, n = sp.offsets[i], int(torch.Size(sp.shapes[i]).numel())
+            if self.mode != "zero":
+                out.append((name, 0, n, sp.param_buf[off:off + n], off))
+                continue
+            b = sp.param_bucket[i]
+            s, e = self.shard_ranges[b.index]
+            lo, hi = max(off, s), min(off + n, e)
+            if lo < hi:
+                out.append((name, lo - off, hi - lo, sp.param_buf[lo:hi], self.shard_offsets[b.index] + (lo - s)))
+        return out
+
+    def full_state_dict(self, rank0_only: bool = True):
+        return {n: p.detach().cpu().clone() for n, p in self.module.named_parameters()}
 
     # ------------------------------------------------------------------ state
     def optimizer_state(self):

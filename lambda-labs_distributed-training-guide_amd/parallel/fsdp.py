@@ -443,13 +443,19 @@ class FullyShard:
         self.exp_avg.copy_(st["exp_avg"])
         self.exp_avg_sq.copy_(st["exp_avg_sq"])
 
-    def sharded_param_items(self):
-        """(unit, name, shard-local slice info) for sharded checkpoints: yields
-        (qualified_name, full_shape, flat_start_in_unit, numel, unit)."""
+    def ckpt_pieces(self):
+        """This rank's owned slices: (param_name, start_in_param, numel, param_view, state_index)."""
+        out = []
         for u in self.all_units:
-            prefix = ""
-            for i, n in enumerate(u.names):
-                yield n, u.shapes[i], u.offsets[i], math.prod(u.shapes[i]), u
+            s = self.rank * u.shard_numel
+            e = s + u.shard_numel
+            for i, name in enumerate(u.names):
+                off, n = u.offsets[i], math.prod(u.shapes[i])
+                lo, hi = max(off, s), min(off + n, e)
+                if lo < hi:
+                    k = u.shard_off + (lo - s)
+                    out.append((name, lo - off, hi - lo, self.shard_params[k:k + (hi - lo)], k))
+        return out
 
     @torch.no_grad()
     def full_state_dict(self, rank0_only: bool = True) -> Dict[str, torch.Tensor]:
