@@ -1,0 +1,66 @@
+"""Per-chapter command lines.
+
+Flags, short forms and defaults are the reference's for every chapter; MI355X-specific knobs are
+additive and never change a reference default.  Fixes: chapters 06/07 default `--seq-length` to
+1024 instead of None, 07 accepts `--tp 1` (#4).
+"""
+import argparse
+
+CHAPTERS = ("rime", "01", "02", "04", "05", "06", "07", "deepspeed")
+
+
+def get_parser(chapter: str) -> argparse.ArgumentParser:
+    assert chapter in CHAPTERS, chapter
+    p = argparse.ArgumentParser(description=f"dtg chapter {chapter} causal-LM trainer (MI355X)")
+    p.add_argument("-e", "--experiment-name", default=None, required=True)
+    if chapter == "rime":
+        p.add_argument("-d", "--dataset-name", default="synthetic:packed",
+                       help="packed 8192-token rows: `disk:<path>` (datasets.load_from_disk) or synthetic:packed")
+        p.add_argument("-m", "--model-name", default="llama-3.2-3b-rime")
+    else:
+        p.add_argument("-d", "--dataset-name", default=None, required=True,
+                       help="HF dataset name/path, or `synthetic` / `synthetic:packed[:mean_doc_len]` (offline)")
+        p.add_argument("-m", "--model-name", default=None, required=True,
+                       help="HF hub name (bundled configs: see dtg.models.available_configs) or config.json path")
+    p.add_argument("--save-dir", default="../outputs")
+    p.add_argument("--seed", default=0, type=int)
+    p.add_argument("--num-epochs", default=1 if chapter == "rime" else 100, type=int)
+    p.add_argument("--lr", default=3e-5, type=float)
+    if chapter != "deepspeed":
+        p.add_argument("-b", "--batch-size", default=1, type=int)
+    p.add_argument("--log-freq", default=50 if chapter == "rime" else 100, type=int)
+    p.add_argument("--ckpt-freq", default=500, type=int)
+    p.add_argument("-s", "--seq-length", default=8192 if chapter == "rime" else 1024, type=int)
+    if chapter == "04":
+        p.add_argument("--numel-to-wrap", default=100_000_000, type=int,
+                       help="Only applies FSDP to modules with numel > this value.")
+    if chapter in ("04", "05"):
+        p.add_argument("--cpu-offload", default="on" if chapter == "05" else "off", choices=["on", "off"])
+    if chapter == "07":
+        p.add_argument("--tp", default=8, type=int)
+    if chapter == "deepspeed":
+        p.add_argument("--local_rank", type=int, default=None)
+        p.add_argument("--deepspeed", action="store_true", help="accepted for launcher compatibility")
+        p.add_argument("--deepspeed_config", default=None, help="ds_config.json (train_micro_batch_size_per_gpu, "
+                       "optimizer.params, scheduler.params, zero_optimization.stage)")
+    # ---- additive MI355X knobs
+    g = p.add_argument_group("dtg (MI355X) options")
+    g.add_argument("--sync-timers", default="on", choices=["on", "off"],
+                   help="on: reference LocalTimer (device sync around every phase); off: HIP-event timers")
+    g.add_argument("--grad-accum", default=1, type=int, help="micro-batches per optimizer step (no_sync)")
+    g.add_argument("--bucket-mb", default=256, type=int, help="gradient bucket size for DDP/ZeRO")
+    if chapter == "02":
+        g.add_argument("--dp-mode", default="zero", choices=["ddp", "zero"],
+                       help="zero: sharded optimizer (reference's ZeroRedundancyOptimizer); ddp: replicated")
+    g.add_argument("--activation-checkpointing", default="on" if chapter == "05" else "off", choices=["on", "off"])
+    g.add_argument("--reshard-after-forward", default="on", choices=["on", "off"])
+    g.add_argument("--num-workers", default=1, type=int)
+    g.add_argument("--prefetch-factor", default=2, type=int)
+    g.add_argument("--num-samples", default=100_000, type=int, help="synthetic dataset size")
+    g.add_argument("--max-steps", default=0, type=int, help="stop after this many optimizer steps (0 = no limit)")
+    g.add_argument("--fault-inject-prob", default=0.0, type=float, help="raise on a step with this probability (elastic tests)")
+    g.add_argument("--wandb", default="auto", choices=["auto", "off"])
+    g.add_argument("--determinism", default="off", choices=["on", "off"])
+    g.add_argument("--init-from", default=None, help="HF safetensors directory to load pretrained weights from")
+    g.add_argument("--tunableop", default="use", choices=["off", "use", "tune"])
+    return p

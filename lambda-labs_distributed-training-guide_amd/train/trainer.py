@@ -1,0 +1,290 @@
+"""The chaptered training driver: one implementation, eight entry points.
+
+Every chapter's `train_llm.py` calls `run("<chapter>")`.  The loop keeps the reference's
+behaviour -- epochs over a (distributed) DataLoader, phase timers data/forward/backward/update,
+skip-ahead resume that still consumes batches, the metric record every `--log-freq` steps and a
+checkpoint every `--ckpt-freq` steps -- on top of this framework's engines:
+
+  rime  single GPU, Llama-3.2-3B + 28,683 tokens, packed 8192-token rows, varlen attention
+  01    single device (GPU, or CPU for the GPT-2 plumbing run)
+  02    data parallel: ZeRO (default, the reference's sharded optimizer) or DDP, bucketed RCCL
+  04    FSDP, size-based wrap (--numel-to-wrap), optional CPU offload, meta-device init
+  05    FSDP, transformer wrap + activation checkpointing + CPU offload (405B recipe)
+  06    tensor + sequence parallel over the node's GPUs, data parallel across nodes
+  07    2-D: FSDP over dp x tensor parallel over tp (--tp)
+  deepspeed  the alternative-framework chapter: ds_config.json keys mapped onto these engines
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import os
+import random
+import time
+from pathlib import Path
+
+import torch
+
+from .. import data as dtg_data
+from ..models import build_model, count_valid_labels, resolve_config
+from ..parallel.checkpointing import apply_activation_checkpointing
+from ..parallel.data_parallel import DataParallel, FlatAdamW
+from ..utils import dist as udist
+from ..utils.metrics import MI355X_BF16_DENSE_FLOPS, MetricSink, get_mem_stats
+from ..utils.timers import make_timers
+from .checkpoint import CheckpointManager, has_checkpoint, new_state
+from .cli import get_parser
+
+LOGGER = logging.getLogger("dtg")
+
+
+def _deepspeed_overrides(args):
+    """Map the ds_config.json keys used by the reference onto this framework."""
+    cfg = {}
+    if args.deepspeed_config:
+        with open(args.deepspeed_config) as fp:
+            cfg = json.load(fp)
+    args.batch_size = int(cfg.get("train_micro_batch_size_per_gpu", 1))
+    opt = cfg.get("optimizer", {}).get("params", {})
+    if "lr" in opt:
+        args.lr = float(opt["lr"])
+    args.betas = tuple(opt.get("betas", (0.9, 0.999)))
+    args.eps = float(opt.get("eps", 1e-8))
+    args.weight_decay = float(opt.get("weight_decay", 0.01))
+    sch = cfg.get("scheduler", {})
+    args.ds_scheduler = sch
+    args.zero_stage = int(cfg.get("zero_optimization", {}).get("stage", 3))
+    args.grad_accum = int(cfg.get("gradient_accumulation_steps", args.grad_accum))
+    return args
+
+
+def _scheduler(args, opt):
+    if getattr(args, "ds_scheduler", None) and args.ds_scheduler.get("type") == "WarmupCosineLR":
+        p = args.ds_scheduler.get("params", {})
+        total = int(p.get("total_num_steps", 1000))
+        warm = int(p.get("warmup_num_steps", 0))
+        floor = float(p.get("cos_min_ratio", 1e-2))
+
+        def f(step):
+            if step < warm:
+                return (step + 1) / max(1, warm)
+            t = min(1.0, (step - warm) / max(1, total - warm))
+            return floor + (1 - floor) * 0.5 * (1 + math.cos(math.pi * t))
+
+        return torch.optim.lr_scheduler.LambdaLR(opt, f)
+    # reference: CosineAnnealingLR(T_max=1000, eta_min=lr*1e-2), stepped every optimizer step
+    return torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=1000, eta_min=args.lr * 1e-2)
+
+
+def _build(args, chapter, device, world):
+    """Model + engine + optimizer for a chapter.  Returns (model, engine, dp_size, dp_rank, ckpt_style)."""
+    cfg = resolve_config(args.model_name)
+    if chapter == "rime" and cfg.vocab_size != 156939:
+        LOGGER.warning("rime chapter expects the +28,683-token vocabulary (llama-3.2-3b-rime)")
+    tp_group = dp_group = None
+    dp_size, dp_rank = world, udist.get_rank()
+    if chapter in ("06", "07"):
+        from ..parallel.tensor_parallel import make_mesh
+
+        tp = args.tp if chapter == "07" else int(os.environ.get("LOCAL_WORLD_SIZE", torch.cuda.device_count() or 1))
+        tp = max(1, min(tp, world))
+        dp_group, tp_group, dp_rank, tp_rank, dp_size = make_mesh(tp)
+        LOGGER.info(f"mesh: dp={dp_size} tp={tp} (dp_rank={dp_rank}, tp_rank={tp_rank})")
+    fsdp = chapter in ("04", "05", "07") or (chapter == "deepspeed" and args.zero_stage == 3)
+    if fsdp:
+        with torch.device("meta"):
+            model = build_model(cfg, tp_group=tp_group, init=False)
+    else:
+        model = build_model(cfg, device=device, tp_group=tp_group)
+    if args.activation_checkpointing == "on":
+        apply_activation_checkpointing(model)
+    LOGGER.info(f"{sum(p.numel() for p in model.parameters()) / 1e9:.3f}B parameters (this rank's shard of TP)")
+    LOGGER.info(f"Before engine: {get_mem_stats(device)}")
+    if fsdp:
+        from ..parallel.fsdp import FullyShard
+
+        policy = "size" if chapter == "04" else "transformer"
+        engine = FullyShard(model, group=dp_group, tp_group=tp_group, policy=policy,
+                            min_num_params=getattr(args, "numel_to_wrap", 100_000_000), device=device,
+                            reshard_after_forward=args.reshard_after_forward == "on",
+                            cpu_offload=getattr(args, "cpu_offload", "off") == "on", seed=args.seed)
+        style = "sharded"
+    else:
+        if chapter in ("01", "rime") or world == 1:
+            mode = "single"
+        elif chapter == "02":
+            mode = args.dp_mode
+        elif chapter == "deepspeed":
+            mode = "ddp" if args.zero_stage == 0 else "zero"
+        else:  # 06: data parallel across TP groups
+            mode = "ddp"
+        engine = DataParallel(model, mode=mode, group=dp_group, tp_group=tp_group, bucket_mb=args.bucket_mb,
+                              broadcast_from_rank0=tp_group is None)
+        style = "full" if mode == "single" and chapter in ("01", "rime") else ("dp" if chapter == "02" else "sharded")
+    LOGGER.info(f"After engine ({engine.mode}): {get_mem_stats(device)}")
+    if args.init_from:
+        from ..models.loading import load_pretrained
+
+        load_pretrained(engine, args.init_from, cfg)
+    return model, engine, dp_size, dp_rank, style, cfg
+
+
+def run(chapter: str, argv=None):
+    parser = get_parser(chapter)
+    args = parser.parse_args(argv)
+    if chapter == "deepspeed":
+        args = _deepspeed_overrides(args)
+    rank, local_rank, world, device = udist.init_distributed(local_rank_arg=getattr(args, "local_rank", None))
+    udist.setup_logging(rank, with_rank=chapter not in ("01", "rime"))
+    LOGGER.info(os.environ)
+    LOGGER.info(args)
+    LOGGER.info(f"local_rank={local_rank} rank={rank} world size={world}")
+    if args.tunableop != "off" and device.type == "cuda":
+        from ..utils.gemm_tuning import enable_tunableop
+
+        enable_tunableop(tune=args.tunableop == "tune")
+    random.seed(args.seed)
+    torch.manual_seed(args.seed)
+    if args.determinism == "on":
+        torch.use_deterministic_algorithms(True, warn_only=True)
+
+    model, engine, dp_size, dp_rank, style, cfg = _build(args, chapter, device, world)
+    opt = FlatAdamW(engine, lr=args.lr, betas=getattr(args, "betas", (0.9, 0.999)), eps=getattr(args, "eps", 1e-8),
+                    weight_decay=getattr(args, "weight_decay", 0.01))
+    lr_scheduler = _scheduler(args, opt)
+
+    # ---- data (reference E1-E8); synthetic by default on the offline boxes
+    with udist.rank0_first():
+        eos = getattr(cfg, "eos_token_id", None)
+        train_data, seq_length, collate = dtg_data.build_dataset(
+            args.dataset_name, tokenizer_name=args.model_name, seq_length=args.seq_length,
+            vocab_size=cfg.vocab_size, max_position_embeddings=cfg.max_position_embeddings,
+            num_samples=args.num_samples, eos_id=eos, seed=args.seed)
+    LOGGER.info(f"{len(train_data)} training samples, seq_length={seq_length}")
+    dataloader = dtg_data.build_dataloader(train_data, args.batch_size, collate, dp_size=dp_size, dp_rank=dp_rank,
+                                           shuffle=chapter != "rime", num_workers=args.num_workers,
+                                           prefetch_factor=args.prefetch_factor, seed=args.seed)
+    LOGGER.info(f"{len(dataloader)} batches per epoch")
+
+    exp_dir = Path(args.save_dir) / args.experiment_name
+    state = new_state()
+    resumed = False
+    mgr = CheckpointManager(exp_dir, engine, opt, lr_scheduler, style, local_rank)
+    if has_checkpoint(exp_dir):
+        LOGGER.info(f"Resuming from {exp_dir}")
+        state = mgr.load()
+        resumed = True
+    LOGGER.info(f"Resumed={resumed} | {state}")
+    udist.make_exp_dir(exp_dir, per_rank_dirs=chapter in ("04", "deepspeed"))
+    sink = MetricSink(exp_dir, rank, use_wandb=args.wandb != "off", wandb_kwargs=dict(
+        project="distributed-training-guide", dir=str(exp_dir), name=args.experiment_name, id=args.experiment_name,
+        resume="must" if resumed else None, config={"args": vars(args), "training_data_size": len(train_data),
+                                                     "num_batches": len(dataloader), "world_size": world}))
+
+    timers = make_timers(device, sync=args.sync_timers == "on")
+    tok_per_step = dp_size * args.batch_size * seq_length * max(1, args.grad_accum)
+    flops_tok = cfg.flops_per_token(seq_length)
+    mem_suffix = "_in_gb" if chapter in ("05", "deepspeed") else "_gb"
+    fault_rng = random.Random(args.seed * 1000 + rank + 7 * state["global_step"])
+    accum = max(1, args.grad_accum)
+    model.train()
+    for state["epoch"] in range(state["epoch"], args.num_epochs):
+        LOGGER.info(f"Begin epoch {state['epoch']} at step {state['epoch_step']}")
+        sampler = getattr(dataloader, "sampler", None)
+        if hasattr(sampler, "set_epoch"):
+            sampler.set_epoch(state["epoch"])  # every chapter (06/07 forgot it: SURVEY §2.11 #3)
+        batches = iter(dataloader)
+        n_steps = len(dataloader) // accum
+        for i_step in range(n_steps):
+            micro = []
+            with timers["data"], torch.no_grad():
+                for _ in range(accum):
+                    b = next(batches)
+                    nv = b.pop("num_valid", None)
+                    if nv is None:
+                        nv = count_valid_labels(b["labels"])
+                    mx = b.pop("max_seqlen", None)
+                    b = {k: v.to(device=device, non_blocking=True) for k, v in b.items()}
+                    b["num_valid"] = nv
+                    if mx is not None:
+                        b["max_seqlen"] = mx
+                    micro.append(b)
+            if i_step < state["epoch_step"]:
+                continue  # resume: data already consumed (order preserved)
+            if args.fault_inject_prob > 0 and fault_rng.random() < args.fault_inject_prob:
+                raise RuntimeError(f"injected fault at global step {state['global_step']} on rank {rank}")
+            opt.zero_grad(set_to_none=True)
+            loss_sum = None
+            for j, b in enumerate(micro):
+                ctx = engine.no_sync() if j < accum - 1 else _null()
+                with ctx:
+                    with timers["forward"]:
+                        out = model(**b)
+                    with timers["backward"]:
+                        engine.backward(out.loss)
+                loss_sum = out.loss.detach() if loss_sum is None else loss_sum + out.loss.detach()
+            with timers["update"]:
+                opt.step()
+                lr_scheduler.step()
+            state["global_step"] += 1
+            state["epoch_step"] += 1
+            state["running_loss"] += (loss_sum / accum).item()
+
+            if state["global_step"] % args.log_freq == 0:
+                ms_per_step = sum(t.avg_elapsed_ms() for t in timers.values())
+                tps = 1000 * tok_per_step / ms_per_step if ms_per_step > 0 else 0.0
+                info = {
+                    "global_step": state["global_step"],
+                    "lr": lr_scheduler.get_last_lr()[0],
+                    "running_loss": state["running_loss"] / args.log_freq,
+                    "epoch": state["epoch"],
+                    "epoch_progress": state["epoch_step"] / n_steps,
+                    "num_batches_remaining": n_steps - i_step,
+                    **get_mem_stats(device, mem_suffix),
+                    "tok/s": tps,
+                    "tok/s/gpu": tps / world,
+                    "mfu": tps * flops_tok / (world * MI355X_BF16_DENSE_FLOPS) if device.type == "cuda" else 0.0,
+                    "time/total": ms_per_step,
+                    **{f"time/{k}": t.avg_elapsed_ms() for k, t in timers.items()},
+                }
+                LOGGER.info(info)
+                sink.log(info, state["global_step"])
+                if device.type == "cuda":
+                    torch.cuda.reset_peak_memory_stats(device)
+                state["running_loss"] = 0
+                for t in timers.values():
+                    t.reset()
+
+            if state["global_step"] % args.ckpt_freq == 0:
+                LOGGER.info("Saving checkpoint.")
+                mgr.save(state)
+            if args.max_steps and state["global_step"] >= args.max_steps:
+                LOGGER.info(f"Reached --max-steps {args.max_steps}")
+                return state
+        state["epoch_step"] = 0
+    return state
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def main(chapter: str, argv=None):
+    """Entry point of every chapter's train_llm.py: @record error capture and a clean
+    process-group teardown."""
+    @udist.record
+    def _main():
+        try:
+            return run(chapter, argv)
+        finally:
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.destroy_process_group()
+
+    return _main()
