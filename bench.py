@@ -55,6 +55,16 @@ def main():
         from dtg.utils.gemm_tuning import enable_tunableop
 
         enable_tunableop(tune=args.tunableop == "tune")
+    if args.tunableop == "tune":
+        import threading
+
+        def _heartbeat():  # tuning can run minutes inside one step: keep the job visibly alive
+            t0 = time.time()
+            while True:
+                time.sleep(30)
+                print(f"[bench] tuning GEMMs... {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+
+        threading.Thread(target=_heartbeat, daemon=True).start()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -99,7 +109,11 @@ def main():
 
     loss = None
     for i in range(args.warmup):
+        tw = time.perf_counter()
         loss = step(i)
+        if cuda:
+            torch.cuda.synchronize()
+        print(f"[bench] warmup step {i}: {time.perf_counter() - tw:.2f}s", file=sys.stderr, flush=True)
     sync()
     if cuda:
         torch.cuda.reset_peak_memory_stats(device)

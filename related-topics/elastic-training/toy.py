@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Fault-injection toy for elastic restarts.  CPU only (gloo), no GPU needed.
+
+Every step each rank draws a random number and raises with probability --fail-prob; torchrun
+(`--max-restarts N`) then restarts ALL workers, which resume from `toy-state.json` (written by
+rank 0 between two barriers).  RNG is reseeded from rank + world_size * num_steps after a
+restart, so a restarted job does not replay the same failure.
+
+    torchrun --nnodes 1 --nproc-per-node 4 --max-restarts 3 toy.py
+"""
+import argparse
+import json
+import os
+import random
+import time
+
+import torch.distributed as dist
+from torch.distributed.elastic.multiprocessing.errors import record
+
+
+@record
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--fail-prob", type=float, default=0.001)
+    ap.add_argument("--state", default="./toy-state.json")
+    ap.add_argument("--sleep", type=float, default=0.0)
+    ap.add_argument("--fail-at-step", type=int, default=-1, help="deterministic failure of rank 1 on the first attempt")
+    a = ap.parse_args()
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    state = {"num_steps": 0}
+    if os.path.exists(a.state):
+        with open(a.state) as fp:
+            state = json.load(fp)
+    random.seed(rank + world * state["num_steps"])
+    print(f"[rank {rank}] starting at step {state['num_steps']} (restart count {os.environ.get('TORCHELASTIC_RESTART_COUNT', 0)})", flush=True)
+    while state["num_steps"] < a.steps:
+        first_attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") == "0"
+        if state["num_steps"] == a.fail_at_step and rank == min(1, world - 1) and first_attempt:
+            raise ValueError(f"rank {rank} deterministic failure at step {state['num_steps']}")
+        if random.random() < a.fail_prob:
+            raise ValueError(f"rank {rank} injected failure at step {state['num_steps']}")
+        time.sleep(a.sleep)
+        state["num_steps"] += 1
+        dist.barrier()
+        if rank == 0:
+            with open(a.state, "w") as fp:
+                json.dump(state, fp)
+        dist.barrier()
+    if rank == 0:
+        print(f"finished {state['num_steps']} steps", flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,45 @@
+"""T5: fault injection + torchrun elastic restart resumes from persisted state."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from _dist import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.slow
+def test_toy_restarts_and_resumes(tmp_path):
+    state = tmp_path / "toy-state.json"
+    err = tmp_path / "error.json"
+    env = dict(os.environ, TORCHELASTIC_ERROR_FILE=str(err), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--max-restarts", "2", "--rdzv-backend", "c10d", "--rdzv-endpoint", f"127.0.0.1:{free_port()}",
+           os.path.join(ROOT, "related-topics", "elastic-training", "toy.py"), "--steps", "40", "--fail-prob", "0",
+           "--fail-at-step", "15", "--state", str(state)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "deterministic failure at step 15" in out
+    assert "starting at step 15 (restart count 1)" in out
+    assert json.loads(state.read_text())["num_steps"] == 40
+
+
+@pytest.mark.slow
+def test_trainer_fault_inject_then_resume(tmp_path):
+    """--fault-inject-prob 1 crashes the first attempt after its checkpoint; the restarted
+    trainer resumes from state.json and completes (trainer-level T5)."""
+    chapter = os.path.join(ROOT, "01-single-gpu", "train_llm.py")
+    base = [sys.executable, chapter, "-e", "ft", "-d", "synthetic", "-m", "gpt2-tiny", "-s", "32", "--num-samples", "64",
+            "--save-dir", str(tmp_path), "--log-freq", "1", "--ckpt-freq", "2", "--num-workers", "0"]
+    r = subprocess.run(base + ["--max-steps", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run(base + ["--max-steps", "6", "--fault-inject-prob", "1.0"], capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "injected fault" in (r.stdout + r.stderr)
+    r = subprocess.run(base + ["--max-steps", "4"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "Resuming" in (r.stdout + r.stderr)
+    st = json.loads((tmp_path / "ft" / "state.json").read_text())
+    assert st["global_step"] == 4

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""RCCL collective bandwidth over xGMI: all_reduce, all_gather,
+reduce_scatter and all_to_all over message sizes, reported as algorithm and bus bandwidth
+(nccl-tests conventions), so bucket sizes for DDP/ZeRO/FSDP can be chosen from measurements.
+
+    torchrun --standalone --nproc-per-node 8 tools/bench_collectives.py --json > coll.jsonl
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+
+def bench(op, nbytes, world, device, iters, warmup):
+    n = nbytes // 2
+    x = torch.randn(n, device=device).bfloat16()
+    if op == "all_reduce":
+        fn = lambda: dist.all_reduce(x)
+        factor = 2 * (world - 1) / world
+    elif op == "all_gather":
+        out = torch.empty(n * world, device=device, dtype=torch.bfloat16)
+        fn = lambda: dist.all_gather_into_tensor(out, x)
+        factor = (world - 1) / world
+        nbytes = nbytes * world
+    elif op == "reduce_scatter":
+        out = torch.empty(n // world, device=device, dtype=torch.bfloat16)
+        fn = lambda: dist.reduce_scatter_tensor(out, x)
+        factor = (world - 1) / world
+    else:
+        out = torch.empty_like(x)
+        fn = lambda: dist.all_to_all_single(out, x)
+        factor = (world - 1) / world
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    algbw = nbytes / dt / 1e9
+    return dt * 1e6, algbw, algbw * factor
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="all_reduce,all_gather,reduce_scatter,all_to_all")
+    ap.add_argument("--min-mb", type=float, default=1)
+    ap.add_argument("--max-mb", type=float, default=1024)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--json", action="store_true")
+    a = ap.parse_args()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    dist.init_process_group("nccl", device_id=device)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    size = a.min_mb
+    while size <= a.max_mb:
+        nbytes = int(size * (1 << 20)) // (2 * world) * (2 * world)
+        for op in a.ops.split(","):
+            us, alg, bus = bench(op, nbytes, world, device, a.iters, a.warmup)
+            if rank == 0:
+                rec = {"op": op, "bytes": nbytes, "world": world, "time_us": round(us, 1), "algbw_GBps": round(alg, 2),
+                       "busbw_GBps": round(bus, 2)}
+                print(json.dumps(rec) if a.json else f"{op:15s} {nbytes / 2**20:9.1f} MiB {us:10.1f} us  "
+                      f"algbw {alg:7.1f} GB/s  busbw {bus:7.1f} GB/s", flush=True)
+        size *= 2
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())
