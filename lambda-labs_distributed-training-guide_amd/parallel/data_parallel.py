@@ -33,7 +33,7 @@ from .flat import FlatSpace, rebind_parameters
 class DataParallel:
     def __init__(self, model: nn.Module, mode: str = "ddp", group=None, tp_group=None,
                  bucket_mb: int = 256, broadcast_from_rank0: bool = True, state_dtype=torch.bfloat16,
-                 master_weights: bool = False):
+                 master_weights: bool = False, overlap_param_gather: bool = True):
         assert mode in ("single", "ddp", "zero")
         self.module = model
         self.group = group
@@ -73,6 +73,13 @@ class DataParallel:
             self._shard_param_copy(self.master)
         self.step_count = 0
         self.accum_count = 0  # micro-batches accumulated since the last step
+        # ZeRO: the post-step parameter all-gathers are left in flight and each bucket is waited
+        # for just before the first module that reads it runs in the next forward, so they
+        # overlap with the embedding/early-layer compute instead of stalling the step.
+        self._pending_ag = {}
+        self.overlap_param_gather = overlap_param_gather and self.mode == "zero"
+        if self.overlap_param_gather:
+            self._install_gather_hooks()
         # The engine owns the loss: backward(loss) uses an implicit gradient of 1 and any
         # scaling goes into AdamW's grad_scale, which lets the loss head write dW in place.
         set_direct_loss_grad(True)
@@ -154,28 +161,63 @@ class DataParallel:
         if grad_scale is None:
             grad_scale = 1.0 / (self.world * max(1, self.accum_count))
         if self.mode == "zero":
+            self.wait_param_gather()  # never update a slice an all-gather may still be reading
             for (s, e), o in zip(self.shard_ranges, self.shard_offsets):
                 n = e - s
                 adamw_step(self.space.param_buf[s:e], self.grad_shard[o:o + n], self.exp_avg[o:o + n],
                            self.exp_avg_sq[o:o + n], lr=lr, step=self.step_count, beta1=beta1, beta2=beta2,
                            eps=eps, weight_decay=weight_decay, grad_scale=grad_scale,
                            master=None if self.master is None else self.master[o:o + n])
-            self._allgather_params()
+            self._allgather_params(wait=not self.overlap_param_gather)
         else:
             adamw_step(self.space.param_buf, self.space.grad_buf, self.exp_avg, self.exp_avg_sq, lr=lr,
                        step=self.step_count, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
                        grad_scale=grad_scale, master=self.master)
 
-    def _allgather_params(self):
-        """ZeRO: every rank updated its slice of each bucket; all-gather them in place."""
+    def _allgather_params(self, wait: bool = True):
+        """ZeRO: every rank updated its slice of each bucket; all-gather them in place, in the
+        order the next forward needs them (`_ag_order`)."""
         gloo = comm.backend_of(self.group) == "gloo"
-        works = []
-        for b, (s, e) in zip(self.space.buckets, self.shard_ranges):
-            src = self.space.param_buf[s:e]
-            works.append(comm.all_gather_into(self.space.param_buf[b.start:b.end], src.clone() if gloo else src,
-                                              group=self.group, async_op=True))
-        for w in works:
-            w.wait()
+        order = getattr(self, "_ag_order", range(len(self.space.buckets)))
+        # `.data` has its own version counter: the in-place gather (which may complete during the
+        # next forward) must not invalidate weights autograd has already saved.
+        buf = self.space.param_buf.data
+        for i in order:
+            b = self.space.buckets[i]
+            s, e = self.shard_ranges[i]
+            src = buf[s:e]
+            self._pending_ag[i] = comm.all_gather_into(buf[b.start:b.end], src.clone() if gloo else src,
+                                                       group=self.group, async_op=True)
+        if wait:
+            self.wait_param_gather()
+
+    def wait_param_gather(self, buckets=None):
+        for i in (list(self._pending_ag) if buckets is None else buckets):
+            w = self._pending_ag.pop(i, None)
+            if w is not None:
+                w.wait()
+
+    def _install_gather_hooks(self):
+        """Map modules -> buckets they read: each decoder layer waits for its own buckets, the
+        root waits for the buckets of parameters outside the layers (embedding, norm, head)."""
+        bucket_of = {id(p): p._dtg_bucket.index for p in self.params}
+        layers = list(getattr(self.module, "layers", []))
+        in_layer = set()
+        order = []
+        for layer in layers:
+            bs = sorted({bucket_of[id(p)] for p in layer.parameters() if id(p) in bucket_of})
+            for p in layer.parameters():
+                in_layer.add(id(p))
+            layer.register_forward_pre_hook(lambda m, a, _bs=bs: self.wait_param_gather(_bs))
+            order.extend(bs)
+        root_bs = sorted({bucket_of[id(p)] for p in self.params if id(p) not in in_layer})
+        self.module.register_forward_pre_hook(lambda m, a: self.wait_param_gather(root_bs))
+        seen, ag_order = set(), []
+        for i in root_bs + order + list(range(len(self.space.buckets))):
+            if i not in seen:
+                seen.add(i)
+                ag_order.append(i)
+        self._ag_order = ag_order
 
     def sync_params_after_load(self):
         if self.mode == "zero":
@@ -187,6 +229,7 @@ class DataParallel:
 
         ddp/single own whole parameters (states indexed like the flat param buffer); zero owns
         the r-th slice of every bucket (states indexed in the shard space)."""
+        self.wait_param_gather()
         sp = self.space
         out = []
         for i, name in enumerate(sp.names):
@@ -202,6 +245,7 @@ class DataParallel:
         return out
 
     def full_state_dict(self, rank0_only: bool = True):
+        self.wait_param_gather()
         return {n: p.detach().cpu().clone() for n, p in self.module.named_parameters()}
 
     # ------------------------------------------------------------------ state

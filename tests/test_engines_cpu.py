@@ -38,6 +38,8 @@ def _train(model_name, mode, rank, world, batches, bucket_mb=1, accum=1):
                 eng.backward(out.loss)
         opt.step()
         losses.append(out.loss.item())
+    if hasattr(eng, "wait_param_gather"):
+        eng.wait_param_gather()  # ZeRO leaves the last all-gather in flight until the next forward
     return {n: p.detach().clone() for n, p in model.named_parameters()}, losses
 
 

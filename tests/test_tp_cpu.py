@@ -43,6 +43,8 @@ def _tp_worker(rank, world, tp, model_name, batches, engine_mode, steps_loss_onl
     if engine_mode == "fsdp":
         sd = eng.full_state_dict(rank0_only=False)
         return sd, losses, tp_rank
+    if hasattr(eng, "wait_param_gather"):
+        eng.wait_param_gather()  # ZeRO leaves the last all-gather in flight until the next forward
     return {n: p.detach().clone() for n, p in model.named_parameters()}, losses, tp_rank
 
 
