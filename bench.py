@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--lr", type=float, default=3e-5)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
+    ap.add_argument("--backend", default=None, help="process-group backend override (default: nccl=RCCL on GPU)")
     ap.add_argument("--tunableop", choices=["off", "use", "tune"], default="use",
                     help="PyTorch TunableOp for the hipBLASLt GEMMs: 'use' loads the committed per-shape "
                          "solution table (tunableop/), 'tune' benchmarks new shapes during warmup and writes it")
@@ -69,11 +70,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
-    device = torch.device(f"cuda:{local_rank}" if cuda else "cpu")
+    # DTG_SHARED_DEVICE=1: every rank on cuda:0 (engine tests with the gloo backend on a 1-GPU box)
+    dev_idx = 0 if os.environ.get("DTG_SHARED_DEVICE") == "1" else local_rank
+    device = torch.device(f"cuda:{dev_idx}" if cuda else "cpu")
     if cuda:
         torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl" if cuda else "gloo", device_id=device if cuda else None)
+        backend = args.backend or ("nccl" if cuda else "gloo")
+        dist.init_process_group(backend, device_id=device if (cuda and backend == "nccl") else None)
     torch.manual_seed(0)
 
     cfg = resolve_config(args.model)
@@ -81,7 +85,7 @@ def main():
     if args.parallel == "fsdp":
         from dtg.parallel.fsdp import FullyShard
 
-        engine = FullyShard(model, group=None if world > 1 else None)
+        engine = FullyShard(model)
     else:
         engine = DataParallel(model, mode=args.parallel if world > 1 else "single", bucket_mb=args.bucket_mb)
     opt = FlatAdamW(engine, lr=args.lr)

@@ -11,7 +11,7 @@ import os
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-TABLE = os.path.join(ROOT, "tunableop", "tunableop_results.csv")
+TABLE = os.path.join(ROOT, "tunableop", "tunableop_results_partial.csv")
 
 
 def enable_tunableop(tune: bool = False, max_tuning_ms: int = 30, table: str = TABLE):
