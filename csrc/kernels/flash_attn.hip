@@ -20,6 +20,8 @@
 //    ds_read_b128 row reads and transposed reads share one copy.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dtg {
 namespace fa {
 
@@ -479,6 +481,195 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_kernel(BwdParams P)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Backward v2: 8 waves share one 256-key block (32 keys per wave, dK^T/dV^T in registers) and
+// sweep 64-row query items.  Per item: phase 1 computes S, dP (key on the lane), P, dS and the
+// dV^T/dK^T products and stores dS^T to LDS; phase 2 computes this item's dQ partial over all
+// 256 keys (one 32x32 tile per wave) and adds it with f32 atomics.  Compared with v1 the K/V
+// block and the Q/dO staging are shared by twice the waves (2 waves per SIMD instead of 1) and
+// the dQ atomic traffic per FLOP halves (256- instead of 128-key blocks).
+constexpr int kB2K = 256;  // keys per workgroup (8 waves x 32)
+constexpr int kB2Q = 64;   // query rows per item (2 x 32-row sub-tiles)
+constexpr int kB2Threads = 512;
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(kB2Threads, 2) void bwd2_kernel(BwdParams P) {
+  constexpr int NC = D / 16;
+  constexpr int ND = D / 32;
+  constexpr int KBYTES = kB2K * D * 2;
+  constexpr int QBYTES = kB2Q * D * 2;
+  constexpr int DSBYTES = kB2K * kB2Q * 2;  // dS^T image [256 keys][64 q]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kl = smem;
+  char* Ql = smem + KBYTES;
+  char* dOl = Ql + QBYTES;
+  char* dSl = dOl + QBYTES;
+  float* rowc = reinterpret_cast<float*>(dSl + DSBYTES);  // lse2[64], delta[64]
+
+  const int seq = blockIdx.z, kvh = blockIdx.y;
+  const int s0 = P.cu[seq];
+  const int seqlen = P.cu[seq + 1] - s0;
+  const int kb = blockIdx.x * kB2K;
+  if (kb >= seqlen) return;
+  const int group = P.hq / P.hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int key = kb + 32 * w + r;
+
+  {
+    Stager<kB2K, D, kB2Threads> stk;
+    stk.load(P.k + (int64_t)(s0 + kb) * P.sk + (int64_t)kvh * D, P.sk, seqlen - kb);
+    stk.store(Kl);
+  }
+  bf16x8 vf[NC];
+  {
+    const bool ok = key < seqlen;
+    const uint16_t* vp = P.v + (int64_t)(s0 + (ok ? key : 0)) * P.sv + (int64_t)kvh * D + 8 * h;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      u16x8 t = ok ? *reinterpret_cast<const u16x8*>(vp + 16 * c) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      vf[c] = __builtin_bit_cast(bf16x8, t);
+    }
+  }
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    dk[i] = f32x16{};
+    dv[i] = f32x16{};
+  }
+
+  const int first_slice = CAUSAL ? (kb / kB2Q) : 0;
+  const int nslices = (seqlen + kB2Q - 1) / kB2Q;
+  const int per_head = nslices - first_slice;
+  const int nitems = per_head * group;
+  auto item = [&](int it, int& hqi, int& qs) {
+    hqi = kvh * group + it / per_head;
+    qs = (first_slice + it % per_head) * kB2Q;
+  };
+
+  Stager<kB2Q, D, kB2Threads> sq, sdo;
+  float rc = 0.f;
+  auto load_item = [&](int it) {
+    int hqi, qs;
+    item(it, hqi, qs);
+    const int nv = seqlen - qs;
+    sq.load(P.q + (int64_t)(s0 + qs) * P.sq + (int64_t)hqi * D, P.sq, nv);
+    sdo.load(P.dout + ((int64_t)(s0 + qs) * P.hq + hqi) * D, (int64_t)P.hq * D, nv);
+    if (threadIdx.x < 128) {
+      const int qi = qs + (threadIdx.x & 63);
+      const bool ok = qi < seqlen;
+      if (threadIdx.x < 64) rc = ok ? P.lse[(int64_t)hqi * P.T + s0 + qi] * kLog2e : 0.f;
+      else rc = ok ? P.delta[(int64_t)hqi * P.T + s0 + qi] : 0.f;
+    }
+  };
+  auto store_item = [&]() {
+    sq.store(Ql);
+    sdo.store(dOl);
+    if (threadIdx.x < 128) rowc[threadIdx.x] = rc;
+  };
+
+  if (nitems > 0) {
+    load_item(0);
+    store_item();
+  }
+  __syncthreads();
+
+  // dQ tile assignment: tiles = 2 q-subtiles x ND d-tiles; waves beyond split the keys.
+  constexpr int TILES = 2 * ND;
+  constexpr int KSPLIT = 8 / TILES;
+  constexpr int KPER = kB2K / KSPLIT;
+  const int tile = w % TILES, kpart = w / TILES;
+  const int tq = tile / ND, tdt = tile % ND;
+
+  for (int it = 0; it < nitems; ++it) {
+    const bool more = it + 1 < nitems;
+    if (more) load_item(it + 1);
+    int hqi, qs;
+    item(it, hqi, qs);
+    // ---------------- phase 1: per 32-row sub-tile, key on the lane (not unrolled: keeps one
+    // sub-tile's S/dP live at a time)
+#pragma unroll 1
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qrow0 = qs + 32 * qt;
+      const bool skip = CAUSAL && (qrow0 + 31 < kb + 32 * w);  // all queries before all keys
+      f32x16 s = f32x16{}, dp = f32x16{};
+      if (!skip) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          s = mfma(row_frag<D>(Ql, 32 * qt + r, 2 * c + h), row_frag<D>(Kl, 32 * w + r, 2 * c + h), s);
+          dp = mfma(row_frag<D>(dOl, 32 * qt + r, 2 * c + h), vf[c], dp);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qr = 32 * qt + acc_row(i, h);
+          const int qi = qs + qr;
+          const bool valid = (qi < seqlen) && (key < seqlen) && (!CAUSAL || key <= qi);
+          const float p = valid ? exp2f(s[i] * P.c2 - rowc[qr]) : 0.f;
+          s[i] = p;
+          dp[i] = p * (dp[i] - rowc[64 + qr]) * P.scale;
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pf = pack8(s, st);
+          const bf16x8 dsf = pack8(dp, st);
+          const int ra = 32 * qt + 16 * st + 4 * h;
+#pragma unroll
+          for (int d = 0; d < ND; ++d) {
+            dv[d] = mfma(tr_frag<D>(dOl, ra, ra + 8, 32 * d), pf, dv[d]);
+            dk[d] = mfma(tr_frag<D>(Ql, ra, ra + 8, 32 * d), dsf, dk[d]);
+          }
+        }
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        ushort4 v;
+        v.x = f2bf(dp[4 * g4 + 0]);
+        v.y = f2bf(dp[4 * g4 + 1]);
+        v.z = f2bf(dp[4 * g4 + 2]);
+        v.w = f2bf(dp[4 * g4 + 3]);
+        *reinterpret_cast<ushort4*>(dSl + off<kB2Q>(32 * w + r, 4 * qt + g4) + 8 * h) = v;
+      }
+    }
+    __syncthreads();
+    // ---------------- phase 2: next item's Q/dO go to LDS while this item's dQ is summed
+    if (more) store_item();
+    {
+      f32x16 q = f32x16{};
+#pragma unroll
+      for (int st = 0; st < KPER / 16; ++st) {
+        const int k0 = kpart * KPER + 16 * st + 8 * h;
+        q = mfma(tr_frag<kB2Q>(dSl, k0, k0 + 4, 32 * tq), tr_frag<D>(Kl, k0, k0 + 4, 32 * tdt), q);
+      }
+      const int qbase = qs + 32 * tq;
+      float* dqp = P.dq + (int64_t)(s0 + qbase) * P.hq * D + (int64_t)hqi * D + 32 * tdt + r;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qr = acc_row(i, h);
+        if (qbase + qr < seqlen) atomicAdd(dqp + (int64_t)qr * P.hq * D, q[i]);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (key < seqlen) {
+    uint16_t* dkp = P.dk + (int64_t)(s0 + key) * P.sdk + (int64_t)kvh * D;
+    uint16_t* dvp = P.dv + (int64_t)(s0 + key) * P.sdv + (int64_t)kvh * D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        ushort4 a, b;
+        a.x = f2bf(dk[d][4 * g4 + 0]); a.y = f2bf(dk[d][4 * g4 + 1]);
+        a.z = f2bf(dk[d][4 * g4 + 2]); a.w = f2bf(dk[d][4 * g4 + 3]);
+        b.x = f2bf(dv[d][4 * g4 + 0]); b.y = f2bf(dv[d][4 * g4 + 1]);
+        b.z = f2bf(dv[d][4 * g4 + 2]); b.w = f2bf(dv[d][4 * g4 + 3]);
+        *reinterpret_cast<ushort4*>(dkp + 32 * d + 8 * g4 + 4 * h) = a;
+        *reinterpret_cast<ushort4*>(dvp + 32 * d + 8 * g4 + 4 * h) = b;
+      }
+    }
+  }
+}
+
 // dq f32 [T, W] (contiguous) -> bf16 destination rows with token stride `ld` (W % 8 == 0).
 __global__ void f32_to_bf16_rows_kernel(const float* __restrict__ in, uint16_t* __restrict__ out,
                                         int64_t T, int W, int64_t ld) {
@@ -583,14 +774,31 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
                   v.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), dq32.data_ptr<float>(),
                   bf16_mut(dk), bf16_mut(dv), dk.stride(0), dv.stride(0), cu_seqlens.data_ptr<int>(), T,
                   (int)hq, (int)hkv, (float)scale, (float)(scale * fa::kLog2e)};
-  dim3 grid((max_seqlen + fa::kBwdBK - 1) / fa::kBwdBK, hkv, nseq);
-  const size_t lds = fa::kBwdBK * D * 2 + 4 * fa::kBwdBQ * D * 2 + fa::kBwdBK * fa::kBwdBQ * 2 + 2 * 64 * 4;
+  // v1 (4 waves x 32 keys, 1 wave/SIMD) is the default; DTG_FA_BWD=2 selects the experimental
+  // 8-wave variant (register-bound at head_dim 128: spills, see profiles/).
+  static const bool use_v1 = [] {
+    const char* e = std::getenv("DTG_FA_BWD");
+    return !(e != nullptr && e[0] == '2');
+  }();
+  if (use_v1) {
+    dim3 grid((max_seqlen + fa::kBwdBK - 1) / fa::kBwdBK, hkv, nseq);
+    const size_t lds = fa::kBwdBK * D * 2 + 4 * fa::kBwdBQ * D * 2 + fa::kBwdBK * fa::kBwdBQ * 2 + 2 * 64 * 4;
 #define DTG_BWD(DD, C)                                                                    \
   do { set_lds_limit((const void*)&fa::bwd_kernel<DD, C>, lds);                              \
        hipLaunchKernelGGL((fa::bwd_kernel<DD, C>), grid, dim3(256), lds, stream(), P); } while (0)
-  if (D == 128) { if (causal) DTG_BWD(128, true); else DTG_BWD(128, false); }
-  else { if (causal) DTG_BWD(64, true); else DTG_BWD(64, false); }
+    if (D == 128) { if (causal) DTG_BWD(128, true); else DTG_BWD(128, false); }
+    else { if (causal) DTG_BWD(64, true); else DTG_BWD(64, false); }
 #undef DTG_BWD
+  } else {
+    dim3 grid((max_seqlen + fa::kB2K - 1) / fa::kB2K, hkv, nseq);
+    const size_t lds = fa::kB2K * D * 2 + 2 * fa::kB2Q * D * 2 + fa::kB2K * fa::kB2Q * 2 + 128 * 4;
+#define DTG_BWD2(DD, C)                                                                   \
+  do { set_lds_limit((const void*)&fa::bwd2_kernel<DD, C>, lds);                             \
+       hipLaunchKernelGGL((fa::bwd2_kernel<DD, C>), grid, dim3(fa::kB2Threads), lds, stream(), P); } while (0)
+    if (D == 128) { if (causal) DTG_BWD2(128, true); else DTG_BWD2(128, false); }
+    else { if (causal) DTG_BWD2(64, true); else DTG_BWD2(64, false); }
+#undef DTG_BWD2
+  }
   DTG_LAUNCH_CHECK();
   const int W = hq * D;
   const int64_t n = T * W;

@@ -13,13 +13,27 @@ import os
 from itertools import chain
 
 
+_BUILDERS = {".txt": "text", ".json": "json", ".jsonl": "json", ".parquet": "parquet", ".csv": "csv"}
+
+
+def _load(datasets, name):
+    """HF hub name, a local dataset directory, or a local data file (text/json/parquet/csv)."""
+    if os.path.isfile(name):
+        ext = os.path.splitext(name)[1].lower()
+        return datasets.load_dataset(_BUILDERS.get(ext, "text"), data_files={"train": name})
+    import inspect
+
+    kw = {"trust_remote_code": True} if "trust_remote_code" in inspect.signature(datasets.load_dataset).parameters else {}
+    return datasets.load_dataset(name, **kw)
+
+
 def load_and_preprocess(dataset_name: str, tokenizer_name: str, seq_length, max_position_embeddings: int,
                         num_proc: int | None = None):
     import datasets
     from transformers import AutoTokenizer
 
     tok = AutoTokenizer.from_pretrained(tokenizer_name)
-    data = datasets.load_dataset(dataset_name, trust_remote_code=True)
+    data = _load(datasets, dataset_name)
     split = data["train"]
     column_names = split.column_names
     text_column = "text" if "text" in column_names else column_names[0]

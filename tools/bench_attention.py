@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Flash-attention kernel micro-benchmark (fwd / bwd) at the model shapes, random data.
+
+    python tools/bench_attention.py --shape llama8b      # B16 S1024 Hq32 Hkv8 D128 causal
+    python tools/bench_attention.py --shape rime         # 1 x 8192 packed docs, Hq24 Hkv8
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch  # noqa: E402
+
+import dtg  # noqa: E402,F401
+import dtg.ops  # noqa: E402,F401
+
+SHAPES = {
+    "llama8b": dict(B=16, S=1024, hq=32, hkv=8, d=128, docs=None),
+    "llama8b-tp8": dict(B=16, S=1024, hq=4, hkv=1, d=128, docs=None),
+    "rime": dict(B=1, S=8192, hq=24, hkv=8, d=128, docs=600),
+    "gpt2": dict(B=16, S=1024, hq=12, hkv=12, d=64, docs=None),
+    "long": dict(B=2, S=8192, hq=32, hkv=8, d=128, docs=None),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="llama8b", choices=list(SHAPES))
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    c = SHAPES[a.shape]
+    dev = torch.device("cuda:0")
+    B, S, hq, hkv, d = c["B"], c["S"], c["hq"], c["hkv"], c["d"]
+    T = B * S
+    if c["docs"]:
+        g = torch.Generator().manual_seed(0)
+        lens = []
+        left = T
+        while left > 0:
+            n = min(left, int(torch.randint(64, 2 * c["docs"], (1,), generator=g)))
+            lens.append(n)
+            left -= n
+        cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32)
+        causal_flops = sum(l * l / 2 for l in lens) * 4 * d * hq
+    else:
+        cu = torch.arange(0, T + 1, S, dtype=torch.int32)
+        causal_flops = B * S * S / 2 * 4 * d * hq
+    cu = cu.to(dev)
+    maxlen = int((cu[1:] - cu[:-1]).max())
+    qkv = torch.randn(T, (hq + 2 * hkv) * d, device=dev).bfloat16()
+    q = qkv[:, : hq * d].view(T, hq, d)
+    k = qkv[:, hq * d:(hq + hkv) * d].view(T, hkv, d)
+    v = qkv[:, (hq + hkv) * d:].view(T, hkv, d)
+    do = torch.randn(T, hq, d, device=dev).bfloat16()
+    ops = torch.ops.dtg
+    scale = 1 / math.sqrt(d)
+    o, lse = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, True)
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / a.iters
+
+    tf = timeit(lambda: ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, True))
+    tb = timeit(lambda: ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, True))
+    rec = {"shape": a.shape, "fwd_ms": tf * 1e3, "bwd_ms": tb * 1e3, "fwd_TFLOPs": causal_flops / tf / 1e12,
+           "bwd_TFLOPs": 2.5 * causal_flops / tb / 1e12, "bwd_variant": os.environ.get("DTG_FA_BWD", "1")}
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
