@@ -54,7 +54,10 @@ def _deepspeed_overrides(args):
     args.weight_decay = float(opt.get("weight_decay", 0.01))
     sch = cfg.get("scheduler", {})
     args.ds_scheduler = sch
-    args.zero_stage = int(cfg.get("zero_optimization", {}).get("stage", 3))
+    zero = cfg.get("zero_optimization", {})
+    args.zero_stage = int(zero.get("stage", 3))
+    off = (zero.get("offload_optimizer") or {}).get("device", "none")
+    args.cpu_offload = "on" if (off == "cpu" and args.zero_stage == 3) else "off"
     args.grad_accum = int(cfg.get("gradient_accumulation_steps", args.grad_accum))
     return args
 
@@ -277,6 +280,14 @@ class _null:
 def main(chapter: str, argv=None):
     """Entry point of every chapter's train_llm.py: @record error capture and a clean
     process-group teardown."""
+    import faulthandler
+    import signal
+
+    try:  # `kill -USR1 <pid>` dumps every thread's Python stack (diagnosing-errors/README.md)
+        faulthandler.register(signal.SIGUSR1, all_threads=True)
+    except (AttributeError, ValueError):
+        pass
+
     @udist.record
     def _main():
         try:

@@ -52,4 +52,7 @@ def test_deepspeed_config_mapping(tmp_path):
                                "zero_optimization": {"stage": 2}}))
     a = get_parser("deepspeed").parse_args(BASE + ["--deepspeed_config", str(cfg)])
     a = _deepspeed_overrides(a)
-    assert a.batch_size == 4 and a.lr == 1e-4 and a.zero_stage == 2
+    assert a.batch_size == 4 and a.lr == 1e-4 and a.zero_stage == 2 and a.cpu_offload == "off"
+    cfg.write_text(json.dumps({"zero_optimization": {"stage": 3, "offload_optimizer": {"device": "cpu"}}}))
+    a = _deepspeed_overrides(get_parser("deepspeed").parse_args(BASE + ["--deepspeed_config", str(cfg)]))
+    assert a.zero_stage == 3 and a.cpu_offload == "on"
