@@ -53,9 +53,9 @@ def transformer_units(model: nn.Module) -> List[nn.Module]:
 
 
 def _callable_unit(m: nn.Module) -> bool:
-    # parameter holders (models.llama.Weight) are never called, so forward hooks cannot gather
-    # them: their parameters belong to the enclosing unit instead.
-    return not getattr(m, "_dtg_param_holder", False)
+    # parameter holders (models.llama.Weight) and containers (ModuleList/ModuleDict) are never
+    # called, so forward hooks cannot gather them: their parameters belong to the enclosing unit.
+    return not getattr(m, "_dtg_param_holder", False) and not isinstance(m, (nn.ModuleList, nn.ModuleDict))
 
 
 def size_based_units(model: nn.Module, min_num_params: int) -> List[nn.Module]:

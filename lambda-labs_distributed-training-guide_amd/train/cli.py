@@ -45,6 +45,8 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                        "optimizer.params, scheduler.params, zero_optimization.stage)")
     # ---- additive MI355X knobs
     g = p.add_argument_group("dtg (MI355X) options")
+    g.add_argument("--waiting-timers", default="off", choices=["on", "off"],
+                   help="time a barrier before forward/backward/update (straggler detection)")
     g.add_argument("--sync-timers", default="on", choices=["on", "off"],
                    help="on: reference LocalTimer (device sync around every phase); off: HIP-event timers")
     g.add_argument("--grad-accum", default=1, type=int, help="micro-batches per optimizer step (no_sync)")

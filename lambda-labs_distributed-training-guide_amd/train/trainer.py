@@ -185,7 +185,16 @@ def run(chapter: str, argv=None):
         resume="must" if resumed else None, config={"args": vars(args), "training_data_size": len(train_data),
                                                      "num_batches": len(dataloader), "world_size": world}))
 
-    timers = make_timers(device, sync=args.sync_timers == "on")
+    waiting = getattr(args, "waiting_timers", "off") == "on" and world > 1
+    names = ("data", "forward", "backward", "update") + (("waiting",) if waiting else ())
+    timers = make_timers(device, names=names, sync=args.sync_timers == "on")
+
+    def wait_for_peers():
+        # Straggler probe (related-topics/optimizing-data-loading): time spent in a barrier
+        # before each phase is time this rank waited for the slowest one.
+        if waiting:
+            with timers["waiting"]:
+                torch.distributed.barrier()
     tok_per_step = dp_size * args.batch_size * seq_length * max(1, args.grad_accum)
     flops_tok = cfg.flops_per_token(seq_length)
     mem_suffix = "_in_gb" if chapter in ("05", "deepspeed") else "_gb"
@@ -222,11 +231,14 @@ def run(chapter: str, argv=None):
             for j, b in enumerate(micro):
                 ctx = engine.no_sync() if j < accum - 1 else _null()
                 with ctx:
+                    wait_for_peers()
                     with timers["forward"]:
                         out = model(**b)
+                    wait_for_peers()
                     with timers["backward"]:
                         engine.backward(out.loss)
                 loss_sum = out.loss.detach() if loss_sum is None else loss_sum + out.loss.detach()
+            wait_for_peers()
             with timers["update"]:
                 opt.step()
                 lr_scheduler.step()

@@ -72,7 +72,7 @@ def main():
     tf = timeit(lambda: ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, True))
     tb = timeit(lambda: ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, True))
     rec = {"shape": a.shape, "fwd_ms": tf * 1e3, "bwd_ms": tb * 1e3, "fwd_TFLOPs": causal_flops / tf / 1e12,
-           "bwd_TFLOPs": 2.5 * causal_flops / tb / 1e12, "bwd_variant": os.environ.get("DTG_FA_BWD", "1")}
+           "bwd_TFLOPs": 2.5 * causal_flops / tb / 1e12, "bwd_variant": os.environ.get("DTG_FA_BWD", "split"), "occ": os.environ.get("DTG_FA_OCC", "1")}
     print(json.dumps(rec), flush=True)
 
 
