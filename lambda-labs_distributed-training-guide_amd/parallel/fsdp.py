@@ -123,13 +123,18 @@ class FullyShard:
     def __init__(self, model: nn.Module, group=None, policy: str = "transformer", min_num_params: int = 100_000_000,
                  device=None, reshard_after_forward: bool = True, cpu_offload: bool = False,
                  state_dtype=torch.bfloat16, init_fn: Optional[Callable] = None, seed: int = 0,
-                 prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None):
+                 prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None, replicate_group=None):
         self.module = model
         self.group = group
+        # HYBRID_SHARD (ZeRO++-style): shard inside `group` (one node's xGMI island), replicate
+        # across `replicate_group` (same local rank on every node); gradient shards are summed
+        # over the replicas once per optimizer step.
+        self.replicate_group = replicate_group
+        self.replicas = comm.world(replicate_group) if (replicate_group is not None and dist.is_initialized()) else 1
         self.tp_group = tp_group  # 2-D: sequence-parallel (replicated) grads are summed over TP first
         self.world = comm.world(group) if dist.is_initialized() else 1
         self.rank = comm.rank(group) if self.world > 1 else 0
-        self.mode = "fsdp"
+        self.mode = "fsdp" if self.replicas == 1 else "hybrid"
         self.reshard_after_forward = reshard_after_forward
         self.cpu_offload = cpu_offload
         self.prefetch = prefetch
@@ -421,7 +426,15 @@ class FullyShard:
     def step(self, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, grad_scale=None):
         self.step_count += 1
         if grad_scale is None:
-            grad_scale = 1.0 / (self.world * max(1, self.accum_count))
+            grad_scale = 1.0 / (self.world * self.replicas * max(1, self.accum_count))
+        if self.replicas > 1:
+            g = self.shard_grads
+            if g.device.type == "cpu" and comm.backend_of(self.replicate_group) != "gloo":
+                gd = g.to(self.device)
+                dist.all_reduce(gd, group=self.replicate_group)
+                g.copy_(gd)
+            else:
+                dist.all_reduce(g, group=self.replicate_group)
         if self.cpu_offload:
             from ..ops.adamw import adamw_step_cpu
 

@@ -36,6 +36,10 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                        help="Only applies FSDP to modules with numel > this value.")
     if chapter in ("04", "05"):
         p.add_argument("--cpu-offload", default="on" if chapter == "05" else "off", choices=["on", "off"])
+        p.add_argument("--sharding", default="full", choices=["full", "hybrid"],
+                       help="full: FULL_SHARD over all ranks; hybrid: shard within --shard-size ranks (one node), "
+                            "replicate across nodes (HYBRID_SHARD)")
+        p.add_argument("--shard-size", default=None, type=int, help="ranks per shard group (default LOCAL_WORLD_SIZE)")
     if chapter == "07":
         p.add_argument("--tp", default=8, type=int)
     if chapter == "deepspeed":

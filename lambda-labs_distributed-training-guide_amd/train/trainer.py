@@ -94,6 +94,15 @@ def _build(args, chapter, device, world):
         tp = max(1, min(tp, world))
         dp_group, tp_group, dp_rank, tp_rank, dp_size = make_mesh(tp)
         LOGGER.info(f"mesh: dp={dp_size} tp={tp} (dp_rank={dp_rank}, tp_rank={tp_rank})")
+    replicate_group = None
+    if getattr(args, "sharding", "full") == "hybrid" and world > 1:
+        from ..parallel.tensor_parallel import make_mesh
+
+        shard = args.shard_size or int(os.environ.get("LOCAL_WORLD_SIZE", torch.cuda.device_count() or 1))
+        shard = max(1, min(shard, world))
+        # contiguous groups of `shard` ranks hold one sharded replica; strided groups replicate
+        replicate_group, dp_group, _, _, n_rep = make_mesh(shard)
+        LOGGER.info(f"hybrid sharding: {n_rep} replicas x {shard}-way shards")
     fsdp = chapter in ("04", "05", "07") or (chapter == "deepspeed" and args.zero_stage == 3)
     if fsdp:
         with torch.device("meta"):
@@ -111,7 +120,8 @@ def _build(args, chapter, device, world):
         engine = FullyShard(model, group=dp_group, tp_group=tp_group, policy=policy,
                             min_num_params=getattr(args, "numel_to_wrap", 100_000_000), device=device,
                             reshard_after_forward=args.reshard_after_forward == "on",
-                            cpu_offload=getattr(args, "cpu_offload", "off") == "on", seed=args.seed)
+                            cpu_offload=getattr(args, "cpu_offload", "off") == "on", seed=args.seed,
+                            replicate_group=replicate_group)
         style = "sharded"
     else:
         if chapter in ("01", "rime") or world == 1:

@@ -88,3 +88,36 @@ def test_size_policy_units():
     # become units (they are not called, so they could not be gathered by hooks)
     assert len(units) == 2 * m.config.num_hidden_layers
     assert all(not getattr(u, "_dtg_param_holder", False) for u in units)
+
+
+def _hybrid_train(rank, world, model_name, batches, shard):
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+    from dtg.parallel.tensor_parallel import make_mesh
+
+    torch.manual_seed(0)
+    replicate, shard_group, _, _, n_rep = make_mesh(shard)
+    model = build_model(model_name, device="cpu", dtype=torch.float32)
+    eng = FullyShard(model, group=shard_group, replicate_group=replicate, device="cpu")
+    opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
+    for ids in batches:
+        per = ids.shape[0] // world
+        mine = ids[rank * per:(rank + 1) * per]
+        opt.zero_grad()
+        out = model(input_ids=mine, labels=mine)
+        eng.backward(out.loss)
+        opt.step()
+    return eng.full_state_dict(rank0_only=False), eng.mode, eng.world, eng.replicas
+
+
+def test_hybrid_shard_matches_single():
+    """HYBRID_SHARD: 2 replicas x 2-way shards (world 4) reproduce single-process training."""
+    batches = _batches(512, 4, 32)
+    ref, _ = _train("llama-tiny", "single", 0, 1, batches)
+    res = run_distributed(_hybrid_train, 4, "llama-tiny", batches, 2)
+    for r in range(4):
+        sd, mode, w, reps = res[r]
+        assert (mode, w, reps) == ("hybrid", 2, 2)
+        for n in ref:
+            torch.testing.assert_close(sd[n], ref[n], **TOL, msg=f"rank {r} {n}")
