@@ -12,12 +12,19 @@
 //    per lane; the row reduction is 31 f32 max + one cross-half shuffle), then
 //    O^T += V^T P^T with P^T taken straight from the S^T accumulator registers (the k order
 //    inside a 16-step is permuted; V^T fragments are fetched in the same permuted order with
-//    ds_read_b64_tr_b16, T10).
-//  * Backward keeps the key on the lane: S and dP accumulators are the B operands of the
-//    dV^T and dK^T products; dS crosses LDS once (stored transposed) for dQ, which is summed
-//    across key blocks with f32 atomics in the full-rate two-128-B-rows shape (Guideline 12).
-//  * All K/V/Q/dO tiles live in LDS as 16-byte-chunk XOR-swizzled images (T10 image (b)), so
-//    ds_read_b128 row reads and transposed reads share one copy.
+//    ds_read_b64_tr_b16, T10).  The running max is rescaled lazily (only when it grows by more
+//    than 2^8, T13), so most tiles skip the O rescale.
+//  * Backward is split in two kernels that both recompute P (seven MFMA products per tile
+//    instead of five) so that no partial sum crosses workgroups: no f32 dQ atomics, whose
+//    chip-wide rate bounds the one-kernel form at these shapes, and dQ is bitwise reproducible.
+//    bwd_dq_kernel is query-stationary with the forward's structure; bwd_dkdv_kernel is
+//    key-stationary with this wave's K and V rows held in registers, so only Q/dO slices stream
+//    through LDS.
+//  * Tiles live in LDS as 16-byte-chunk XOR-swizzled images (T10 image (b)); ds_read_b128 row
+//    reads and transposed reads share one copy, and every lane's LDS offsets are computed once
+//    (the swizzle depends on the low 4 row bits only, so tile/step offsets are immediates).
+//  * Global -> register staging goes through buffer descriptors: rows past the end of a
+//    sequence read as zeros from the range check, with no per-row branches.
 #include "common.h"
 
 #include <cstdlib>
@@ -29,42 +36,28 @@ typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kRescaleThreshold = 8.f;  // log2 units: P values stay below 2^8
 
 // Byte offset of 16-byte chunk `ch` of row `row` in a [rows][W] bf16 LDS image.
 template <int W>
 __device__ __forceinline__ int off(int row, int ch) {
   constexpr int NCH = W / 8;
+  static_assert(NCH == 8 || NCH == 16, "head_dim 64 or 128");
   int sw;
-  if constexpr (NCH >= 16) sw = ((row & 3) << 2) | ((row >> 2) & 3);
-  else if constexpr (NCH == 8) sw = ((row & 1) << 2) | ((row >> 1) & 3);
-  else sw = row & (NCH - 1);
+  if constexpr (NCH == 16) sw = ((row & 3) << 2) | ((row >> 2) & 3);
+  else sw = ((row & 1) << 2) | ((row >> 1) & 3);
   return row * (W * 2) + 16 * (ch ^ sw);
-}
-
-// A/B fragment whose MFMA row index is the tile row and whose k index runs along the row:
-// lane (r, h) gets tile[row][8*chunk .. +7].
-template <int W>
-__device__ __forceinline__ bf16x8 row_frag(const char* tile, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(tile + off<W>(row, ch));
 }
 
 __device__ __forceinline__ i16x4 tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p));
 }
 
-// Fragment whose MFMA row index is a tile COLUMN (col0 + lane%32) and whose k index runs down
-// the tile rows: elements 0..3 come from rows rowA..rowA+3, elements 4..7 from rowB..rowB+3.
-// Must be executed by all 64 lanes (EXEC all ones, T10).
-template <int W>
-__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int rowA, int rowB, int col0) {
-  const int lane = threadIdx.x & 63;
-  const int i = lane & 15, g = lane >> 4;
-  const int q = i >> 2, p = i & 3;
-  const int colbase = col0 + 16 * (g & 1);
-  const int ch = (colbase >> 3) + (p >> 1);
-  const int half = 8 * (p & 1);
-  const i16x4 a = tr_read(tile + off<W>(rowA + q, ch) + half);
-  const i16x4 b = tr_read(tile + off<W>(rowB + q, ch) + half);
+// Transposed fragment (MFMA row index = a tile column, k index running down the rows) from
+// the two precomputed lane addresses of tr_offsets.  Must run with all 64 lanes active.
+__device__ __forceinline__ bf16x8 tr_frag_at(const char* pa, const char* pb) {
+  const i16x4 a = tr_read(pa);
+  const i16x4 b = tr_read(pb);
   // Whole-vector concatenation: per-element extraction of the tr-read result miscompiles on
   // ROCm 7.2 (hipcc duplicates the low dword; caught by tests/native/probe_fragments.hip).
   typedef short i16x8 __attribute__((ext_vector_type(8)));
@@ -72,9 +65,25 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int rowA, int rowB, 
   return __builtin_bit_cast(bf16x8, ab);
 }
 
+// Lane offsets of the transposed fragment for output column tile d (columns 32d..32d+31) and
+// k rows {4h+q .. +3} (A half) and {4h+q+8 ..} (B half) of a 16-row step; add 16*step*rowbytes.
+template <int W>
+__device__ __forceinline__ void tr_offsets(int d, int& oa, int& ob) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane & 15, g = lane >> 4;
+  const int q = i >> 2, p = i & 3;
+  const int ch = ((32 * d + 16 * (g & 1)) >> 3) + (p >> 1);
+  const int half = 8 * (p & 1);
+  const int row = 4 * (g >> 1) + q;
+  oa = off<W>(row, ch) + half;
+  ob = off<W>(row + 8, ch) + half;
+}
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+
+__device__ __forceinline__ bf16x8 lds_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 // Pack accumulator registers 8s .. 8s+7 into a bf16 operand fragment.
 __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
@@ -84,8 +93,72 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
   return r;
 }
 
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Scheduling hints (T19) for a region of n MFMAs fed by n*rpm LDS reads: keep `ahead` reads in
+// flight in front of the MFMA chain instead of hipcc's read -> wait -> MFMA serialisation.
+constexpr int kSchedMfma = 0x008, kSchedDsRead = 0x100;
+template <int N, int RPM, int AHEAD>
+__device__ __forceinline__ void pipeline_reads() {
+  __builtin_amdgcn_sched_group_barrier(kSchedDsRead, AHEAD * RPM, 0);
+#pragma unroll
+  for (int i = 0; i < N - AHEAD; ++i) {
+    __builtin_amdgcn_sched_group_barrier(kSchedMfma, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(kSchedDsRead, RPM, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(kSchedMfma, AHEAD, 0);
+}
+
 // Row of accumulator register `reg` for lane half h (32x32 C/D map).
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// Buffer descriptor over `bytes` bytes at p, built from provably wave-uniform values (T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo),
+                                           (short)0, n, 0x00020000);
+}
+
+// Register-staged copy of R rows x W bf16 (token stride `stride`) into a swizzled LDS image.
+// Rows at or past `nvalid` are outside the descriptor's range and read as zeros.
+template <int R, int W, int NT>
+struct Stager {
+  static constexpr int NCH = W / 8;
+  static constexpr int PER = (R * NCH) / NT;
+  static constexpr int RSTEP = NT / NCH;  // rows between a thread's consecutive chunks
+  static_assert((R * NCH) % NT == 0 && NT % NCH == 0 && RSTEP % 16 == 0, "tile split");
+  u16x8 regs[PER];
+  __device__ __forceinline__ void load(const uint16_t* base, int64_t stride, int nvalid) {
+    const int row0 = threadIdx.x / NCH, ch = threadIdx.x % NCH;
+    const int bytes = nvalid > 0 ? static_cast<int>((nvalid - 1) * stride * 2 + W * 2) : 0;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, bytes);
+    const int s2 = static_cast<int>(stride) * 2;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int voff = (row0 + i * RSTEP) * s2 + ch * 16;
+      regs[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+    }
+  }
+  __device__ __forceinline__ void store(char* tile) const {
+    const int o = off<W>(threadIdx.x / NCH, threadIdx.x % NCH);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) *reinterpret_cast<u16x8*>(tile + o + i * RSTEP * W * 2) = regs[i];
+  }
+};
+
+// One lane's 16-byte slices of a row: elements [16c + 8h, +8) for c < D/16 (zero if !ok).
+template <int NC>
+__device__ __forceinline__ void load_row_frags(const uint16_t* row, bool ok, int h, bf16x8* out) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const u16x8 z{0, 0, 0, 0, 0, 0, 0, 0};
+    const u16x8 v = ok ? *reinterpret_cast<const u16x8*>(row + 16 * c + 8 * h) : z;
+    out[c] = __builtin_bit_cast(bf16x8, v);
+  }
+}
 
 struct FwdParams {
   const uint16_t *q, *k, *v;
@@ -101,40 +174,13 @@ struct FwdParams {
 constexpr int kFwdBQ = 128;  // query rows per workgroup (4 waves x 32)
 constexpr int kFwdBK = 64;   // keys per K/V tile
 
-// Register-staged copy of R rows x W bf16 from global into a swizzled LDS image.
-template <int R, int W, int NT>
-struct Stager {
-  static constexpr int NCH = W / 8;
-  static constexpr int PER = (R * NCH) / NT;
-  static_assert((R * NCH) % NT == 0, "tile must split evenly over the threads");
-  u16x8 regs[PER];
-  __device__ __forceinline__ void load(const uint16_t* base, int64_t stride, int nvalid) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int idx = threadIdx.x + i * NT;
-      const int row = idx / NCH, ch = idx % NCH;
-      if (row < nvalid) regs[i] = *reinterpret_cast<const u16x8*>(base + row * stride + ch * 8);
-      else regs[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  }
-  __device__ __forceinline__ void store(char* tile) const {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int idx = threadIdx.x + i * NT;
-      const int row = idx / NCH, ch = idx % NCH;
-      *reinterpret_cast<u16x8*>(tile + off<W>(row, ch)) = regs[i];
-    }
-  }
-};
-
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
-  constexpr int TILE_BYTES = kFwdBK * D * 2;
+  constexpr int RB = 2 * D;
+  constexpr int TILE = kFwdBK * RB;
   constexpr int NC = D / 16;  // k-steps over head_dim
   constexpr int ND = D / 32;  // 32-wide d tiles of the output
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  auto kbuf = [&](int i) { return smem + i * 2 * TILE_BYTES; };
-  auto vbuf = [&](int i) { return smem + i * 2 * TILE_BYTES + TILE_BYTES; };
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1]
 
   const int seq = blockIdx.z, head = blockIdx.y;
   const int s0 = P.cu[seq];
@@ -143,21 +189,17 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   const int q0 = qb * kFwdBQ;
   if (q0 >= seqlen) return;
   const int kvh = head / (P.hq / P.hkv);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int qrow = q0 + 32 * w + r;  // this lane's query (sequence-relative)
 
-  // Q^T fragments for all k-steps, straight from global into registers.
-  bf16x8 qf[NC];
-  {
-    const bool ok = qrow < seqlen;
-    const uint16_t* qp = P.q + (int64_t)(s0 + (ok ? qrow : 0)) * P.sq + (int64_t)head * D + 8 * h;
+  bf16x8 qf[NC];  // Q^T fragments for all k-steps
+  load_row_frags<NC>(P.q + (int64_t)(s0 + min(qrow, seqlen - 1)) * P.sq + (int64_t)head * D, qrow < seqlen, h, qf);
+  int koff[NC], toa[ND], tob[ND];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      u16x8 v = ok ? *reinterpret_cast<const u16x8*>(qp + 16 * c) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      qf[c] = __builtin_bit_cast(bf16x8, v);
-    }
-  }
+  for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
+#pragma unroll
+  for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
 
   const int kv_end = CAUSAL ? min(seqlen, q0 + kFwdBQ) : seqlen;
   const int ntiles = (kv_end + kFwdBK - 1) / kFwdBK;
@@ -172,11 +214,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   Stager<kFwdBK, D, 256> sk, sv;
   sk.load(kbase, P.sk, seqlen);
   sv.load(vbase, P.sv, seqlen);
-  sk.store(kbuf(0));
-  sv.store(vbuf(0));
+  sk.store(smem);
+  sv.store(smem + TILE);
   __syncthreads();
 
-  const int wave_qmax = q0 + 32 * w + 31;
+  const int wave_q0 = q0 + 32 * w, wave_qmax = wave_q0 + 31;
   for (int t = 0; t < ntiles; ++t) {
     const int kt0 = t * kFwdBK;
     const bool more = t + 1 < ntiles;
@@ -185,65 +227,80 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       sk.load(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk);
       sv.load(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk);
     }
-    const char* K = kbuf(t & 1);
-    const char* V = vbuf(t & 1);
-    // Wave-uniform skip of tiles entirely above this wave's causal diagonal.
-    const bool active = !CAUSAL || kt0 <= wave_qmax;
-    if (active) {
+    const char* K = smem + (t & 1) * 2 * TILE;
+    const char* V = K + TILE;
+    if (!CAUSAL || kt0 <= wave_qmax) {  // wave-uniform skip of tiles above the diagonal
       f32x16 s[2];
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
+        bf16x8 kf[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) kf[c] = lds_frag(K + kt * 32 * RB + koff[c]);
         s[kt] = f32x16{};
 #pragma unroll
-        for (int c = 0; c < NC; ++c) s[kt] = mfma(row_frag<D>(K, kt * 32 + r, 2 * c + h), qf[c], s[kt]);
+        for (int c = 0; c < NC; ++c) s[kt] = mfma(kf[c], qf[c], s[kt]);
       }
-      const bool need_mask = (CAUSAL && kt0 + kFwdBK - 1 > q0 + 32 * w) || (kt0 + kFwdBK > seqlen);
-      float mx = -INFINITY;
+      pipeline_reads<2 * NC, 1, 4>();
+      __builtin_amdgcn_sched_barrier(0);
+      if ((CAUSAL && kt0 + kFwdBK - 1 > wave_q0) || kt0 + kFwdBK > seqlen) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = kt0 + kt * 32 + acc_row(i, h);
+            const bool bad = (key >= seqlen) | (CAUSAL & (key > qrow));
+            s[kt][i] = bad ? -INFINITY : s[kt][i];
+          }
+        }
+      }
+      float mx = s[0][0];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float x = s[kt][i] * P.c2;
-          if (need_mask) {
-            const int key = kt0 + kt * 32 + acc_row(i, h);
-            if (key >= seqlen || (CAUSAL && key > qrow)) x = -INFINITY;
-          }
-          s[kt][i] = x;
-          mx = fmaxf(mx, x);
-        }
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kt][i]);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m, mx);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m - m_use);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * P.c2;
+      if (__builtin_amdgcn_ballot_w64(mx > m + kRescaleThreshold) != 0) {
+        const float mn = fmaxf(m, mx);
+        const float alpha = (mn == -INFINITY) ? 1.f : fexp2(m - mn);
+        l *= alpha;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) acc[d] *= alpha;
+        m = mn;
+      }
+      const float mu = (m == -INFINITY) ? 0.f : m;
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = exp2f(s[kt][i] - m_use);
+          const float p = fexp2(__builtin_fmaf(s[kt][i], P.c2, -mu));
           s[kt][i] = p;
           rs += p;
         }
       }
-      l = l * alpha + rs;
-      m = m_new;
+      l += rs;
+      bf16x8 pf[4];
 #pragma unroll
-      for (int d = 0; d < ND; ++d) acc[d] *= alpha;
+      for (int j = 0; j < 4; ++j) pf[j] = pack8(s[j >> 1], j & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
+      for (int j = 0; j < 4; ++j) {  // 16-key steps
+        const char* vb = V + 16 * j * RB;
+        bf16x8 vt[ND];
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8 pf = pack8(s[kt], st);
-          const int ra = kt * 32 + 16 * st + 4 * h;
+        for (int d = 0; d < ND; ++d) vt[d] = tr_frag_at(vb + toa[d], vb + tob[d]);
 #pragma unroll
-          for (int d = 0; d < ND; ++d) acc[d] = mfma(tr_frag<D>(V, ra, ra + 8, 32 * d), pf, acc[d]);
-        }
+        for (int d = 0; d < ND; ++d) acc[d] = mfma(vt[d], pf[j], acc[d]);
       }
+      pipeline_reads<4 * ND, 2, 3>();
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (more) {
-      sk.store(kbuf((t + 1) & 1));
-      sv.store(vbuf((t + 1) & 1));
+      char* nb = smem + ((t + 1) & 1) * 2 * TILE;
+      sk.store(nb);
+      sv.store(nb + TILE);
     }
     __syncthreads();
   }
@@ -268,83 +325,211 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   }
 }
 
-// delta[h][t] = sum_d dO[t][h][d] * O[t][h][d]   (one wave per (t, h) row)
-template <int D>
-__global__ void bwd_pre_kernel(const uint16_t* __restrict__ o, const uint16_t* __restrict__ dout,
-                               float* __restrict__ delta, int64_t T, int hq) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= T * hq) return;
-  constexpr int PERL = D / 64;  // elements per lane
-  const uint16_t* op = o + row * D + lane * PERL;
-  const uint16_t* dp = dout + row * D + lane * PERL;
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < PERL; ++j) s += bf2f(op[j]) * bf2f(dp[j]);
-  s = wave_sum(s);
-  if (lane == 0) {
-    const int64_t t = row / hq;
-    const int hh = row % hq;
-    delta[(int64_t)hh * T + t] = s;
-  }
-}
-
 struct BwdParams {
-  const uint16_t *q, *k, *v, *dout;
-  int64_t sq, sk, sv;  // token strides of q, k, v (dout is contiguous [T, Hq, D])
-  const float *lse, *delta;
-  float* dq;           // [T, Hq, D] f32 accumulator
-  uint16_t *dk, *dv;   // [T, Hkv, D] views
-  int64_t sdk, sdv;    // token strides of dk, dv
+  const uint16_t *q, *k, *v, *dout, *o;
+  int64_t sq, sk, sv;  // token strides of q, k, v (dout and o are contiguous [T, Hq, D])
+  const float* lse;    // [Hq, T]
+  float* delta;        // [Hq, T]: written by bwd_dq_kernel, read by bwd_dkdv_kernel
+  uint16_t *dq, *dk, *dv;  // [T, H, D] views
+  int64_t sdq, sdk, sdv;   // token strides of dq, dk, dv
   const int* cu;
   int64_t T;
   int hq, hkv;
   float scale, c2;
 };
 
-constexpr int kBwdBK = 128;  // keys per workgroup (4 waves x 32)
-constexpr int kBwdBQ = 32;   // query rows per slice
+constexpr int kDqBQ = 128;  // query rows per workgroup (4 waves x 32)
+constexpr int kDqBK = 64;   // keys per K/V tile
+constexpr int kKvBK = 128;  // keys per workgroup (4 waves x 32)
+constexpr int kKvBQ = 32;   // query rows per item
 
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_kernel(BwdParams P) {
+// dQ = scale * sum_keys dS K, query-stationary (the forward's structure).  Also writes
+// delta = rowsum(dO * O) for its rows, which bwd_dkdv_kernel (launched after it) reads.
+template <int D, bool CAUSAL, int OCC>
+__global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
+  constexpr int RB = 2 * D;
+  constexpr int TILE = kDqBK * RB;
   constexpr int NC = D / 16;
   constexpr int ND = D / 32;
-  constexpr int SLICE = kBwdBQ * D * 2;           // bytes of one Q (or dO) slice image
-  constexpr int KBYTES = kBwdBK * D * 2;
-  constexpr int DSBYTES = kBwdBK * kBwdBQ * 2;    // dS^T image [128 keys][32 q]
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Kl = smem;
-  auto qbuf = [&](int i) { return smem + KBYTES + i * 2 * SLICE; };
-  auto dobuf = [&](int i) { return smem + KBYTES + i * 2 * SLICE + SLICE; };
-  char* dSl = smem + KBYTES + 4 * SLICE;
-  float* rowc = reinterpret_cast<float*>(smem + KBYTES + 4 * SLICE + DSBYTES);  // [2][2][32]
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1]
+
+  const int seq = blockIdx.z, head = blockIdx.y;
+  const int s0 = P.cu[seq];
+  const int seqlen = P.cu[seq + 1] - s0;
+  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;  // heavy blocks first
+  const int q0 = qb * kDqBQ;
+  if (q0 >= seqlen) return;
+  const int kvh = head / (P.hq / P.hkv);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int qrow = q0 + 32 * w + r;
+  const bool qok = qrow < seqlen;
+  const int64_t t_row = s0 + (qok ? qrow : seqlen - 1);
+
+  bf16x8 qf[NC], dof[NC];
+  load_row_frags<NC>(P.q + t_row * P.sq + (int64_t)head * D, qok, h, qf);
+  load_row_frags<NC>(P.dout + (t_row * P.hq + head) * D, qok, h, dof);
+  float delta;
+  {
+    bf16x8 of[NC];
+    load_row_frags<NC>(P.o + (t_row * P.hq + head) * D, qok, h, of);
+    float part = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += static_cast<float>(dof[c][j]) * static_cast<float>(of[c][j]);
+    }
+    delta = part + __shfl_xor(part, 32, 64);
+    if (qok && h == 0) P.delta[(int64_t)head * P.T + s0 + qrow] = delta;
+  }
+  const float lse2 = qok ? P.lse[(int64_t)head * P.T + s0 + qrow] * kLog2e : 0.f;
+
+  int koff[NC], toa[ND], tob[ND];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
+#pragma unroll
+  for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
+
+  const int kv_end = CAUSAL ? min(seqlen, q0 + kDqBQ) : seqlen;
+  const int ntiles = (kv_end + kDqBK - 1) / kDqBK;
+  const uint16_t* kbase = P.k + (int64_t)s0 * P.sk + (int64_t)kvh * D;
+  const uint16_t* vbase = P.v + (int64_t)s0 * P.sv + (int64_t)kvh * D;
+
+  f32x16 acc[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) acc[i] = f32x16{};
+
+  Stager<kDqBK, D, 256> sk, sv;
+  sk.load(kbase, P.sk, seqlen);
+  sv.load(vbase, P.sv, seqlen);
+  sk.store(smem);
+  sv.store(smem + TILE);
+  __syncthreads();
+
+  const int wave_q0 = q0 + 32 * w, wave_qmax = wave_q0 + 31;
+  for (int t = 0; t < ntiles; ++t) {
+    const int kt0 = t * kDqBK;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      const int nk = kt0 + kDqBK;
+      sk.load(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk);
+      sv.load(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk);
+    }
+    const char* K = smem + (t & 1) * 2 * TILE;
+    const char* V = K + TILE;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int key0 = kt0 + 32 * kt;
+      // Wave-uniform skip of 32-key halves entirely above the diagonal or past the end.
+      if ((CAUSAL && key0 > wave_qmax) || key0 >= seqlen) continue;
+      f32x16 s = f32x16{}, dp = f32x16{};
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        bf16x8 f[NC], g[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) f[c] = lds_frag(K + kt * 32 * RB + koff[c]);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) s = mfma(f[c], qf[c], s);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) g[c] = lds_frag(V + kt * 32 * RB + koff[c]);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) dp = mfma(g[c], dof[c], dp);
+      }
+      pipeline_reads<2 * NC, 1, 4>();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = fexp2(__builtin_fmaf(s[i], P.c2, -lse2));
+      if ((CAUSAL && key0 + 31 > wave_q0) || key0 + 32 > seqlen) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = key0 + acc_row(i, h);
+          const bool bad = (key >= seqlen) | (CAUSAL & (key > qrow));
+          s[i] = bad ? 0.f : s[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] *= dp[i] - delta;  // dS^T / scale
+      const bf16x8 dsf[2] = {pack8(s, 0), pack8(s, 1)};
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const char* kb = K + (32 * kt + 16 * st) * RB;
+        bf16x8 kt_[ND];
+#pragma unroll
+        for (int d = 0; d < ND; ++d) kt_[d] = tr_frag_at(kb + toa[d], kb + tob[d]);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) acc[d] = mfma(kt_[d], dsf[st], acc[d]);
+      }
+      pipeline_reads<2 * ND, 2, 3>();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more) {
+      char* nb = smem + ((t + 1) & 1) * 2 * TILE;
+      sk.store(nb);
+      sv.store(nb + TILE);
+    }
+    __syncthreads();
+  }
+
+  if (qok) {
+    uint16_t* op = P.dq + (int64_t)(s0 + qrow) * P.sdq + (int64_t)head * D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        ushort4 v;
+        v.x = f2bf(acc[d][4 * g4 + 0] * P.scale);
+        v.y = f2bf(acc[d][4 * g4 + 1] * P.scale);
+        v.z = f2bf(acc[d][4 * g4 + 2] * P.scale);
+        v.w = f2bf(acc[d][4 * g4 + 3] * P.scale);
+        *reinterpret_cast<ushort4*>(op + 32 * d + 8 * g4 + 4 * h) = v;
+      }
+    }
+  }
+}
+
+// dK, dV, key-stationary: 4 waves x 32 keys; the block's K and V rows sit in LDS (B operands of
+// S = Q K^T and dP = dO V^T; holding them in registers instead pushes the wave past 256 VGPRs
+// and hipcc then shuffles the dK/dV accumulators through AGPRs every item), and the workgroup
+// sweeps (query head, 32-row slice) items with Q/dO double-buffered in LDS.  S and dP start from the row constants
+// (-lse/scale, -delta) so p = exp2(c2 S') and dS = p dP' need no per-element subtraction;
+// only the causal diagonal is masked (padded query rows carry Q = dO = 0 and contribute 0).
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdParams P) {
+  constexpr int RB = 2 * D;
+  constexpr int NC = D / 16;
+  constexpr int ND = D / 32;
+  constexpr int SLICE = kKvBQ * RB;
+  constexpr int KV = kKvBK * RB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [K | V | Q0 | dO0 | Q1 | dO1 | rowc]
+  const char* Kl = smem;
+  const char* Vl = smem + KV;
+  char* qd = smem + 2 * KV;
+  float* rowc = reinterpret_cast<float*>(qd + 4 * SLICE);      // [2][-lse/scale x32, -delta x32]
 
   const int seq = blockIdx.z, kvh = blockIdx.y;
   const int s0 = P.cu[seq];
   const int seqlen = P.cu[seq + 1] - s0;
-  const int kb = blockIdx.x * kBwdBK;
+  const int kb = blockIdx.x * kKvBK;
   if (kb >= seqlen) return;
   const int group = P.hq / P.hkv;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const int key = kb + 32 * w + r;  // this lane's key (sequence-relative)
+  const int wkey0 = kb + 32 * w;
+  const int key = wkey0 + r;
 
-  // K block -> LDS (used by S and dQ); V rows for this lane's key -> registers (dP B operand).
   {
-    Stager<kBwdBK, D, 256> stk;
-    stk.load(P.k + (int64_t)(s0 + kb) * P.sk + (int64_t)kvh * D, P.sk, seqlen - kb);
-    stk.store(Kl);
+    Stager<kKvBK, D, 256> st;
+    st.load(P.k + (int64_t)(s0 + kb) * P.sk + (int64_t)kvh * D, P.sk, seqlen - kb);
+    st.store(smem);
+    st.load(P.v + (int64_t)(s0 + kb) * P.sv + (int64_t)kvh * D, P.sv, seqlen - kb);
+    st.store(smem + KV);
   }
-  bf16x8 vf[NC];
-  {
-    const bool ok = key < seqlen;
-    const uint16_t* vp = P.v + (int64_t)(s0 + (ok ? key : 0)) * P.sv + (int64_t)kvh * D + 8 * h;
+  int roff[NC], toa[ND], tob[ND];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      u16x8 t = ok ? *reinterpret_cast<const u16x8*>(vp + 16 * c) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      vf[c] = __builtin_bit_cast(bf16x8, t);
-    }
-  }
+  for (int c = 0; c < NC; ++c) roff[c] = off<D>(r, 2 * c + h);  // rows r (+32w for K/V)
+#pragma unroll
+  for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
 
   f32x16 dk[ND], dv[ND];
 #pragma unroll
@@ -353,34 +538,29 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_kernel(BwdParams P)
     dv[i] = f32x16{};
   }
 
-  const int first_slice = CAUSAL ? (kb / kBwdBQ) : 0;
-  const int nslices_q = (seqlen + kBwdBQ - 1) / kBwdBQ;
-  const int per_head = nslices_q - first_slice;
+  const int first_slice = CAUSAL ? (kb / kKvBQ) : 0;
+  const int per_head = (seqlen + kKvBQ - 1) / kKvBQ - first_slice;
   const int nitems = per_head * group;
+  const float inv_scale = 1.f / P.scale;
 
-  auto item_rows = [&](int it, int& hqi, int& qs) {
-    hqi = kvh * group + it / per_head;
-    qs = (first_slice + it % per_head) * kBwdBQ;
-  };
-
-  Stager<kBwdBQ, D, 256> sq, sdo;
-  float rc = 0.f;  // lse2 / delta prefetch for threads 0..63
+  Stager<kKvBQ, D, 256> sq, sdo;
+  float rc = 0.f;
   auto load_item = [&](int it) {
-    int hqi, qs;
-    item_rows(it, hqi, qs);
+    const int hqi = kvh * group + it / per_head;
+    const int qs = (first_slice + it % per_head) * kKvBQ;
     const int nv = seqlen - qs;
     sq.load(P.q + (int64_t)(s0 + qs) * P.sq + (int64_t)hqi * D, P.sq, nv);
     sdo.load(P.dout + ((int64_t)(s0 + qs) * P.hq + hqi) * D, (int64_t)P.hq * D, nv);
     if (threadIdx.x < 64) {
       const int qi = qs + (threadIdx.x & 31);
       const bool ok = qi < seqlen;
-      if (threadIdx.x < 32) rc = ok ? P.lse[(int64_t)hqi * P.T + s0 + qi] * kLog2e : 0.f;
-      else rc = ok ? P.delta[(int64_t)hqi * P.T + s0 + qi] : 0.f;
+      if (threadIdx.x < 32) rc = ok ? -P.lse[(int64_t)hqi * P.T + s0 + qi] * inv_scale : 0.f;
+      else rc = ok ? -P.delta[(int64_t)hqi * P.T + s0 + qi] : 0.f;
     }
   };
   auto store_item = [&](int buf) {
-    sq.store(qbuf(buf));
-    sdo.store(dobuf(buf));
+    sq.store(qd + buf * 2 * SLICE);
+    sdo.store(qd + buf * 2 * SLICE + SLICE);
     if (threadIdx.x < 64) rowc[buf * 64 + threadIdx.x] = rc;
   };
 
@@ -394,69 +574,67 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_kernel(BwdParams P)
     const int buf = it & 1;
     const bool more = it + 1 < nitems;
     if (more) load_item(it + 1);
-    int hqi, qs;
-    item_rows(it, hqi, qs);
-    const char* Ql = qbuf(buf);
-    const char* dOl = dobuf(buf);
-    const float* lse2 = rowc + buf * 64;
-    const float* dlt = lse2 + 32;
-
-    f32x16 s = f32x16{}, dp = f32x16{};
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      s = mfma(row_frag<D>(Ql, r, 2 * c + h), row_frag<D>(Kl, 32 * w + r, 2 * c + h), s);
-      dp = mfma(row_frag<D>(dOl, r, 2 * c + h), vf[c], dp);
-    }
-    // P and dS (key on the lane, query rows in the registers).
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qr = acc_row(i, h);
-      const int qi = qs + qr;
-      const bool valid = (qi < seqlen) && (key < seqlen) && (!CAUSAL || key <= qi);
-      const float p = valid ? exp2f(s[i] * P.c2 - lse2[qr]) : 0.f;
-      s[i] = p;
-      dp[i] = p * (dp[i] - dlt[qr]) * P.scale;
-    }
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const bf16x8 pf = pack8(s, st);
-      const bf16x8 dsf = pack8(dp, st);
-      const int ra = 16 * st + 4 * h;
-#pragma unroll
-      for (int d = 0; d < ND; ++d) {
-        dv[d] = mfma(tr_frag<D>(dOl, ra, ra + 8, 32 * d), pf, dv[d]);
-        dk[d] = mfma(tr_frag<D>(Ql, ra, ra + 8, 32 * d), dsf, dk[d]);
-      }
-    }
-    // dS^T -> LDS image [128 keys][32 q]: this lane's key row, 4 groups of 4 queries.
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      ushort4 v;
-      v.x = f2bf(dp[4 * g4 + 0]);
-      v.y = f2bf(dp[4 * g4 + 1]);
-      v.z = f2bf(dp[4 * g4 + 2]);
-      v.w = f2bf(dp[4 * g4 + 3]);
-      *reinterpret_cast<ushort4*>(dSl + off<kBwdBQ>(32 * w + r, g4) + 8 * h) = v;
-    }
-    __syncthreads();
-    // dQ[q][d] = sum_key dS[q][key] K[key][d]; wave -> (d tile, key range).
+    const int qs = (first_slice + it % per_head) * kKvBQ;
+    // No skip of the (at most 3 per head) slices whose queries all precede this wave's keys:
+    // a branch around the dK/dV updates makes hipcc carry the accumulators through VGPR copies
+    // every item; the mask zeroes those slices' contributions instead.
     {
-      constexpr int KSPLIT = 4 / ND;  // waves sharing one d tile split the keys
-      const int dt = w % ND;
-      const int kpart = w / ND;
-      constexpr int KPER = kBwdBK / KSPLIT;
-      f32x16 q = f32x16{};
-#pragma unroll
-      for (int st = 0; st < KPER / 16; ++st) {
-        const int k0 = kpart * KPER + 16 * st + 8 * h;
-        q = mfma(tr_frag<kBwdBQ>(dSl, k0, k0 + 4, 0), tr_frag<D>(Kl, k0, k0 + 4, 32 * dt), q);
-      }
-      float* dqp = P.dq + (int64_t)(s0 + qs) * P.hq * D + (int64_t)hqi * D + 32 * dt + r;
+      const char* Ql = qd + buf * 2 * SLICE;
+      const char* dOl = Ql + SLICE;
+      const float* c0 = rowc + buf * 64;
+      f32x16 s, dp;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int qr = acc_row(i, h);
-        if (qs + qr < seqlen) atomicAdd(dqp + (int64_t)qr * P.hq * D, q[i]);
+        s[i] = c0[acc_row(i, h)];
+        dp[i] = c0[32 + acc_row(i, h)];
       }
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        bf16x8 f[NC], g[NC], kf[NC], vf[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          f[c] = lds_frag(Ql + roff[c]);
+          kf[c] = lds_frag(Kl + 32 * w * RB + roff[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) s = mfma(f[c], kf[c], s);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          g[c] = lds_frag(dOl + roff[c]);
+          vf[c] = lds_frag(Vl + 32 * w * RB + roff[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) dp = mfma(g[c], vf[c], dp);
+      }
+      pipeline_reads<2 * NC, 2, 3>();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
+      if (CAUSAL && wkey0 + 31 > qs) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = (key > qs + acc_row(i, h)) ? 0.f : s[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dp[i] *= s[i];  // dS / scale
+      const bf16x8 pf[2] = {pack8(s, 0), pack8(s, 1)};
+      const bf16x8 dsf[2] = {pack8(dp, 0), pack8(dp, 1)};
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const char* ob = dOl + 16 * st * RB;
+        const char* qb = Ql + 16 * st * RB;
+        bf16x8 a[ND], b[ND];
+#pragma unroll
+        for (int d = 0; d < ND; ++d) a[d] = tr_frag_at(ob + toa[d], ob + tob[d]);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) dv[d] = mfma(a[d], pf[st], dv[d]);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) b[d] = tr_frag_at(qb + toa[d], qb + tob[d]);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) dk[d] = mfma(b[d], dsf[st], dk[d]);
+      }
+      pipeline_reads<4 * ND, 2, 3>();
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (more) store_item(buf ^ 1);
     __syncthreads();
@@ -470,8 +648,8 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_kernel(BwdParams P)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         ushort4 a, b;
-        a.x = f2bf(dk[d][4 * g4 + 0]); a.y = f2bf(dk[d][4 * g4 + 1]);
-        a.z = f2bf(dk[d][4 * g4 + 2]); a.w = f2bf(dk[d][4 * g4 + 3]);
+        a.x = f2bf(dk[d][4 * g4 + 0] * P.scale); a.y = f2bf(dk[d][4 * g4 + 1] * P.scale);
+        a.z = f2bf(dk[d][4 * g4 + 2] * P.scale); a.w = f2bf(dk[d][4 * g4 + 3] * P.scale);
         b.x = f2bf(dv[d][4 * g4 + 0]); b.y = f2bf(dv[d][4 * g4 + 1]);
         b.z = f2bf(dv[d][4 * g4 + 2]); b.w = f2bf(dv[d][4 * g4 + 3]);
         *reinterpret_cast<ushort4*>(dkp + 32 * d + 8 * g4 + 4 * h) = a;
@@ -479,208 +657,6 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_kernel(BwdParams P)
       }
     }
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Backward v2: 8 waves share one 256-key block (32 keys per wave, dK^T/dV^T in registers) and
-// sweep 64-row query items.  Per item: phase 1 computes S, dP (key on the lane), P, dS and the
-// dV^T/dK^T products and stores dS^T to LDS; phase 2 computes this item's dQ partial over all
-// 256 keys (one 32x32 tile per wave) and adds it with f32 atomics.  Compared with v1 the K/V
-// block and the Q/dO staging are shared by twice the waves (2 waves per SIMD instead of 1) and
-// the dQ atomic traffic per FLOP halves (256- instead of 128-key blocks).
-constexpr int kB2K = 256;  // keys per workgroup (8 waves x 32)
-constexpr int kB2Q = 64;   // query rows per item (2 x 32-row sub-tiles)
-constexpr int kB2Threads = 512;
-
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(kB2Threads, 2) void bwd2_kernel(BwdParams P) {
-  constexpr int NC = D / 16;
-  constexpr int ND = D / 32;
-  constexpr int KBYTES = kB2K * D * 2;
-  constexpr int QBYTES = kB2Q * D * 2;
-  constexpr int DSBYTES = kB2K * kB2Q * 2;  // dS^T image [256 keys][64 q]
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Kl = smem;
-  char* Ql = smem + KBYTES;
-  char* dOl = Ql + QBYTES;
-  char* dSl = dOl + QBYTES;
-  float* rowc = reinterpret_cast<float*>(dSl + DSBYTES);  // lse2[64], delta[64]
-
-  const int seq = blockIdx.z, kvh = blockIdx.y;
-  const int s0 = P.cu[seq];
-  const int seqlen = P.cu[seq + 1] - s0;
-  const int kb = blockIdx.x * kB2K;
-  if (kb >= seqlen) return;
-  const int group = P.hq / P.hkv;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int key = kb + 32 * w + r;
-
-  {
-    Stager<kB2K, D, kB2Threads> stk;
-    stk.load(P.k + (int64_t)(s0 + kb) * P.sk + (int64_t)kvh * D, P.sk, seqlen - kb);
-    stk.store(Kl);
-  }
-  bf16x8 vf[NC];
-  {
-    const bool ok = key < seqlen;
-    const uint16_t* vp = P.v + (int64_t)(s0 + (ok ? key : 0)) * P.sv + (int64_t)kvh * D + 8 * h;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      u16x8 t = ok ? *reinterpret_cast<const u16x8*>(vp + 16 * c) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      vf[c] = __builtin_bit_cast(bf16x8, t);
-    }
-  }
-  f32x16 dk[ND], dv[ND];
-#pragma unroll
-  for (int i = 0; i < ND; ++i) {
-    dk[i] = f32x16{};
-    dv[i] = f32x16{};
-  }
-
-  const int first_slice = CAUSAL ? (kb / kB2Q) : 0;
-  const int nslices = (seqlen + kB2Q - 1) / kB2Q;
-  const int per_head = nslices - first_slice;
-  const int nitems = per_head * group;
-  auto item = [&](int it, int& hqi, int& qs) {
-    hqi = kvh * group + it / per_head;
-    qs = (first_slice + it % per_head) * kB2Q;
-  };
-
-  Stager<kB2Q, D, kB2Threads> sq, sdo;
-  float rc = 0.f;
-  auto load_item = [&](int it) {
-    int hqi, qs;
-    item(it, hqi, qs);
-    const int nv = seqlen - qs;
-    sq.load(P.q + (int64_t)(s0 + qs) * P.sq + (int64_t)hqi * D, P.sq, nv);
-    sdo.load(P.dout + ((int64_t)(s0 + qs) * P.hq + hqi) * D, (int64_t)P.hq * D, nv);
-    if (threadIdx.x < 128) {
-      const int qi = qs + (threadIdx.x & 63);
-      const bool ok = qi < seqlen;
-      if (threadIdx.x < 64) rc = ok ? P.lse[(int64_t)hqi * P.T + s0 + qi] * kLog2e : 0.f;
-      else rc = ok ? P.delta[(int64_t)hqi * P.T + s0 + qi] : 0.f;
-    }
-  };
-  auto store_item = [&]() {
-    sq.store(Ql);
-    sdo.store(dOl);
-    if (threadIdx.x < 128) rowc[threadIdx.x] = rc;
-  };
-
-  if (nitems > 0) {
-    load_item(0);
-    store_item();
-  }
-  __syncthreads();
-
-  // dQ tile assignment: tiles = 2 q-subtiles x ND d-tiles; waves beyond split the keys.
-  constexpr int TILES = 2 * ND;
-  constexpr int KSPLIT = 8 / TILES;
-  constexpr int KPER = kB2K / KSPLIT;
-  const int tile = w % TILES, kpart = w / TILES;
-  const int tq = tile / ND, tdt = tile % ND;
-
-  for (int it = 0; it < nitems; ++it) {
-    const bool more = it + 1 < nitems;
-    if (more) load_item(it + 1);
-    int hqi, qs;
-    item(it, hqi, qs);
-    // ---------------- phase 1: per 32-row sub-tile, key on the lane (not unrolled: keeps one
-    // sub-tile's S/dP live at a time)
-#pragma unroll 1
-    for (int qt = 0; qt < 2; ++qt) {
-      const int qrow0 = qs + 32 * qt;
-      const bool skip = CAUSAL && (qrow0 + 31 < kb + 32 * w);  // all queries before all keys
-      f32x16 s = f32x16{}, dp = f32x16{};
-      if (!skip) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          s = mfma(row_frag<D>(Ql, 32 * qt + r, 2 * c + h), row_frag<D>(Kl, 32 * w + r, 2 * c + h), s);
-          dp = mfma(row_frag<D>(dOl, 32 * qt + r, 2 * c + h), vf[c], dp);
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qr = 32 * qt + acc_row(i, h);
-          const int qi = qs + qr;
-          const bool valid = (qi < seqlen) && (key < seqlen) && (!CAUSAL || key <= qi);
-          const float p = valid ? exp2f(s[i] * P.c2 - rowc[qr]) : 0.f;
-          s[i] = p;
-          dp[i] = p * (dp[i] - rowc[64 + qr]) * P.scale;
-        }
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8 pf = pack8(s, st);
-          const bf16x8 dsf = pack8(dp, st);
-          const int ra = 32 * qt + 16 * st + 4 * h;
-#pragma unroll
-          for (int d = 0; d < ND; ++d) {
-            dv[d] = mfma(tr_frag<D>(dOl, ra, ra + 8, 32 * d), pf, dv[d]);
-            dk[d] = mfma(tr_frag<D>(Ql, ra, ra + 8, 32 * d), dsf, dk[d]);
-          }
-        }
-      }
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        ushort4 v;
-        v.x = f2bf(dp[4 * g4 + 0]);
-        v.y = f2bf(dp[4 * g4 + 1]);
-        v.z = f2bf(dp[4 * g4 + 2]);
-        v.w = f2bf(dp[4 * g4 + 3]);
-        *reinterpret_cast<ushort4*>(dSl + off<kB2Q>(32 * w + r, 4 * qt + g4) + 8 * h) = v;
-      }
-    }
-    __syncthreads();
-    // ---------------- phase 2: next item's Q/dO go to LDS while this item's dQ is summed
-    if (more) store_item();
-    {
-      f32x16 q = f32x16{};
-#pragma unroll
-      for (int st = 0; st < KPER / 16; ++st) {
-        const int k0 = kpart * KPER + 16 * st + 8 * h;
-        q = mfma(tr_frag<kB2Q>(dSl, k0, k0 + 4, 32 * tq), tr_frag<D>(Kl, k0, k0 + 4, 32 * tdt), q);
-      }
-      const int qbase = qs + 32 * tq;
-      float* dqp = P.dq + (int64_t)(s0 + qbase) * P.hq * D + (int64_t)hqi * D + 32 * tdt + r;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qr = acc_row(i, h);
-        if (qbase + qr < seqlen) atomicAdd(dqp + (int64_t)qr * P.hq * D, q[i]);
-      }
-    }
-    __syncthreads();
-  }
-
-  if (key < seqlen) {
-    uint16_t* dkp = P.dk + (int64_t)(s0 + key) * P.sdk + (int64_t)kvh * D;
-    uint16_t* dvp = P.dv + (int64_t)(s0 + key) * P.sdv + (int64_t)kvh * D;
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        ushort4 a, b;
-        a.x = f2bf(dk[d][4 * g4 + 0]); a.y = f2bf(dk[d][4 * g4 + 1]);
-        a.z = f2bf(dk[d][4 * g4 + 2]); a.w = f2bf(dk[d][4 * g4 + 3]);
-        b.x = f2bf(dv[d][4 * g4 + 0]); b.y = f2bf(dv[d][4 * g4 + 1]);
-        b.z = f2bf(dv[d][4 * g4 + 2]); b.w = f2bf(dv[d][4 * g4 + 3]);
-        *reinterpret_cast<ushort4*>(dkp + 32 * d + 8 * g4 + 4 * h) = a;
-        *reinterpret_cast<ushort4*>(dvp + 32 * d + 8 * g4 + 4 * h) = b;
-      }
-    }
-  }
-}
-
-// dq f32 [T, W] (contiguous) -> bf16 destination rows with token stride `ld` (W % 8 == 0).
-__global__ void f32_to_bf16_rows_kernel(const float* __restrict__ in, uint16_t* __restrict__ out,
-                                        int64_t T, int W, int64_t ld) {
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (i >= T * W) return;
-  const int64_t t = i / W;
-  const int c = i % W;
-  const float4 a = reinterpret_cast<const float4*>(in + i)[0];
-  const float4 b = reinterpret_cast<const float4*>(in + i)[1];
-  float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  store8(out + t * ld + c, v);
 }
 
 }  // namespace fa
@@ -761,50 +737,40 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
     dv.zero_();
     return;
   }
-  auto dq32 = at::zeros({T, hq, D}, opts.dtype(at::kFloat));
   auto delta = at::empty({hq, T}, opts.dtype(at::kFloat));
+  fa::BwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), bf16_ptr(dout), bf16_ptr(o), q.stride(0), k.stride(0),
+                  v.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), bf16_mut(dq), bf16_mut(dk),
+                  bf16_mut(dv), dq.stride(0), dk.stride(0), dv.stride(0), cu_seqlens.data_ptr<int>(), T, (int)hq,
+                  (int)hkv, (float)scale, (float)(scale * fa::kLog2e)};
+  // Waves per SIMD of the dq kernel at head_dim 128 (DTG_FA_OCC=1|2; measured in profiles/).
+  static const int occ = [] {
+    const char* e = std::getenv("DTG_FA_OCC");
+    return (e != nullptr && e[0] == '2') ? 2 : 1;
+  }();
   {
-    const int64_t rows = T * hq;
-    const int blocks = (rows + 3) / 4;
-    if (D == 128) fa::bwd_pre_kernel<128><<<blocks, 256, 0, stream()>>>(bf16_ptr(o), bf16_ptr(dout), delta.data_ptr<float>(), T, hq);
-    else fa::bwd_pre_kernel<64><<<blocks, 256, 0, stream()>>>(bf16_ptr(o), bf16_ptr(dout), delta.data_ptr<float>(), T, hq);
+    dim3 grid((max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ, hq, nseq);
+    const size_t lds = 4 * fa::kDqBK * D * 2;
+#define DTG_BWD_DQ(DD, C, O)                                                              \
+  do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O>, lds);                        \
+       hipLaunchKernelGGL((fa::bwd_dq_kernel<DD, C, O>), grid, dim3(256), lds, stream(), P); } while (0)
+    if (D == 128) {
+      if (occ == 2) { if (causal) DTG_BWD_DQ(128, true, 2); else DTG_BWD_DQ(128, false, 2); }
+      else { if (causal) DTG_BWD_DQ(128, true, 1); else DTG_BWD_DQ(128, false, 1); }
+    } else { if (causal) DTG_BWD_DQ(64, true, 2); else DTG_BWD_DQ(64, false, 2); }
+#undef DTG_BWD_DQ
     DTG_LAUNCH_CHECK();
   }
-  fa::BwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), bf16_ptr(dout), q.stride(0), k.stride(0),
-                  v.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), dq32.data_ptr<float>(),
-                  bf16_mut(dk), bf16_mut(dv), dk.stride(0), dv.stride(0), cu_seqlens.data_ptr<int>(), T,
-                  (int)hq, (int)hkv, (float)scale, (float)(scale * fa::kLog2e)};
-  // v1 (4 waves x 32 keys, 1 wave/SIMD) is the default; DTG_FA_BWD=2 selects the experimental
-  // 8-wave variant (register-bound at head_dim 128: spills, see profiles/).
-  static const bool use_v1 = [] {
-    const char* e = std::getenv("DTG_FA_BWD");
-    return !(e != nullptr && e[0] == '2');
-  }();
-  if (use_v1) {
-    dim3 grid((max_seqlen + fa::kBwdBK - 1) / fa::kBwdBK, hkv, nseq);
-    const size_t lds = fa::kBwdBK * D * 2 + 4 * fa::kBwdBQ * D * 2 + fa::kBwdBK * fa::kBwdBQ * 2 + 2 * 64 * 4;
-#define DTG_BWD(DD, C)                                                                    \
-  do { set_lds_limit((const void*)&fa::bwd_kernel<DD, C>, lds);                              \
-       hipLaunchKernelGGL((fa::bwd_kernel<DD, C>), grid, dim3(256), lds, stream(), P); } while (0)
-    if (D == 128) { if (causal) DTG_BWD(128, true); else DTG_BWD(128, false); }
-    else { if (causal) DTG_BWD(64, true); else DTG_BWD(64, false); }
-#undef DTG_BWD
-  } else {
-    dim3 grid((max_seqlen + fa::kB2K - 1) / fa::kB2K, hkv, nseq);
-    const size_t lds = fa::kB2K * D * 2 + 2 * fa::kB2Q * D * 2 + fa::kB2K * fa::kB2Q * 2 + 128 * 4;
-#define DTG_BWD2(DD, C)                                                                   \
-  do { set_lds_limit((const void*)&fa::bwd2_kernel<DD, C>, lds);                             \
-       hipLaunchKernelGGL((fa::bwd2_kernel<DD, C>), grid, dim3(fa::kB2Threads), lds, stream(), P); } while (0)
-    if (D == 128) { if (causal) DTG_BWD2(128, true); else DTG_BWD2(128, false); }
-    else { if (causal) DTG_BWD2(64, true); else DTG_BWD2(64, false); }
-#undef DTG_BWD2
+  {
+    dim3 grid((max_seqlen + fa::kKvBK - 1) / fa::kKvBK, hkv, nseq);
+    const size_t lds = 2 * fa::kKvBK * D * 2 + 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
+#define DTG_BWD_KV(DD, C)                                                                 \
+  do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C>, lds);                         \
+       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C>), grid, dim3(256), lds, stream(), P); } while (0)
+    if (D == 128) { if (causal) DTG_BWD_KV(128, true); else DTG_BWD_KV(128, false); }
+    else { if (causal) DTG_BWD_KV(64, true); else DTG_BWD_KV(64, false); }
+#undef DTG_BWD_KV
+    DTG_LAUNCH_CHECK();
   }
-  DTG_LAUNCH_CHECK();
-  const int W = hq * D;
-  const int64_t n = T * W;
-  fa::f32_to_bf16_rows_kernel<<<(n / 8 + 255) / 256, 256, 0, stream()>>>(dq32.data_ptr<float>(), bf16_mut(dq),
-                                                                          T, W, dq.stride(0));
-  DTG_LAUNCH_CHECK();
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(
