@@ -28,6 +28,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dtg {
 namespace fa {
@@ -111,6 +112,9 @@ __device__ __forceinline__ void pipeline_reads() {
 
 // Row of accumulator register `reg` for lane half h (32x32 C/D map).
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+// The lane-independent part: acc_row(reg, h) == acc_row0(reg) + 4h, a compile-time constant, so
+// a mask test against a row becomes one compare with a per-lane threshold.
+constexpr int acc_row0(int reg) { return (reg & 3) + 8 * (reg >> 2); }
 
 // Buffer descriptor over `bytes` bytes at p, built from provably wave-uniform values (T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int bytes) {
@@ -160,6 +164,16 @@ __device__ __forceinline__ void load_row_frags(const uint16_t* row, bool ok, int
   }
 }
 
+// Grid order.  Workgroups are dispatched x-fastest and handed to the 8 XCDs round-robin, so
+//  * the block index goes in z (slowest) with the heaviest causal blocks first across ALL
+//    (head, sequence) pairs -- the tail of the launch is then made of the lightest blocks;
+//  * the head index x is permuted so that the query heads of one GQA group (which read the same
+//    K/V) land on the same XCD and share its L2: head = (x % hkv) * group + x / hkv.
+__device__ __forceinline__ int grid_head(int x, int hq, int hkv) {
+  const int group = hq / hkv;
+  return (x % hkv) * group + x / hkv;
+}
+
 struct FwdParams {
   const uint16_t *q, *k, *v;
   int64_t sq, sk, sv;  // token strides (elements)
@@ -182,10 +196,10 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   constexpr int ND = D / 32;  // 32-wide d tiles of the output
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1]
 
-  const int seq = blockIdx.z, head = blockIdx.y;
+  const int seq = blockIdx.y, head = grid_head(blockIdx.x, P.hq, P.hkv);
   const int s0 = P.cu[seq];
   const int seqlen = P.cu[seq + 1] - s0;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;  // heavy blocks first
+  const int qb = CAUSAL ? (gridDim.z - 1 - blockIdx.z) : blockIdx.z;  // heavy blocks first
   const int q0 = qb * kFwdBQ;
   if (q0 >= seqlen) return;
   const int kvh = head / (P.hq / P.hkv);
@@ -219,7 +233,9 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   __syncthreads();
 
   const int wave_q0 = q0 + 32 * w, wave_qmax = wave_q0 + 31;
-  for (int t = 0; t < ntiles; ++t) {
+  // Tile loop unrolled by two so the double-buffer offsets are compile-time immediates.
+  auto tile_step = [&](int t, auto buf) {
+    constexpr int B = decltype(buf)::value;
     const int kt0 = t * kFwdBK;
     const bool more = t + 1 < ntiles;
     if (more) {
@@ -227,7 +243,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       sk.load(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk);
       sv.load(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk);
     }
-    const char* K = smem + (t & 1) * 2 * TILE;
+    const char* K = smem + B * 2 * TILE;
     const char* V = K + TILE;
     if (!CAUSAL || kt0 <= wave_qmax) {  // wave-uniform skip of tiles above the diagonal
       f32x16 s[2];
@@ -246,12 +262,10 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       if ((CAUSAL && kt0 + kFwdBK - 1 > wave_q0) || kt0 + kFwdBK > seqlen) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
+          // key = kt0 + 32 kt + acc_row is masked when key > min(qrow, seqlen - 1)
+          const int lim = (CAUSAL ? min(qrow, seqlen - 1) : seqlen - 1) - (kt0 + 32 * kt + 4 * h);
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = kt0 + kt * 32 + acc_row(i, h);
-            const bool bad = (key >= seqlen) | (CAUSAL & (key > qrow));
-            s[kt][i] = bad ? -INFINITY : s[kt][i];
-          }
+          for (int i = 0; i < 16; ++i) s[kt][i] = acc_row0(i) > lim ? -INFINITY : s[kt][i];
         }
       }
       float mx = s[0][0];
@@ -298,12 +312,18 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       __builtin_amdgcn_sched_barrier(0);
     }
     if (more) {
-      char* nb = smem + ((t + 1) & 1) * 2 * TILE;
+      char* nb = smem + (1 - B) * 2 * TILE;
       sk.store(nb);
       sv.store(nb + TILE);
     }
     __syncthreads();
+  };
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    tile_step(t, std::integral_constant<int, 0>{});
+    tile_step(t + 1, std::integral_constant<int, 1>{});
   }
+  if (t < ntiles) tile_step(t, std::integral_constant<int, 0>{});
 
   const float lt = l + __shfl_xor(l, 32, 64);
   if (qrow < seqlen) {
@@ -353,10 +373,10 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   constexpr int ND = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1]
 
-  const int seq = blockIdx.z, head = blockIdx.y;
+  const int seq = blockIdx.y, head = grid_head(blockIdx.x, P.hq, P.hkv);
   const int s0 = P.cu[seq];
   const int seqlen = P.cu[seq + 1] - s0;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;  // heavy blocks first
+  const int qb = CAUSAL ? (gridDim.z - 1 - blockIdx.z) : blockIdx.z;  // heavy blocks first
   const int q0 = qb * kDqBQ;
   if (q0 >= seqlen) return;
   const int kvh = head / (P.hq / P.hkv);
@@ -407,7 +427,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   __syncthreads();
 
   const int wave_q0 = q0 + 32 * w, wave_qmax = wave_q0 + 31;
-  for (int t = 0; t < ntiles; ++t) {
+  // Tile loop unrolled by two so the double-buffer offsets are compile-time immediates.
+  auto tile_step = [&](int t, auto buf) {
+    constexpr int B = decltype(buf)::value;
     const int kt0 = t * kDqBK;
     const bool more = t + 1 < ntiles;
     if (more) {
@@ -415,7 +437,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
       sk.load(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk);
       sv.load(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk);
     }
-    const char* K = smem + (t & 1) * 2 * TILE;
+    const char* K = smem + B * 2 * TILE;
     const char* V = K + TILE;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -440,12 +462,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = fexp2(__builtin_fmaf(s[i], P.c2, -lse2));
       if ((CAUSAL && key0 + 31 > wave_q0) || key0 + 32 > seqlen) {
+        const int lim = (CAUSAL ? min(qrow, seqlen - 1) : seqlen - 1) - (key0 + 4 * h);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = key0 + acc_row(i, h);
-          const bool bad = (key >= seqlen) | (CAUSAL & (key > qrow));
-          s[i] = bad ? 0.f : s[i];
-        }
+        for (int i = 0; i < 16; ++i) s[i] = acc_row0(i) > lim ? 0.f : s[i];
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] *= dp[i] - delta;  // dS^T / scale
@@ -464,12 +483,18 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
       __builtin_amdgcn_sched_barrier(0);
     }
     if (more) {
-      char* nb = smem + ((t + 1) & 1) * 2 * TILE;
+      char* nb = smem + (1 - B) * 2 * TILE;
       sk.store(nb);
       sv.store(nb + TILE);
     }
     __syncthreads();
+  };
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    tile_step(t, std::integral_constant<int, 0>{});
+    tile_step(t + 1, std::integral_constant<int, 1>{});
   }
+  if (t < ntiles) tile_step(t, std::integral_constant<int, 0>{});
 
   if (qok) {
     uint16_t* op = P.dq + (int64_t)(s0 + qrow) * P.sdq + (int64_t)head * D;
@@ -488,29 +513,26 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   }
 }
 
-// dK, dV, key-stationary: 4 waves x 32 keys; the block's K and V rows sit in LDS (B operands of
-// S = Q K^T and dP = dO V^T; holding them in registers instead pushes the wave past 256 VGPRs
-// and hipcc then shuffles the dK/dV accumulators through AGPRs every item), and the workgroup
-// sweeps (query head, 32-row slice) items with Q/dO double-buffered in LDS.  S and dP start from the row constants
+// dK, dV, key-stationary: 4 waves x 32 keys, one wave per SIMD with the dK/dV accumulators in
+// AGPRs; this lane's K and V rows live in VGPRs (they are the B operands of S = Q K^T and
+// dP = dO V^T), and the workgroup sweeps (query head, 32-row slice) items with Q/dO
+// double-buffered in LDS.  S and dP start from the row constants
 // (-lse/scale, -delta) so p = exp2(c2 S') and dS = p dP' need no per-element subtraction;
 // only the causal diagonal is masked (padded query rows carry Q = dO = 0 and contribute 0).
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdParams P) {
+__global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int NC = D / 16;
   constexpr int ND = D / 32;
   constexpr int SLICE = kKvBQ * RB;
-  constexpr int KV = kKvBK * RB;
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // [K | V | Q0 | dO0 | Q1 | dO1 | rowc]
-  const char* Kl = smem;
-  const char* Vl = smem + KV;
-  char* qd = smem + 2 * KV;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [Q0 | dO0 | Q1 | dO1 | rowc]
+  char* qd = smem;
   float* rowc = reinterpret_cast<float*>(qd + 4 * SLICE);      // [2][-lse/scale x32, -delta x32]
 
-  const int seq = blockIdx.z, kvh = blockIdx.y;
+  const int seq = blockIdx.y, kvh = blockIdx.x;
   const int s0 = P.cu[seq];
   const int seqlen = P.cu[seq + 1] - s0;
-  const int kb = blockIdx.x * kKvBK;
+  const int kb = blockIdx.z * kKvBK;  // z = 0 first: the heaviest causal key blocks
   if (kb >= seqlen) return;
   const int group = P.hq / P.hkv;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -518,16 +540,16 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdParams P) {
   const int wkey0 = kb + 32 * w;
   const int key = wkey0 + r;
 
+  bf16x8 kf[NC], vf[NC];
   {
-    Stager<kKvBK, D, 256> st;
-    st.load(P.k + (int64_t)(s0 + kb) * P.sk + (int64_t)kvh * D, P.sk, seqlen - kb);
-    st.store(smem);
-    st.load(P.v + (int64_t)(s0 + kb) * P.sv + (int64_t)kvh * D, P.sv, seqlen - kb);
-    st.store(smem + KV);
+    const bool ok = key < seqlen;
+    const int64_t t = s0 + (ok ? key : seqlen - 1);
+    load_row_frags<NC>(P.k + t * P.sk + (int64_t)kvh * D, ok, h, kf);
+    load_row_frags<NC>(P.v + t * P.sv + (int64_t)kvh * D, ok, h, vf);
   }
   int roff[NC], toa[ND], tob[ND];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) roff[c] = off<D>(r, 2 * c + h);  // rows r (+32w for K/V)
+  for (int c = 0; c < NC; ++c) roff[c] = off<D>(r, 2 * c + h);
 #pragma unroll
   for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
 
@@ -590,29 +612,24 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdParams P) {
       }
       __builtin_amdgcn_sched_barrier(0);
       {
-        bf16x8 f[NC], g[NC], kf[NC], vf[NC];
+        bf16x8 f[NC], g[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          f[c] = lds_frag(Ql + roff[c]);
-          kf[c] = lds_frag(Kl + 32 * w * RB + roff[c]);
-        }
+        for (int c = 0; c < NC; ++c) f[c] = lds_frag(Ql + roff[c]);
 #pragma unroll
         for (int c = 0; c < NC; ++c) s = mfma(f[c], kf[c], s);
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          g[c] = lds_frag(dOl + roff[c]);
-          vf[c] = lds_frag(Vl + 32 * w * RB + roff[c]);
-        }
+        for (int c = 0; c < NC; ++c) g[c] = lds_frag(dOl + roff[c]);
 #pragma unroll
         for (int c = 0; c < NC; ++c) dp = mfma(g[c], vf[c], dp);
       }
-      pipeline_reads<2 * NC, 2, 3>();
+      pipeline_reads<2 * NC, 1, 4>();
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
       if (CAUSAL && wkey0 + 31 > qs) {
+        const int lim = key - qs - 4 * h;  // query row qs + acc_row < key is masked
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = (key > qs + acc_row(i, h)) ? 0.f : s[i];
+        for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) < lim) ? 0.f : s[i];
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) dp[i] *= s[i];  // dS / scale
@@ -693,7 +710,8 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   fa::FwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), q.stride(0), k.stride(0), v.stride(0),
                   bf16_mut(o), lse.data_ptr<float>(), cu_seqlens.data_ptr<int>(), T, (int)hq, (int)hkv,
                   (float)(scale * fa::kLog2e)};
-  dim3 grid((max_seqlen + fa::kFwdBQ - 1) / fa::kFwdBQ, hq, nseq);
+  DTG_CHECK(nseq <= 65535, "flash_attn: at most 65535 sequences per call");
+  dim3 grid(hq, nseq, (max_seqlen + fa::kFwdBQ - 1) / fa::kFwdBQ);
   const size_t lds = 4 * fa::kFwdBK * D * 2;
 #define DTG_FWD(DD, C)                                                                    \
   do { set_lds_limit((const void*)&fa::fwd_kernel<DD, C>, lds);                              \
@@ -737,6 +755,7 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
     dv.zero_();
     return;
   }
+  DTG_CHECK(nseq <= 65535, "flash_attn: at most 65535 sequences per call");
   auto delta = at::empty({hq, T}, opts.dtype(at::kFloat));
   fa::BwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), bf16_ptr(dout), bf16_ptr(o), q.stride(0), k.stride(0),
                   v.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), bf16_mut(dq), bf16_mut(dk),
@@ -748,7 +767,7 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
     return (e != nullptr && e[0] == '2') ? 2 : 1;
   }();
   {
-    dim3 grid((max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ, hq, nseq);
+    dim3 grid(hq, nseq, (max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ);
     const size_t lds = 4 * fa::kDqBK * D * 2;
 #define DTG_BWD_DQ(DD, C, O)                                                              \
   do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O>, lds);                        \
@@ -761,8 +780,8 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
     DTG_LAUNCH_CHECK();
   }
   {
-    dim3 grid((max_seqlen + fa::kKvBK - 1) / fa::kKvBK, hkv, nseq);
-    const size_t lds = 2 * fa::kKvBK * D * 2 + 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
+    dim3 grid(hkv, nseq, (max_seqlen + fa::kKvBK - 1) / fa::kKvBK);
+    const size_t lds = 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
 #define DTG_BWD_KV(DD, C)                                                                 \
   do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C>, lds);                         \
        hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C>), grid, dim3(256), lds, stream(), P); } while (0)

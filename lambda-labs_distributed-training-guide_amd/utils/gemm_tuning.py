@@ -18,6 +18,16 @@ def enable_tunableop(tune: bool = False, max_tuning_ms: int = 30, table: str = T
     os.makedirs(os.path.dirname(table), exist_ok=True)
     t = torch.cuda.tunable
     t.enable(True)
+    if not tune:
+        # Read-only use: point TunableOp's own results file at a per-process scratch copy so
+        # that no rank can rewrite the committed table at exit (8 ranks, one file).
+        import shutil
+        import tempfile
+
+        scratch = os.path.join(tempfile.gettempdir(), f"dtg_tunableop_{os.getpid()}.csv")
+        if os.path.exists(table):
+            shutil.copyfile(table, scratch)
+        table = scratch
     t.set_filename(table, insert_device_ordinal=False)
     t.tuning_enable(tune)
     if tune:

@@ -1,5 +1,6 @@
 """T5: fault injection + torchrun elastic restart resumes from persisted state."""
 import json
+import re
 import os
 import subprocess
 import sys
@@ -15,16 +16,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_toy_restarts_and_resumes(tmp_path):
     state = tmp_path / "toy-state.json"
     err = tmp_path / "error.json"
-    env = dict(os.environ, TORCHELASTIC_ERROR_FILE=str(err), OMP_NUM_THREADS="1")
+    # lo + extra restarts: a gloo full-mesh reconnect after a restart occasionally times out in
+    # this container; the test is about resuming from persisted state, not about gloo.
+    env = dict(os.environ, TORCHELASTIC_ERROR_FILE=str(err), OMP_NUM_THREADS="1", GLOO_SOCKET_IFNAME="lo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-           "--max-restarts", "2", "--rdzv-backend", "c10d", "--rdzv-endpoint", f"127.0.0.1:{free_port()}",
+           "--max-restarts", "4", "--rdzv-backend", "c10d", "--rdzv-endpoint", f"127.0.0.1:{free_port()}",
            os.path.join(ROOT, "related-topics", "elastic-training", "toy.py"), "--steps", "40", "--fail-prob", "0",
            "--fail-at-step", "15", "--state", str(state)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
-    assert "deterministic failure at step 15" in out
-    assert "starting at step 15 (restart count 1)" in out
+    starts = [ln for ln in out.splitlines() if "starting at step" in ln]
+    assert "deterministic failure at step 15" in out, out[-3000:]
+    # resumed from the persisted step on a restart (count >= 1: a restart whose gloo mesh
+    # failed to connect is retried by torchrun and does not reach this line)
+    assert any(re.search(r"starting at step 15 \(restart count [1-9]\)", ln) for ln in starts), starts
     assert json.loads(state.read_text())["num_steps"] == 40
 
 
