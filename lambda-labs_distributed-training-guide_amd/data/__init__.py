@@ -43,21 +43,48 @@ def seed_worker(worker_id):
     random.seed(s)
 
 
+class ResumableSampler(torch.utils.data.Sampler):
+    """Epoch-seeded sharded order (DistributedSampler semantics, also for one rank) that can
+    start part-way through an epoch: `skip` samples of this rank's order are not yielded, so a
+    resumed run continues the same data order without loading and collating the consumed
+    batches (the reference re-reads them)."""
+
+    def __init__(self, dataset, num_replicas: int = 1, rank: int = 0, shuffle: bool = True, drop_last: bool = True,
+                 seed: int = 0):
+        self.base = DistributedSampler(dataset, num_replicas=num_replicas, rank=rank, shuffle=shuffle,
+                                       drop_last=drop_last, seed=seed)
+        self.skip = 0
+
+    def set_epoch(self, epoch: int, skip: int = 0):
+        self.base.set_epoch(epoch)
+        self.skip = skip
+
+    def full_len(self) -> int:
+        return len(self.base)
+
+    def __len__(self):
+        return max(0, len(self.base) - self.skip)
+
+    def __iter__(self):
+        it = iter(self.base)
+        for _ in range(self.skip):
+            next(it, None)
+        return it
+
+
 def build_dataloader(dataset, batch_size: int, collate_fn, *, dp_size: int = 1, dp_rank: int = 0, shuffle: bool = True,
                      drop_last: bool = True, num_workers: int = 1, prefetch_factor: int = 2, seed: int = 0,
                      pin_memory: bool = True):
-    sampler = None
-    if dp_size > 1:
-        sampler = DistributedSampler(dataset, num_replicas=dp_size, rank=dp_rank, shuffle=shuffle, drop_last=drop_last, seed=seed)
+    sampler = ResumableSampler(dataset, num_replicas=dp_size, rank=dp_rank, shuffle=shuffle, drop_last=drop_last,
+                               seed=seed)
     g = torch.Generator()
     g.manual_seed(seed)
     kw = {}
     if num_workers > 0:
         kw = dict(prefetch_factor=prefetch_factor, worker_init_fn=seed_worker, persistent_workers=False)
-    return DataLoader(dataset, batch_size=batch_size, sampler=sampler, shuffle=(shuffle and sampler is None),
-                      drop_last=drop_last, collate_fn=collate_fn, num_workers=num_workers, generator=g,
-                      pin_memory=pin_memory and torch.cuda.is_available(), **kw)
+    return DataLoader(dataset, batch_size=batch_size, sampler=sampler, drop_last=drop_last, collate_fn=collate_fn,
+                      num_workers=num_workers, generator=g, pin_memory=pin_memory and torch.cuda.is_available(), **kw)
 
 
-__all__ = ["PackedCollator", "dense_collate", "packed_position_ids", "SyntheticPacked", "SyntheticTokens",
+__all__ = ["ResumableSampler", "PackedCollator", "dense_collate", "packed_position_ids", "SyntheticPacked", "SyntheticTokens",
            "build_dataset", "build_dataloader", "seed_worker"]

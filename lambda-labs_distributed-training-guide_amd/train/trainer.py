@@ -213,12 +213,14 @@ def run(chapter: str, argv=None):
     model.train()
     for state["epoch"] in range(state["epoch"], args.num_epochs):
         LOGGER.info(f"Begin epoch {state['epoch']} at step {state['epoch_step']}")
-        sampler = getattr(dataloader, "sampler", None)
-        if hasattr(sampler, "set_epoch"):
-            sampler.set_epoch(state["epoch"])  # every chapter (06/07 forgot it: SURVEY §2.11 #3)
+        sampler = dataloader.sampler
+        # every chapter sets the epoch (06/07 forgot it: SURVEY §2.11 #3); a resumed epoch starts
+        # at its first unconsumed sample instead of re-reading the consumed batches
+        per_step = args.batch_size * accum
+        sampler.set_epoch(state["epoch"], skip=state["epoch_step"] * per_step)
         batches = iter(dataloader)
-        n_steps = len(dataloader) // accum
-        for i_step in range(n_steps):
+        n_steps = (sampler.full_len() // args.batch_size) // accum
+        for i_step in range(state["epoch_step"], n_steps):
             micro = []
             with timers["data"], torch.no_grad():
                 for _ in range(accum):
@@ -232,8 +234,6 @@ def run(chapter: str, argv=None):
                     if mx is not None:
                         b["max_seqlen"] = mx
                     micro.append(b)
-            if i_step < state["epoch_step"]:
-                continue  # resume: data already consumed (order preserved)
             if args.fault_inject_prob > 0 and fault_rng.random() < args.fault_inject_prob:
                 raise RuntimeError(f"injected fault at global step {state['global_step']} on rank {rank}")
             opt.zero_grad(set_to_none=True)

@@ -70,3 +70,19 @@ def test_hf_text_pipeline_groups_texts(tmp_path):
     # seq_length None -> tokenizer max clamped to min(1024, max_position_embeddings)
     _, seq2, _ = build_dataset(str(f), tokenizer_name=tok, seq_length=None, vocab_size=16, max_position_embeddings=256)
     assert seq2 == 256
+
+
+def test_resumable_sampler_skips_consumed_samples():
+    """Resume mid-epoch: the order continues exactly where it stopped, for one rank and for a
+    shard of several, without re-reading the consumed samples."""
+    from dtg.data import ResumableSampler
+
+    ds = list(range(103))
+    for world, rank in ((1, 0), (4, 2)):
+        s = ResumableSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=5)
+        s.set_epoch(3)
+        full = list(s)
+        s.set_epoch(3, skip=10)
+        assert list(s) == full[10:] and len(s) == len(full) - 10 and s.full_len() == len(full)
+        s.set_epoch(4)
+        assert list(s) != full and sorted(list(s)) != []
