@@ -51,6 +51,9 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     g = p.add_argument_group("dtg (MI355X) options")
     g.add_argument("--waiting-timers", default="off", choices=["on", "off"],
                    help="time a barrier before forward/backward/update (straggler detection)")
+    g.add_argument("--roctx", default="off", choices=["on", "off"], help="roctx ranges around the step phases")
+    g.add_argument("--torch-profile-steps", default=0, type=int,
+                   help="record N steps (after the first 3) with torch.profiler; chrome trace in the exp dir")
     g.add_argument("--sync-timers", default="on", choices=["on", "off"],
                    help="on: reference LocalTimer (device sync around every phase); off: HIP-event timers")
     g.add_argument("--grad-accum", default=1, type=int, help="micro-batches per optimizer step (no_sync)")

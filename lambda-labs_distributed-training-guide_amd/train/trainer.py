@@ -197,7 +197,9 @@ def run(chapter: str, argv=None):
 
     waiting = getattr(args, "waiting_timers", "off") == "on" and world > 1
     names = ("data", "forward", "backward", "update") + (("waiting",) if waiting else ())
-    timers = make_timers(device, names=names, sync=args.sync_timers == "on")
+    timers = make_timers(device, names=names, sync=args.sync_timers == "on", ranges=args.roctx == "on")
+    prof = None
+    prof_start, prof_stop = 3, 3 + args.torch_profile_steps
 
     def wait_for_peers():
         # Straggler probe (related-topics/optimizing-data-loading): time spent in a barrier
@@ -254,6 +256,8 @@ def run(chapter: str, argv=None):
                 lr_scheduler.step()
             state["global_step"] += 1
             state["epoch_step"] += 1
+            if args.torch_profile_steps > 0:
+                prof = _profile_tick(prof, state["global_step"], prof_start, prof_stop, exp_dir, rank, device)
             state["running_loss"] += (loss_sum / accum).item()
 
             if state["global_step"] % args.log_freq == 0:
@@ -289,6 +293,23 @@ def run(chapter: str, argv=None):
                 return state
         state["epoch_step"] = 0
     return state
+
+
+def _profile_tick(prof, step, start, stop, exp_dir, rank, device):
+    """torch.profiler (ROCm kineto) over steps [start, stop): chrome trace per rank."""
+    if step == start and prof is None:
+        from torch.profiler import ProfilerActivity, profile
+
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if device.type == "cuda" else [])
+        prof = profile(activities=acts, record_shapes=True)
+        prof.__enter__()
+    elif step == stop and prof is not None:
+        prof.__exit__(None, None, None)
+        path = Path(exp_dir) / f"trace-rank{rank}.json"
+        prof.export_chrome_trace(str(path))
+        LOGGER.info(f"torch.profiler trace written to {path}")
+        prof = None
+    return prof
 
 
 class _null:

@@ -79,6 +79,32 @@ class EventTimer:
         self.done_ms = []
 
 
-def make_timers(device, names=("data", "forward", "backward", "update"), sync: bool = True):
+class _Ranged:
+    """Wraps a timer with a roctx range (torch.cuda.nvtx maps to roctx on ROCm), so phases show
+    up by name in rocprofv3 --marker-trace / Perfetto timelines."""
+
+    def __init__(self, timer, name: str):
+        self.timer, self.name = timer, name
+
+    def __enter__(self):
+        torch.cuda.nvtx.range_push(self.name)
+        self.timer.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self.timer.__exit__(*exc)
+        torch.cuda.nvtx.range_pop()
+
+    def avg_elapsed_ms(self):
+        return self.timer.avg_elapsed_ms()
+
+    def reset(self):
+        self.timer.reset()
+
+
+def make_timers(device, names=("data", "forward", "backward", "update"), sync: bool = True, ranges: bool = False):
     cls = LocalTimer if sync else EventTimer
-    return {k: cls(device) for k in names}
+    timers = {k: cls(device) for k in names}
+    if ranges and device.type == "cuda":
+        timers = {k: _Ranged(t, k) for k, t in timers.items()}
+    return timers
