@@ -28,6 +28,7 @@ _DEFS = [
     "int max_seqlen, float scale, bool causal) -> (Tensor, Tensor, Tensor)",
     "flash_attn_bwd_qkv(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
     "Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> Tensor",
+    "transpose2d(Tensor x) -> Tensor",
 ]
 
 for _d in _DEFS:

@@ -66,15 +66,23 @@ def notify_param(param):
     _mark(param)
 
 
-def route_weight_grad_mm(param, a, b):
-    """Weight gradient a^T @ b (a: [T, out], b: [T, in]) into main_grad without a temporary."""
+def route_weight_grad_mm(param, a, b, a_t=None, b_t=None):
+    """Weight gradient a^T @ b (a: [T, out], b: [T, in]) into main_grad without a temporary.
+
+    `a_t` / `b_t` are optional contiguous transposes of a / b ([out, T], [in, T]): given both,
+    the GEMM is issued as a_t @ b_t^T, whose operands are both contiguous along the reduction
+    (token) dimension -- the layout hipBLASLt runs fastest."""
+    if a_t is not None and b_t is not None:
+        lhs, rhs = a_t, b_t.t()
+    else:
+        lhs, rhs = a.t(), b
     mg = getattr(param, "main_grad", None)
     if mg is None:
-        return a.t() @ b
+        return lhs @ rhs
     if _fresh(param):
-        torch.mm(a.t(), b, out=mg)
+        torch.mm(lhs, rhs, out=mg)
     else:
-        mg.addmm_(a.t(), b)
+        mg.addmm_(lhs, rhs)
     _mark(param)
     return None
 

@@ -82,6 +82,34 @@ def test_swiglu(cuda):
     _close(dops.swiglu_bwd(dh.to(cuda), gu.to(cuda)), dops.swiglu_bwd(dh, gu), 3e-2, 2e-2, "swiglu bwd")
 
 
+@pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (4096, 6144, 6144), (1000, 520, 528), (8, 8, 8), (136, 7000, 7000)])
+def test_transpose2d(cuda, R, C, ld):
+    x = torch.randn(R, ld).bfloat16()[:, :C]
+    y = dops.transpose2d(x.to(cuda))
+    assert y.shape == (C, R) and y.is_contiguous()
+    assert torch.equal(y.cpu(), x.t().contiguous())
+
+
+@pytest.mark.parametrize("mode", ["native", "tn", "auto"])
+def test_linear_bwd_layouts(cuda, mode, monkeypatch):
+    """The transposed-operand (TN) backward GEMMs give the same dX / dW as the strided forms."""
+    from dtg.ops import functional as F_
+
+    monkeypatch.setattr(F_, "_LINEAR_BWD", mode)
+    torch.manual_seed(0)
+    T, n_in, n_out = 4096, 512, 1536
+    x = torch.randn(T, n_in).bfloat16()
+    w = (0.05 * torch.randn(n_out, n_in)).bfloat16()
+    dy = torch.randn(T, n_out).bfloat16()
+    xg = x.to(cuda).requires_grad_()
+    wg = w.to(cuda).requires_grad_()
+    F_.linear(xg, wg).backward(dy.to(cuda))
+    dx_ref = dy.float() @ w.float()
+    dw_ref = dy.float().t() @ x.float()
+    assert _rel(xg.grad, dx_ref) < 1e-2
+    assert _rel(wg.grad, dw_ref) < 1e-2
+
+
 @pytest.mark.parametrize("V", [50257, 1000, 128256, 156939])
 def test_cross_entropy(cuda, V):
     torch.manual_seed(0)

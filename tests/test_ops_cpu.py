@@ -158,3 +158,21 @@ def test_packed_position_ids_edge_cases():
     x = torch.tensor([1, 2, 3, eos])
     pos, lens = packed_position_ids(x, eos)
     assert pos.tolist() == [0, 1, 2, 3] and lens.tolist() == [4]
+
+
+def test_transpose2d_and_tn_weight_grad_routing():
+    """CPU reference of transpose2d and the transposed-operand weight-gradient GEMM path."""
+    from dtg.ops.grad_routing import reset_grad_state, route_weight_grad_mm
+
+    torch.manual_seed(0)
+    a, b = torch.randn(64, 24), torch.randn(64, 16)
+    at = torch.ops.dtg.transpose2d(a)
+    assert at.is_contiguous() and torch.equal(at, a.t())
+    ref = a.t() @ b
+    p = torch.nn.Parameter(torch.zeros(24, 16))
+    torch.testing.assert_close(route_weight_grad_mm(p, a, b, a_t=at, b_t=torch.ops.dtg.transpose2d(b)), ref)
+    p.main_grad = torch.zeros(24, 16)
+    reset_grad_state([p])
+    assert route_weight_grad_mm(p, a, b, a_t=at, b_t=b.t().contiguous()) is None
+    assert route_weight_grad_mm(p, a, b) is None  # second contribution accumulates
+    torch.testing.assert_close(p.main_grad, 2 * ref)
