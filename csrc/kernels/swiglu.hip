@@ -48,6 +48,103 @@ __global__ void swiglu_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_
   store8(dgu + t * 2 * I + I + c, du);
 }
 
+// Backward that also emits the operands of the MLP's weight-gradient GEMMs in K-contiguous
+// (token-minor) layout, so hipBLASLt runs them as "TN" without separate transpose passes:
+//   dgu  [T, 2I]   (row-major, for dX = dgu @ W_gu)
+//   dguT [2I, T]   (for dW_gu = dguT @ X)
+//   hT   [I, T]    (h = silu(g) * u recomputed from gu, for dW_down = dY^T @ h)
+// One workgroup owns a 64-token x 64-feature tile: 16-byte row loads of g, u, dh; the three
+// transposed tiles are staged through LDS (pitch 66 halfwords) and stored as 16-byte columns.
+namespace {
+constexpr int kSgTile = 64;
+constexpr int kSgPitch = kSgTile + 2;
+}  // namespace
+
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
+    const uint16_t* __restrict__ dh, const uint16_t* __restrict__ gu, int64_t gu_stride,
+    uint16_t* __restrict__ dgu, uint16_t* __restrict__ dguT, uint16_t* __restrict__ hT, int64_t T, int I) {
+  __shared__ uint16_t s_dg[kSgTile * kSgPitch];
+  __shared__ uint16_t s_du[kSgTile * kSgPitch];
+  __shared__ uint16_t s_h[kSgTile * kSgPitch];
+  const int64_t t0 = (int64_t)blockIdx.y * kSgTile;
+  const int c0 = blockIdx.x * kSgTile;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int lt = (tid >> 3) + 32 * i;
+    const int lc = (tid & 7) * 8;
+    const int64_t t = t0 + lt;
+    const int c = c0 + lc;
+    float g[8], u[8], d[8];
+    u16x8 vdg = {0, 0, 0, 0, 0, 0, 0, 0}, vdu = vdg, vh = vdg;
+    if (t < T && c < I) {
+      load8(gu + t * gu_stride + c, g);
+      load8(gu + t * gu_stride + I + c, u);
+      load8(dh + t * I + c, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float sg = sigmoidf_(g[j]);
+        const float silu = g[j] * sg;
+        vdu[j] = f2bf(d[j] * silu);
+        vdg[j] = f2bf(d[j] * u[j] * sg * (1.f + g[j] * (1.f - sg)));
+        vh[j] = f2bf(silu * u[j]);
+      }
+      *reinterpret_cast<u16x8*>(dgu + t * 2 * I + c) = vdg;
+      *reinterpret_cast<u16x8*>(dgu + t * 2 * I + I + c) = vdu;
+    }
+    uint32_t* a = reinterpret_cast<uint32_t*>(s_dg + lt * kSgPitch + lc);
+    uint32_t* b = reinterpret_cast<uint32_t*>(s_du + lt * kSgPitch + lc);
+    uint32_t* h = reinterpret_cast<uint32_t*>(s_h + lt * kSgPitch + lc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] = (uint32_t)vdg[2 * j] | ((uint32_t)vdg[2 * j + 1] << 16);
+      b[j] = (uint32_t)vdu[2 * j] | ((uint32_t)vdu[2 * j + 1] << 16);
+      h[j] = (uint32_t)vh[2 * j] | ((uint32_t)vh[2 * j + 1] << 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oc = (tid >> 3) + 32 * i;  // feature within the tile -> output row
+    const int ot = (tid & 7) * 8;        // first token of this 8-token vector
+    const int c = c0 + oc;
+    const int64_t t = t0 + ot;
+    if (c >= I || t >= T) continue;
+    u16x8 a, b, h;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = s_dg[(ot + j) * kSgPitch + oc];
+      b[j] = s_du[(ot + j) * kSgPitch + oc];
+      h[j] = s_h[(ot + j) * kSgPitch + oc];
+    }
+    *reinterpret_cast<u16x8*>(dguT + (int64_t)c * T + t) = a;
+    *reinterpret_cast<u16x8*>(dguT + (int64_t)(I + c) * T + t) = b;
+    *reinterpret_cast<u16x8*>(hT + (int64_t)c * T + t) = h;
+  }
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& dh_, const at::Tensor& gu) {
+  auto dh = dh_.contiguous();
+  DTG_CHECK_CUDA_BF16(gu);
+  DTG_CHECK_CUDA_BF16(dh);
+  DTG_CHECK(gu.dim() == 2 && gu.stride(1) == 1 && gu.stride(0) % 8 == 0, "swiglu_bwd_t: gu must be [T, 2I] row-major");
+  const int64_t T = gu.size(0);
+  const int I = gu.size(1) / 2;
+  DTG_CHECK(T % 8 == 0 && I % 8 == 0, "swiglu_bwd_t: T and I must be multiples of 8");
+  DTG_CHECK(dh.size(0) == T && dh.size(1) == I, "swiglu_bwd_t: shape mismatch");
+  const c10::DeviceGuard g(gu.device());
+  auto dgu = at::empty({T, 2 * I}, gu.options());
+  auto dguT = at::empty({2 * I, T}, gu.options());
+  auto hT = at::empty({I, T}, gu.options());
+  if (T == 0 || I == 0) return {dgu, dguT, hT};
+  const dim3 grid((I + kSgTile - 1) / kSgTile, (T + kSgTile - 1) / kSgTile);
+  DTG_CHECK(grid.y <= 65535, "swiglu_bwd_t: too many tokens");
+  swiglu_bwd_t_kernel<<<grid, 256, 0, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu),
+                                                  bf16_mut(dguT), bf16_mut(hT), T, I);
+  DTG_LAUNCH_CHECK();
+  return {dgu, dguT, hT};
+}
+
 at::Tensor swiglu_fwd(const at::Tensor& gu) {
   DTG_CHECK_CUDA_BF16(gu);
   DTG_CHECK(gu.dim() == 2 && gu.stride(1) == 1 && gu.stride(0) % 8 == 0 && gu.size(1) % 16 == 0,
@@ -84,6 +181,7 @@ at::Tensor swiglu_bwd(const at::Tensor& dh_, const at::Tensor& gu) {
 TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("swiglu_bwd_t", &swiglu_bwd_t);
 }
 
 }  // namespace dtg

@@ -91,8 +91,7 @@ class LlamaMLP(nn.Module):
         self.down_proj = Weight(cfg.hidden_size, self.inter, device=device, dtype=dtype)
 
     def forward(self, x):
-        gu = ops.linear(x, self.gate_up_proj.weight)
-        return ops.linear(ops.swiglu(gu), self.down_proj.weight)
+        return ops.swiglu_mlp(x, self.gate_up_proj.weight, self.down_proj.weight)
 
 
 class LlamaDecoderLayer(nn.Module):

@@ -24,6 +24,7 @@ from .functional import (  # noqa: E402
     rms_norm,
     rope_tables,
     swiglu,
+    swiglu_mlp,
     vocab_parallel_fused_linear_cross_entropy,
 )
 from .grad_routing import route_param_grad  # noqa: E402
@@ -31,5 +32,5 @@ from .adamw import adamw_step  # noqa: E402
 
 __all__ = [
     "add_rms_norm", "attention", "embedding", "fused_linear_cross_entropy", "linear", "rms_norm",
-    "rope_tables", "swiglu", "vocab_parallel_fused_linear_cross_entropy", "route_param_grad", "adamw_step",
+    "rope_tables", "swiglu", "swiglu_mlp", "vocab_parallel_fused_linear_cross_entropy", "route_param_grad", "adamw_step",
 ]

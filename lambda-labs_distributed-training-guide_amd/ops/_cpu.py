@@ -178,6 +178,11 @@ def flash_attn_bwd_qkv(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seq
     return torch.cat([dq.reshape(T, -1), dk.reshape(T, -1), dv.reshape(T, -1)], dim=1)
 
 
+def swiglu_bwd_t(dh, gu):
+    dgu = swiglu_bwd(dh, gu)
+    return dgu, dgu.t().contiguous(), swiglu_fwd(gu).t().contiguous()
+
+
 def transpose2d(x):
     return x.t().contiguous()
 
@@ -186,6 +191,6 @@ for _name, _fn in list(globals().items()):
     if _name in (
         "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "flash_attn_fwd", "flash_attn_bwd",
-        "flash_attn_bwd_qkv", "transpose2d",
+        "flash_attn_bwd_qkv", "transpose2d", "swiglu_bwd_t",
     ):
         LIB.impl(_name, _fn, "CPU")

@@ -16,6 +16,7 @@ _DEFS = [
     "rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, Tensor pos, int nheads, int head_dim, bool inverse) -> ()",
     "swiglu_fwd(Tensor gu) -> Tensor",
     "swiglu_bwd(Tensor dh, Tensor gu) -> Tensor",
+    "swiglu_bwd_t(Tensor dh, Tensor gu) -> (Tensor, Tensor, Tensor)",
     "ce_fwd_bwd_(Tensor(a!) logits, Tensor labels, int ignore_index, float grad_scale, bool compute_grad) -> Tensor",
     "ce_stats(Tensor logits, Tensor labels, int vocab_start) -> (Tensor, Tensor, Tensor)",
     "ce_grad_(Tensor(a!) logits, Tensor labels, Tensor lse, int vocab_start, int ignore_index, float grad_scale) -> ()",

@@ -232,6 +232,52 @@ def swiglu(gu):
     return _SwiGLU.apply(gu)
 
 
+class _SwiGLUMLP(torch.autograd.Function):
+    """down(swiglu(x @ W_gu^T)) as one autograd node.
+
+    Saves only x and gu (h = silu(g)*u is recomputed in backward, [T, I] less resident per
+    layer).  On the TN path the backward's SwiGLU kernel writes dgu together with dgu^T and h^T,
+    the token-contiguous operands of the two weight-gradient GEMMs, so neither needs a separate
+    transpose pass; dX GEMMs use transposed weight copies (see _bwd_layout)."""
+
+    @staticmethod
+    def forward(ctx, x, w_gu, w_down):
+        gu = torch.mm(x, w_gu.t())
+        h = ops.swiglu_fwd(gu)
+        ctx.save_for_backward(x, w_gu, w_down, gu)
+        return torch.mm(h, w_down.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_gu, w_down, gu = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx_tn, dw_tn = _bwd_layout(x, w_gu)
+        fused = dw_tn and _tn_ok(dy, gu) and gu.stride(0) == gu.shape[1]
+        dh = torch.mm(dy, ops.transpose2d(w_down).t()) if dx_tn else torch.mm(dy, w_down)
+        if fused:
+            dgu, dgu_t, h_t = ops.swiglu_bwd_t(dh, gu)
+            del dh
+            dw_down = route_weight_grad_mm(w_down, dy, None, a_t=ops.transpose2d(dy), b_t=h_t)
+            del h_t
+        else:
+            h = ops.swiglu_fwd(gu)
+            dgu = ops.swiglu_bwd(dh, gu)
+            del dh
+            dw_down = route_weight_grad_mm(w_down, dy, h)
+            del h
+        dx = torch.mm(dgu, ops.transpose2d(w_gu).t()) if dx_tn else torch.mm(dgu, w_gu)
+        if fused:
+            dw_gu = route_weight_grad_mm(w_gu, dgu, x, a_t=dgu_t, b_t=ops.transpose2d(x))
+        else:
+            dw_gu = route_weight_grad_mm(w_gu, dgu, x)
+        return dx, dw_gu, dw_down
+
+
+def swiglu_mlp(x, w_gu, w_down):
+    """Llama MLP: down_proj(silu(gate(x)) * up(x)) with the fused [gate; up] weight."""
+    return _SwiGLUMLP.apply(x, w_gu, w_down)
+
+
 # --------------------------------------------------------------------------------------------
 # Embedding
 # --------------------------------------------------------------------------------------------

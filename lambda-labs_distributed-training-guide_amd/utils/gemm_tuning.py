@@ -38,4 +38,12 @@ def enable_tunableop(tune: bool = False, max_tuning_ms: int = 30, table: str = T
 
 
 def save_tunableop(table: str = TABLE):
-    torch.cuda.tunable.write_file(table)
+    """Write the tuned results now if this torch exposes `write_file`; otherwise TunableOp
+    writes them to its results file (set by enable_tunableop / set_filename) at process exit."""
+    t = torch.cuda.tunable
+    if hasattr(t, "write_file"):
+        t.write_file(table)
+    elif os.path.abspath(t.get_filename()) != os.path.abspath(table):
+        import warnings
+
+        warnings.warn(f"tunableop: results go to {t.get_filename()} at exit, not {table}")

@@ -90,6 +90,44 @@ def test_transpose2d(cuda, R, C, ld):
     assert torch.equal(y.cpu(), x.t().contiguous())
 
 
+@pytest.mark.parametrize("T,I", [(64, 64), (4096, 1792), (520, 136)])
+def test_swiglu_bwd_t(cuda, T, I):
+    torch.manual_seed(0)
+    gu = (2 * torch.randn(T, 2 * I)).bfloat16()
+    dh = torch.randn(T, I).bfloat16()
+    dgu, dgu_t, h_t = dops.swiglu_bwd_t(dh.to(cuda), gu.to(cuda))
+    ref = dops.swiglu_bwd(dh, gu)
+    _close(dgu, ref, 3e-2, 2e-2, "dgu")
+    _close(dgu_t, ref.t(), 3e-2, 2e-2, "dgu^T")
+    _close(h_t, dops.swiglu_fwd(gu).t(), 2e-2, 1e-2, "h^T")
+    assert torch.equal(dgu_t.cpu(), dgu.cpu().t())
+
+
+@pytest.mark.parametrize("mode", ["native", "tn"])
+def test_swiglu_mlp_bwd(cuda, mode, monkeypatch):
+    """Fused MLP node (TN path with the transposing SwiGLU backward) vs an f32 autograd reference."""
+    from dtg.ops import functional as F_
+
+    monkeypatch.setattr(F_, "_LINEAR_BWD", mode)
+    torch.manual_seed(0)
+    T, H, I = 4096, 256, 704
+    x = torch.randn(T, H).bfloat16()
+    wgu = (0.06 * torch.randn(2 * I, H)).bfloat16()
+    wd = (0.04 * torch.randn(H, I)).bfloat16()
+    dy = torch.randn(T, H).bfloat16()
+    xs = [t.to(cuda).requires_grad_() for t in (x, wgu, wd)]
+    y = F_.swiglu_mlp(*xs)
+    y.backward(dy.to(cuda))
+    rs = [t.float().requires_grad_() for t in (x, wgu, wd)]
+    gu = rs[0] @ rs[1].t()
+    g, u = gu.chunk(2, 1)
+    yr = (torch.nn.functional.silu(g) * u) @ rs[2].t()
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    for a, b in zip(xs, rs):
+        assert _rel(a.grad, b.grad) < 2e-2
+
+
 @pytest.mark.parametrize("mode", ["native", "tn", "auto"])
 def test_linear_bwd_layouts(cuda, mode, monkeypatch):
     """The transposed-operand (TN) backward GEMMs give the same dX / dW as the strided forms."""

@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Llama-3.1-405B per-GPU throughput on one MI355X: exact width, reduced depth, extrapolated.
+
+The reference's only published throughput is its 405B run (64 x H100,
+FSDP FULL_SHARD + activation checkpointing + CPU offload, batch 1 x seq 4096 per GPU, ~30 s per
+step => 136.5 tok/s/GPU).  The full 405B training state (3.25 TB in pure bf16) cannot live on
+one GPU, so this tool trains the *exact-width* model (hidden 16384, 128/8 heads, FFN 53248,
+vocab 128256) at depths L = 2, 4, ... on one GPU with the same per-GPU workload (1 x 4096
+tokens, activation checkpointing on, pure-bf16 AdamW step included), fits
+step_ms(L) = a + b * L, and extrapolates to the real 126 layers.
+
+The extrapolated number is the per-GPU *compute* throughput: it excludes the FSDP parameter
+all-gather / gradient reduce-scatter traffic of a multi-GPU run (overlapped with compute when
+the fabric keeps up) and is labelled as such in every output line.
+
+    python tools/bench_405b_depth.py --depths 2,4 --steps 3 --warmup 2 [--no-ac]
+"""
+import argparse
+import gc
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+REF_TOK_S_PER_GPU = 136.5  # BASELINE.md row 9 (derived from 05-training-llama-405b/README.md:210-214)
+FULL_DEPTH = 126
+
+
+def run_depth(L, a, torch):
+    import dtg  # noqa: F401
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.checkpointing import apply_activation_checkpointing
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    dev = torch.device("cuda")
+    cfg = resolve_config("llama-3.1-405b", num_hidden_layers=L)
+    torch.manual_seed(0)
+    model = build_model(cfg, device=dev)
+    if a.ac:
+        apply_activation_checkpointing(model)
+    eng = DataParallel(model, mode="single")
+    opt = FlatAdamW(eng, lr=3e-5)
+    S = a.seq_len
+    # a fresh synthetic batch every step (a repeated batch is memorised within a few steps)
+    batches = [torch.randint(0, cfg.vocab_size, (a.batch_size, S), device=dev) for _ in range(a.warmup + a.steps)]
+    it = iter(batches)
+
+    def step():
+        ids = next(it)
+        opt.zero_grad()
+        out = model(input_ids=ids, labels=ids, num_valid=a.batch_size * (S - 1))
+        eng.backward(out.loss)
+        opt.step()
+        return out.loss
+
+    for i in range(a.warmup):
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        print(f"[405b] L={L} warmup {i}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
+    torch.cuda.reset_peak_memory_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    ms = 1000 * (time.perf_counter() - t0) / a.steps
+    rec = {"depth": L, "ms_per_step": round(ms, 2), "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2),
+           "loss": round(float(loss.item()), 4), "params_b": round(cfg.num_params() / 1e9, 3)}
+    del model, eng, opt, batches, it, step, loss
+    gc.collect()  # parameters <-> engine callbacks form reference cycles
+    torch.cuda.empty_cache()
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--depths", default="2,4")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--batch-size", type=int, default=1)
+    ap.add_argument("--no-ac", dest="ac", action="store_false")
+    ap.add_argument("--tunableop", choices=["off", "use"], default="use")
+    a = ap.parse_args()
+    import torch
+
+    import dtg  # noqa: F401
+    from dtg.models import resolve_config
+
+    if a.tunableop == "use":
+        from dtg.utils.gemm_tuning import enable_tunableop
+
+        enable_tunableop(tune=False)
+    depths = [int(x) for x in a.depths.split(",")]
+    recs = []
+    for L in depths:
+        r = run_depth(L, a, torch)
+        print(json.dumps(r), flush=True)
+        recs.append(r)
+    if len(recs) >= 2:
+        xs = [r["depth"] for r in recs]
+        ys = [r["ms_per_step"] for r in recs]
+        n = len(xs)
+        mx, my = sum(xs) / n, sum(ys) / n
+        b = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
+        a0 = my - b * mx
+        full_ms = a0 + b * FULL_DEPTH
+        tokens = a.batch_size * a.seq_len
+        tps = 1000 * tokens / full_ms
+        cfg = resolve_config("llama-3.1-405b")
+        mfu = tps * cfg.flops_per_token(a.seq_len) / 2.5e15
+        print(json.dumps({
+            "metric": "Llama-3.1-405B tok/s/GPU (exact width, depth-extrapolated to 126 layers, compute only)",
+            "value": round(tps, 1), "unit": "tokens/s per GPU", "reference_tok_s_per_gpu": REF_TOK_S_PER_GPU,
+            "vs_reference": round(tps / REF_TOK_S_PER_GPU, 3), "per_layer_ms": round(b, 2), "fixed_ms": round(a0, 2),
+            "extrapolated_step_s": round(full_ms / 1000, 3), "activation_checkpointing": a.ac,
+            "batch_size": a.batch_size, "seq_len": a.seq_len, "depths_measured": xs,
+            "model_flops_utilization_vs_2.5PF": round(mfu, 4),
+            "note": "1 GPU, synthetic tokens, random init, pure-bf16 AdamW; excludes FSDP communication",
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--tokens", type=int, default=16384)
-    ap.add_argument("--which", default="dw", help="comma list of fwd,dx,dw")
+    ap.add_argument("--which", default="dw", help="comma list of fwd,dx,dw,dx_tn,dw_tn")
     ap.add_argument("--only", default="", help="comma list of qkv,o,gate_up,down")
     ap.add_argument("--out", default="gpurun_out/tunableop_new.csv")
     ap.add_argument("--max-ms", type=int, default=20)
@@ -66,16 +66,21 @@ def main():
         w = torch.randn(out_f, in_f, device=dev, dtype=torch.bfloat16) * 0.02
         dy = torch.randn(T, out_f, device=dev, dtype=torch.bfloat16)
         mg = torch.empty(out_f, in_f, device=dev, dtype=torch.bfloat16)
+        wt, dyt, xt = w.t().contiguous(), dy.t().contiguous(), x.t().contiguous()
         jobs = {"fwd": lambda: torch.mm(x, w.t()), "dx": lambda: torch.mm(dy, w),
-                "dw": lambda: torch.mm(dy.t(), x, out=mg)}
+                "dw": lambda: torch.mm(dy.t(), x, out=mg),
+                # the TN forms issued by ops.functional._Linear (DTG_LINEAR_BWD=tn, the default)
+                "dx_tn": lambda: torch.mm(dy, wt.t()), "dw_tn": lambda: torch.mm(dyt, xt.t(), out=mg)}
         for k in which:
             current["name"], current["t0"] = f"{name}/{k}", time.time()
             jobs[k]()
             torch.cuda.synchronize()
             print(f"[tune] {name}/{k} done in {time.time() - current['t0']:.1f}s", flush=True)
-        del x, w, dy, mg
+        del x, w, dy, mg, wt, dyt, xt
         torch.cuda.empty_cache()
-    t.write_file(a.out)
+    from dtg.utils.gemm_tuning import save_tunableop
+
+    save_tunableop(a.out)
     print(f"[tune] wrote {a.out}", flush=True)
 
 
