@@ -303,8 +303,24 @@ def embedding(ids, w):
 # Fused lm_head + causal-LM cross entropy (chunked; logits never materialised whole)
 # --------------------------------------------------------------------------------------------
 def _default_chunk(vocab, hidden_rows):
-    # ~1 GiB of bf16 logits per chunk; at least 1024 rows.
-    return max(1024, min(hidden_rows, (1 << 29) // max(vocab, 1)))
+    """Rows per chunk: ~1 GiB of bf16 logits, split evenly over the rows (16,384 rows x 128,256
+    vocab -> 4 x 4,096), a multiple of 64 rows (transposable, MFMA-tile aligned), >= 1024."""
+    n = max(1, -(-hidden_rows * max(vocab, 1) // (1 << 29)))
+    per = -(-hidden_rows // n)
+    return max(1024, min(hidden_rows, -(-per // 64) * 64))
+
+
+def _ce_tn(h, w):
+    """Use K-contiguous (TN) operands for the loss head's dX / dW GEMMs (see _bwd_layout)."""
+    return _LINEAR_BWD != "native" and _tn_ok(h, w)
+
+
+def _ce_dx(logits, w, w_t, out):
+    """out = logits @ w, as logits @ (w^T)^T when a contiguous w^T is given."""
+    if w_t is not None:
+        torch.mm(logits, w_t.t(), out=out)
+    else:
+        torch.mm(logits, w, out=out)
 
 
 class _FusedLinearCE(torch.autograd.Function):
@@ -319,14 +335,19 @@ class _FusedLinearCE(torch.autograd.Function):
         # direct: dW goes straight into w.main_grad now (engine-owned loss, grad_output == 1)
         direct = want_dw and _gr.direct_loss_grad() and getattr(w, "main_grad", None) is not None
         dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if (want_dw and not direct) else None
+        tn = need and _ce_tn(h, w) and chunk % 8 == 0
+        w_t = ops.transpose2d(w) if (tn and ctx.needs_input_grad[0]) else None
         for s in range(0, T, chunk):
             e = min(T, s + chunk)
             logits = torch.mm(h[s:e], w.t())
             rows = ops.ce_fwd_bwd_(logits, labels[s:e], ignore_index, scale, need)
             loss_sum += rows.sum()
             if need:
-                torch.mm(logits, w, out=dh[s:e])
-                if direct:
+                _ce_dx(logits, w, w_t, dh[s:e])
+                if direct and tn:
+                    _gr.accumulate_mm_into_main_grad(w, logits, h[s:e], a_t=ops.transpose2d(logits),
+                                                     b_t=ops.transpose2d(h[s:e]))
+                elif direct:
                     _gr.accumulate_mm_into_main_grad(w, logits, h[s:e])
                 elif dw is not None:
                     # f32 accumulate inside the GEMM, one bf16 rounding per chunk
@@ -379,6 +400,7 @@ class _VocabParallelFusedLinearCE(torch.autograd.Function):
         loss_sum = torch.zeros((), dtype=torch.float32, device=h.device)
         dh = torch.empty_like(h) if need else None
         dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if need else None
+        w_t = ops.transpose2d(w) if (need and _ce_tn(h, w)) else None
         for s in range(0, T, chunk):
             e = min(T, s + chunk)
             lab = labels[s:e]
@@ -394,7 +416,7 @@ class _VocabParallelFusedLinearCE(torch.autograd.Function):
             loss_sum += torch.where(valid, lse - stats[1], torch.zeros_like(lse)).sum()
             if need:
                 ops.ce_grad_(logits, lab, lse.contiguous(), vocab_start, ignore_index, scale)
-                torch.mm(logits, w, out=dh[s:e])
+                _ce_dx(logits, w, w_t, dh[s:e])
                 if s == 0:
                     torch.mm(logits.t(), h[s:e], out=dw)
                 else:

@@ -49,16 +49,18 @@ def route_param_grad(param, grad):
     return None
 
 
-def accumulate_mm_into_main_grad(param, a, b) -> bool:
-    """main_grad (+)= a^T @ b without notifying (used by the fused loss head's forward)."""
+def accumulate_mm_into_main_grad(param, a, b, a_t=None, b_t=None) -> bool:
+    """main_grad (+)= a^T @ b without notifying (used by the fused loss head's forward).
+    `a_t` / `b_t`: optional contiguous transposes (see route_weight_grad_mm)."""
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return False
+    lhs, rhs = (a_t, b_t.t()) if (a_t is not None and b_t is not None) else (a.t(), b)
     if _fresh(param):
-        torch.mm(a.t(), b, out=mg)
+        torch.mm(lhs, rhs, out=mg)
         param._dtg_grad_written = True
     else:
-        mg.addmm_(a.t(), b)
+        mg.addmm_(lhs, rhs)
     return True
 
 

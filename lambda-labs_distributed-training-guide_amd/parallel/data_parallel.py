@@ -11,6 +11,13 @@
                  not checkpointable) is strictly more traffic; this engine's state is
                  checkpointable (§2.11 #1).
 
+`overlap_optimizer=True` moves the AdamW update into backward: the moment a bucket's gradients
+are final (and, with DDP/ZeRO, its all-reduce / reduce-scatter has landed) its update runs on a
+side HIP stream while backward keeps the matrix cores busy with the remaining layers; under
+ZeRO the bucket's parameter all-gather is issued right behind it.  `optimizer.step()` then only
+joins the side stream.  Updates are bit-identical to the post-backward step (same kernel, same
+hyper-parameters: the LR scheduler has already stepped for this iteration).
+
 Gradient accumulation (`no_sync()`), parameters unused in a step, tensor-parallel replicated
 (sequence-parallel) norm weights and tied embeddings are handled.  All engines present a
 torch.optim.Optimizer (`FlatAdamW`) so LR schedulers and the reference's loop shape work.
@@ -33,7 +40,8 @@ from .flat import FlatSpace, rebind_parameters
 class DataParallel:
     def __init__(self, model: nn.Module, mode: str = "ddp", group=None, tp_group=None,
                  bucket_mb: int = 256, broadcast_from_rank0: bool = True, state_dtype=torch.bfloat16,
-                 master_weights: bool = False, overlap_param_gather: bool = True):
+                 master_weights: bool = False, overlap_param_gather: bool = True,
+                 overlap_optimizer: bool = False):
         assert mode in ("single", "ddp", "zero")
         self.module = model
         self.group = group
@@ -80,6 +88,10 @@ class DataParallel:
         self.overlap_param_gather = overlap_param_gather and self.mode == "zero"
         if self.overlap_param_gather:
             self._install_gather_hooks()
+        self.overlap_optimizer = overlap_optimizer
+        self._hparams = None  # () -> (lr, beta1, beta2, eps, weight_decay); set by FlatAdamW
+        self._opt_stream = torch.cuda.Stream(device=dev) if (overlap_optimizer and dev.type == "cuda") else None
+        self._bwd_stepped = False
         # The engine owns the loss: backward(loss) uses an implicit gradient of 1 and any
         # scaling goes into AdamW's grad_scale, which lets the loss head write dW in place.
         set_direct_loss_grad(True)
@@ -98,7 +110,7 @@ class DataParallel:
     def _on_grad(self, p):
         if getattr(p, "_dtg_sequence_parallel", False) and self.tp_group is not None:
             dist.all_reduce(p.main_grad, group=self.tp_group)
-        if not self._sync_enabled or self.mode == "single":
+        if not self._sync_enabled or (self.mode == "single" and not self.overlap_optimizer):
             return
         b = p._dtg_bucket
         b.pending -= 1
@@ -112,16 +124,52 @@ class DataParallel:
         view = self.space.grad_buf[b.start:b.end]
         if self.mode == "ddp":
             b.work = dist.all_reduce(view, group=self.group, async_op=True)
-        else:
+        elif self.mode == "zero":
             i = b.index
             o = self.shard_offsets[i]
             s, e = self.shard_ranges[i]
             b.work = comm.reduce_scatter_into(self.grad_shard[o:o + (e - s)], view, group=self.group, async_op=True)
         self._inflight.append(b)
+        if self.overlap_optimizer:
+            self._step_bucket_in_backward(b)
+
+    def _step_bucket_in_backward(self, b):
+        assert self._hparams is not None, "overlap_optimizer needs a FlatAdamW bound to this engine"
+        lr, beta1, beta2, eps, wd = self._hparams()
+        if not self._bwd_stepped:
+            self._bwd_stepped = True
+            self.step_count += 1
+        if self.mode == "zero":
+            self.wait_param_gather([b.index])  # last step's gather of this bucket (normally long done)
+        scale = 1.0 / (self.world * (self.accum_count + 1))  # this backward is micro-batch accum_count+1
+        st = self._opt_stream
+        if st is not None:
+            st.wait_stream(torch.cuda.current_stream())  # this bucket's gradients are written
+        with (torch.cuda.stream(st) if st is not None else contextlib.nullcontext()):
+            if b.work is not None:
+                b.work.wait()  # HIP: the side stream waits for the collective; gloo: blocks
+            self._update_bucket(b, lr, beta1, beta2, eps, wd, scale)
+            if self.mode == "zero":
+                self._gather_bucket(b.index)
+        b.stepped = True
+
+    def _update_bucket(self, b, lr, beta1, beta2, eps, wd, scale):
+        # `.data`: own version counter, so updating finished buckets in place does not trip
+        # autograd's saved-tensor checks for weights later layers' backward still reads.
+        buf = self.space.param_buf.data
+        if self.mode == "zero":
+            s, e = self.shard_ranges[b.index]
+            o = self.shard_offsets[b.index]
+            pv, gv, lo, hi = buf[s:e], self.grad_shard[o:o + (e - s)], o, o + (e - s)
+        else:
+            pv, gv, lo, hi = buf[b.start:b.end], self.space.grad_buf[b.start:b.end], b.start, b.end
+        adamw_step(pv, gv, self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], lr=lr, step=self.step_count, beta1=beta1,
+                   beta2=beta2, eps=eps, weight_decay=wd, grad_scale=scale,
+                   master=None if self.master is None else self.master[lo:hi])
 
     def finish_grad_sync(self):
         """Call after backward (the last micro-batch): flush unlaunched buckets, wait for all."""
-        if self.mode != "single" and self._sync_enabled:
+        if (self.mode != "single" or self.overlap_optimizer) and self._sync_enabled:
             for p in self.params:
                 if not getattr(p, "_dtg_grad_written", False):
                     p.main_grad.zero_()  # unused parameter this step
@@ -145,6 +193,7 @@ class DataParallel:
         for b in self.space.buckets:
             b.pending = b.expected
             b.launched = False
+            b.stepped = False
             b.work = None
         self.accum_count = 0
 
@@ -157,6 +206,12 @@ class DataParallel:
             out.copy_(self.space.param_buf)
 
     def step(self, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, grad_scale=None):
+        if self._bwd_stepped:  # overlap_optimizer: every bucket was updated during backward
+            assert all(b.stepped for b in self.space.buckets), "a bucket missed its in-backward update"
+            if self._opt_stream is not None:
+                torch.cuda.current_stream().wait_stream(self._opt_stream)
+            self._bwd_stepped = False
+            return
         self.step_count += 1
         if grad_scale is None:
             grad_scale = 1.0 / (self.world * max(1, self.accum_count))
@@ -181,15 +236,20 @@ class DataParallel:
         order = getattr(self, "_ag_order", range(len(self.space.buckets)))
         # `.data` has its own version counter: the in-place gather (which may complete during the
         # next forward) must not invalidate weights autograd has already saved.
-        buf = self.space.param_buf.data
         for i in order:
-            b = self.space.buckets[i]
-            s, e = self.shard_ranges[i]
-            src = buf[s:e]
-            self._pending_ag[i] = comm.all_gather_into(buf[b.start:b.end], src.clone() if gloo else src,
-                                                       group=self.group, async_op=True)
+            self._gather_bucket(i, gloo)
         if wait:
             self.wait_param_gather()
+
+    def _gather_bucket(self, i, gloo=None):
+        if gloo is None:
+            gloo = comm.backend_of(self.group) == "gloo"
+        buf = self.space.param_buf.data
+        b = self.space.buckets[i]
+        s, e = self.shard_ranges[i]
+        src = buf[s:e]
+        self._pending_ag[i] = comm.all_gather_into(buf[b.start:b.end], src.clone() if gloo else src,
+                                                   group=self.group, async_op=True)
 
     def wait_param_gather(self, buckets=None):
         for i in (list(self._pending_ag) if buckets is None else buckets):
@@ -275,6 +335,9 @@ class FlatAdamW(torch.optim.Optimizer):
         self.engine = engine
         params = [p for p in engine.module.parameters() if p.requires_grad]
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        if hasattr(engine, "_hparams"):
+            g = self.param_groups[0]
+            engine._hparams = lambda: (g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"])
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -27,7 +27,7 @@ def _round_up(x, m):
 
 
 class Bucket:
-    __slots__ = ("index", "start", "end", "params", "pending", "expected", "work", "launched")
+    __slots__ = ("index", "start", "end", "params", "pending", "expected", "work", "launched", "stepped")
 
     def __init__(self, index, start, end, params):
         self.index, self.start, self.end, self.params = index, start, end, params
@@ -35,6 +35,7 @@ class Bucket:
         self.pending = self.expected
         self.work = None
         self.launched = False
+        self.stepped = False
 
     @property
     def numel(self):

@@ -14,13 +14,13 @@ def _batches(vocab, B, S, n=STEPS, seed=0):
     return [torch.randint(0, vocab, (B, S), generator=g) for _ in range(n)]
 
 
-def _train(model_name, mode, rank, world, batches, bucket_mb=1, accum=1):
+def _train(model_name, mode, rank, world, batches, bucket_mb=1, accum=1, overlap=False):
     from dtg.models import build_model
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
 
     torch.manual_seed(0)
     model = build_model(model_name, device="cpu", dtype=torch.float32)
-    eng = DataParallel(model, mode=mode, bucket_mb=bucket_mb)
+    eng = DataParallel(model, mode=mode, bucket_mb=bucket_mb, overlap_optimizer=overlap)
     opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)  # eps >> float reduction-order noise (Adam amplifies it)
     losses = []
     for ids in batches:
@@ -43,8 +43,8 @@ def _train(model_name, mode, rank, world, batches, bucket_mb=1, accum=1):
     return {n: p.detach().clone() for n, p in model.named_parameters()}, losses
 
 
-def _worker(rank, world, model_name, mode, batches, accum):
-    return _train(model_name, mode, rank, world, batches, accum=accum)
+def _worker(rank, world, model_name, mode, batches, accum, overlap=False):
+    return _train(model_name, mode, rank, world, batches, accum=accum, overlap=overlap)
 
 
 @pytest.mark.parametrize("model_name", ["llama-tiny", "gpt2-tiny"])
@@ -83,3 +83,24 @@ def test_flat_buffers_are_views_and_buckets_cover_params():
     assert sum(p.numel() for p in m.parameters()) == n_before
     assert len(eng.space.buckets) > 1
     assert eng.space.buckets[-1].end == eng.space.numel
+
+
+@pytest.mark.parametrize("model_name", ["llama-tiny", "gpt2-tiny"])
+def test_optimizer_in_backward_single_is_exact(model_name):
+    """overlap_optimizer (per-bucket AdamW during backward) == the post-backward step, bit for bit."""
+    batches = _batches(512, 4, 32)
+    ref, lr = _train(model_name, "single", 0, 1, batches)
+    got, lg = _train(model_name, "single", 0, 1, batches, overlap=True)
+    assert lr == lg
+    for n in ref:
+        assert torch.equal(got[n], ref[n]), n
+
+
+@pytest.mark.parametrize("mode,accum", [("ddp", 1), ("zero", 1), ("zero", 2)])
+def test_optimizer_in_backward_distributed(mode, accum):
+    batches = _batches(512, 8, 16)
+    ref, _ = _train("llama-tiny", "single", 0, 1, batches)
+    res = run_distributed(_worker, 2, "llama-tiny", mode, batches, accum, True)
+    for r in range(2):
+        for n in ref:
+            torch.testing.assert_close(res[r][0][n], ref[n], atol=3e-4, rtol=1e-3, msg=f"rank {r} {n}")

@@ -21,7 +21,7 @@ def shapes(cfg):
     h, i = cfg.hidden_size, cfg.intermediate_size
     hd = h // cfg.num_attention_heads
     qkv = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * hd
-    return {"qkv": (qkv, h), "o": (h, h), "gate_up": (2 * i, h), "down": (h, i)}
+    return {"qkv": (qkv, h), "o": (h, h), "gate_up": (2 * i, h), "down": (h, i), "lm_head": (cfg.vocab_size, h)}
 
 
 def main():
@@ -60,8 +60,8 @@ def main():
     which = a.which.split(",")
     only = [s for s in a.only.split(",") if s]
     for name, (out_f, in_f) in shapes(cfg).items():
-        if only and name not in only:
-            continue
+        if (only and name not in only) or (not only and name == "lm_head"):
+            continue  # the loss head runs per chunk: tune it with --only lm_head --tokens <chunk>
         x = torch.randn(T, in_f, device=dev, dtype=torch.bfloat16)
         w = torch.randn(out_f, in_f, device=dev, dtype=torch.bfloat16) * 0.02
         dy = torch.randn(T, out_f, device=dev, dtype=torch.bfloat16)
