@@ -1,0 +1,359 @@
+// Direct-peer collectives over xGMI for tensor/sequence-parallel messages.
+//
+// An MI355X node is a fully connected graph: every GPU has 7 point-to-point xGMI links.  A ring
+// collective (RCCL's default for these sizes) moves every byte over ONE link per direction per
+// step; a direct-peer collective has each GPU read its 7 peers concurrently, i.e. over 7
+// distinct links at once.  That is the pattern here:
+//
+//   * Every rank owns one symmetric workspace: [data: capacity bytes][signals: 2 x 64 x u32],
+//     allocated uncached (hipDeviceMallocUncached) and exported with hipIpcGetMemHandle; every
+//     rank maps all peers' workspaces (hipIpcOpenMemHandle), so a kernel can load or store
+//     peer HBM directly.
+//   * A collective = stage -> barrier -> pull -> barrier, four launches on the caller's stream:
+//       stage   copy the input into the own workspace (many workgroups, 16-byte vectors)
+//       barrier one wave: store `epoch` into slot [me] of every peer's signal row (system-scope
+//               release), then spin until all peers' stores arrived in the own row (acquire);
+//               the spin is bounded in wall time (s_memrealtime): a missing peer sets an
+//               error word and the wave exits, so a broken peer can never hang the GPU
+//       pull    all_gather: out[r] = peer_r.data[0:shard];  reduce_scatter: out = sum_r
+//               peer_r.data[me*shard : (me+1)*shard] (f32 accumulation);  all_reduce:
+//               out = sum_r peer_r.data (one-shot).  Workgroups are dealt round-robin over
+//               the peers (workgroup b reads peer (b + me) % world first), so all links
+//               carry traffic at once.
+//       barrier the "done" row: nobody restages its workspace while a peer may still read it.
+//     Kernel boundaries give the acquire/release of the data itself (caches are written back
+//     at the end of a kernel and invalidated at the start of the next).
+//   * Epochs increase monotonically per communicator, so signal rows never need resetting.
+//
+// RCCL stays the path for the large DDP/ZeRO/FSDP buckets and for inter-node traffic.
+// All stores are vector-memory stores / atomics; nothing writes through the scalar cache.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+namespace dtg {
+namespace xgmi {
+
+constexpr int kMaxRanks = 8;
+constexpr int kSigSlots = 64;  // u32 per signal row (rank slots; padded to a 256-B row)
+
+#define XGMI_CHECK(expr)                                                                         \
+  do {                                                                                           \
+    hipError_t _e = (expr);                                                                      \
+    TORCH_CHECK(_e == hipSuccess, "xgmi: ", #expr, " failed: ", hipGetErrorString(_e));          \
+  } while (0)
+
+struct Peers {
+  uint8_t* data[kMaxRanks];
+  uint32_t* sig[kMaxRanks];
+};
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+__global__ void barrier_kernel(Peers peers, int me, int world, int row, uint32_t epoch, uint32_t* err,
+                               uint64_t timeout_ticks) {
+  const int t = threadIdx.x;
+  if (t < world) {
+    uint32_t* dst = peers.sig[t] + row * kSigSlots + me;
+    __hip_atomic_store(dst, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (t < world) {
+    const uint32_t* src = peers.sig[me] + row * kSigSlots + t;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      const uint32_t v = __hip_atomic_load(src, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((int32_t)(v - epoch) >= 0) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+        __hip_atomic_store(err, 1u + (uint32_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// dst[i] = src[i] for n16 16-byte vectors.
+__global__ void copy16_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+// out[r * shard + i] = peer_r.data[i]; workgroups split as (peer, slice).
+__global__ void all_gather_kernel(Peers peers, int me, int world, u32x4* __restrict__ out, int64_t shard16,
+                                  int blocks_per_peer) {
+  const int p = (blockIdx.x / blocks_per_peer + me) % world;
+  const int b = blockIdx.x % blocks_per_peer;
+  const u32x4* src = reinterpret_cast<const u32x4*>(peers.data[p]);
+  u32x4* dst = out + (int64_t)p * shard16;
+  for (int64_t i = (int64_t)b * blockDim.x + threadIdx.x; i < shard16; i += (int64_t)blocks_per_peer * blockDim.x)
+    dst[i] = __builtin_nontemporal_load(src + i);
+}
+
+__device__ __forceinline__ void acc8_bf16(float* a, u32x4 v) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a[2 * j] += __uint_as_float(v[j] << 16);
+    a[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ u32x4 pack8_bf16(const float* a) {
+  u32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lo = __builtin_bit_cast(uint16_t, static_cast<__bf16>(a[2 * j]));
+    const uint32_t hi = __builtin_bit_cast(uint16_t, static_cast<__bf16>(a[2 * j + 1]));
+    r[j] = lo | (hi << 16);
+  }
+  return r;
+}
+
+// out[i] = sum_r peer_r.data[offset16 + i] over n16 vectors; IS_BF16 selects 8 x bf16 or 4 x f32
+// per 16-byte vector.  Each workgroup reads its slice from every peer, starting at a different
+// peer per workgroup so the links are loaded evenly.
+template <bool IS_BF16>
+__global__ void reduce_kernel(Peers peers, int me, int world, u32x4* __restrict__ out, int64_t offset16, int64_t n16) {
+  const int first = (blockIdx.x + me) % world;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < world; ++k) {
+      const int p = (first + k) % world;
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(peers.data[p]) + offset16 + i);
+      if constexpr (IS_BF16) {
+        acc8_bf16(a, v);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] += __uint_as_float(v[j]);
+      }
+    }
+    if constexpr (IS_BF16) {
+      out[i] = pack8_bf16(a);
+    } else {
+      u32x4 r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = __float_as_uint(a[j]);
+      out[i] = r;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// communicator
+// ------------------------------------------------------------------------------------------
+struct Comm {
+  int rank = 0, world = 1, device = 0;
+  int64_t capacity = 0;  // data bytes per rank
+  uint8_t* base = nullptr;  // own workspace: data + signals
+  uint32_t* err = nullptr;  // host-pinned error word
+  Peers peers{};
+  std::vector<void*> opened;
+  uint32_t epoch = 0;
+  double timeout_s = 10.0;
+
+  ~Comm() {
+    for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+    if (base) (void)hipFree(base);
+    if (err) (void)hipHostFree(err);
+  }
+  uint32_t* sig_of(uint8_t* b) const { return reinterpret_cast<uint32_t*>(b + capacity); }
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<Comm>> g_comms;
+
+Comm& get(int64_t id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TORCH_CHECK(id >= 0 && id < (int64_t)g_comms.size() && g_comms[id], "xgmi: bad communicator id ", id);
+  return *g_comms[id];
+}
+
+int64_t create(int64_t capacity, int64_t rank, int64_t world, int64_t device) {
+  TORCH_CHECK(world >= 1 && world <= kMaxRanks, "xgmi: world size must be 1..", kMaxRanks);
+  TORCH_CHECK(rank >= 0 && rank < world, "xgmi: bad rank");
+  TORCH_CHECK(capacity > 0 && capacity % 4096 == 0, "xgmi: capacity must be a positive multiple of 4096");
+  auto c = std::make_unique<Comm>();
+  c->rank = rank;
+  c->world = world;
+  c->device = device;
+  c->capacity = capacity;
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device));
+  const size_t bytes = capacity + 2 * kSigSlots * sizeof(uint32_t);
+  XGMI_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->base), bytes, hipDeviceMallocUncached));
+  XGMI_CHECK(hipMemset(c->base + capacity, 0, 2 * kSigSlots * sizeof(uint32_t)));
+  XGMI_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c->err), sizeof(uint32_t), hipHostMallocCoherent));
+  *c->err = 0;
+  XGMI_CHECK(hipDeviceSynchronize());
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_comms.push_back(std::move(c));
+  return (int64_t)g_comms.size() - 1;
+}
+
+at::Tensor ipc_handle(int64_t id) {
+  Comm& c = get(id);
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c.device));
+  hipIpcMemHandle_t h;
+  XGMI_CHECK(hipIpcGetMemHandle(&h, c.base));
+  auto t = at::empty({(int64_t)sizeof(h)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), &h, sizeof(h));
+  return t;
+}
+
+void open_peers(int64_t id, const at::Tensor& handles) {
+  Comm& c = get(id);
+  TORCH_CHECK(handles.device().is_cpu() && handles.scalar_type() == at::kByte && handles.dim() == 2 &&
+                  handles.size(0) == c.world && handles.size(1) == (int64_t)sizeof(hipIpcMemHandle_t),
+              "xgmi: handles must be a CPU uint8 tensor [world, ", sizeof(hipIpcMemHandle_t), "]");
+  auto hc = handles.contiguous();
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c.device));
+  for (int r = 0; r < c.world; ++r) {
+    uint8_t* p = nullptr;
+    if (r == c.rank) {
+      p = c.base;
+    } else {
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, hc.data_ptr<uint8_t>() + r * sizeof(h), sizeof(h));
+      void* q = nullptr;
+      XGMI_CHECK(hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess));
+      c.opened.push_back(q);
+      p = static_cast<uint8_t*>(q);
+    }
+    c.peers.data[r] = p;
+    c.peers.sig[r] = c.sig_of(p);
+  }
+}
+
+void set_timeout(int64_t id, double seconds) { get(id).timeout_s = seconds; }
+
+int64_t error(int64_t id) {
+  Comm& c = get(id);
+  return (int64_t)__atomic_load_n(c.err, __ATOMIC_ACQUIRE);
+}
+
+void destroy(int64_t id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TORCH_CHECK(id >= 0 && id < (int64_t)g_comms.size(), "xgmi: bad id");
+  g_comms[id].reset();
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void barrier(Comm& c, int row, hipStream_t st) {
+  // s_memrealtime runs at 100 MHz on gfx950.
+  const uint64_t ticks = (uint64_t)(c.timeout_s * 1e8);
+  barrier_kernel<<<1, 64, 0, st>>>(c.peers, c.rank, c.world, row, c.epoch, c.err, ticks);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+int grid_for(int64_t n16, int cap = 2048) {
+  int64_t g = (n16 + 255) / 256;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+void stage(Comm& c, const at::Tensor& inp, hipStream_t st) {
+  const int64_t n16 = inp.numel() * inp.element_size() / 16;
+  copy16_kernel<<<grid_for(n16), 256, 0, st>>>(reinterpret_cast<const u32x4*>(inp.data_ptr()),
+                                               reinterpret_cast<u32x4*>(c.base), n16);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+void check_io(const Comm& c, const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.get_device() == c.device, "xgmi: ", what, " must be on cuda:", c.device);
+  TORCH_CHECK(t.is_contiguous(), "xgmi: ", what, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, "xgmi: ", what, " must be bf16 or f32");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && (t.numel() * t.element_size()) % 16 == 0,
+              "xgmi: ", what, " must be 16-byte aligned and a multiple of 16 bytes");
+}
+
+}  // namespace
+
+void all_gather(int64_t id, const at::Tensor& out, const at::Tensor& inp) {
+  Comm& c = get(id);
+  check_io(c, inp, "input");
+  check_io(c, out, "output");
+  TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == inp.numel() * c.world, "xgmi all_gather: shape");
+  const int64_t bytes = inp.numel() * inp.element_size();
+  TORCH_CHECK(bytes <= c.capacity, "xgmi: message of ", bytes, " B exceeds the workspace (", c.capacity, " B)");
+  c10::DeviceGuard g(inp.device());
+  hipStream_t st = cur_stream();
+  ++c.epoch;
+  stage(c, inp, st);
+  barrier(c, 0, st);
+  const int64_t shard16 = bytes / 16;
+  const int bpp = std::max(1, grid_for(shard16, 1024) / 1);
+  all_gather_kernel<<<bpp * c.world, 256, 0, st>>>(c.peers, c.rank, c.world, reinterpret_cast<u32x4*>(out.data_ptr()),
+                                                   shard16, bpp);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  barrier(c, 1, st);
+}
+
+void reduce_scatter(int64_t id, const at::Tensor& out, const at::Tensor& inp) {
+  Comm& c = get(id);
+  check_io(c, inp, "input");
+  check_io(c, out, "output");
+  TORCH_CHECK(out.scalar_type() == inp.scalar_type() && inp.numel() == out.numel() * c.world, "xgmi reduce_scatter: shape");
+  const int64_t bytes = inp.numel() * inp.element_size();
+  TORCH_CHECK(bytes <= c.capacity, "xgmi: message of ", bytes, " B exceeds the workspace (", c.capacity, " B)");
+  c10::DeviceGuard g(inp.device());
+  hipStream_t st = cur_stream();
+  ++c.epoch;
+  stage(c, inp, st);
+  barrier(c, 0, st);
+  const int64_t n16 = out.numel() * out.element_size() / 16;
+  auto* o = reinterpret_cast<u32x4*>(out.data_ptr());
+  if (inp.scalar_type() == at::kBFloat16)
+    reduce_kernel<true><<<grid_for(n16), 256, 0, st>>>(c.peers, c.rank, c.world, o, (int64_t)c.rank * n16, n16);
+  else
+    reduce_kernel<false><<<grid_for(n16), 256, 0, st>>>(c.peers, c.rank, c.world, o, (int64_t)c.rank * n16, n16);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  barrier(c, 1, st);
+}
+
+void all_reduce(int64_t id, const at::Tensor& inout) {
+  Comm& c = get(id);
+  check_io(c, inout, "tensor");
+  const int64_t bytes = inout.numel() * inout.element_size();
+  TORCH_CHECK(bytes <= c.capacity, "xgmi: message of ", bytes, " B exceeds the workspace (", c.capacity, " B)");
+  c10::DeviceGuard g(inout.device());
+  hipStream_t st = cur_stream();
+  ++c.epoch;
+  stage(c, inout, st);
+  barrier(c, 0, st);
+  const int64_t n16 = bytes / 16;
+  auto* o = reinterpret_cast<u32x4*>(inout.data_ptr());
+  if (inout.scalar_type() == at::kBFloat16)
+    reduce_kernel<true><<<grid_for(n16), 256, 0, st>>>(c.peers, c.rank, c.world, o, 0, n16);
+  else
+    reduce_kernel<false><<<grid_for(n16), 256, 0, st>>>(c.peers, c.rank, c.world, o, 0, n16);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  barrier(c, 1, st);
+}
+
+TORCH_LIBRARY(dtg_xgmi, m) {
+  m.def("create(int capacity, int rank, int world, int device) -> int", &create);
+  m.def("ipc_handle(int id) -> Tensor", &ipc_handle);
+  m.def("open_peers(int id, Tensor handles) -> ()", &open_peers);
+  m.def("set_timeout(int id, float seconds) -> ()", &set_timeout);
+  m.def("error(int id) -> int", &error);
+  m.def("destroy(int id) -> ()", &destroy);
+  m.def("all_gather(int id, Tensor(a!) out, Tensor inp) -> ()", &all_gather);
+  m.def("reduce_scatter(int id, Tensor(a!) out, Tensor inp) -> ()", &reduce_scatter);
+  m.def("all_reduce(int id, Tensor(a!) inout) -> ()", &all_reduce);
+}
+
+}  // namespace xgmi
+}  // namespace dtg

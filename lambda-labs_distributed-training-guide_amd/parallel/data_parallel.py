@@ -109,7 +109,7 @@ class DataParallel:
 
     def _on_grad(self, p):
         if getattr(p, "_dtg_sequence_parallel", False) and self.tp_group is not None:
-            dist.all_reduce(p.main_grad, group=self.tp_group)
+            comm.all_reduce_(p.main_grad, self.tp_group)
         if not self._sync_enabled or (self.mode == "single" and not self.overlap_optimizer):
             return
         b = p._dtg_bucket

@@ -46,17 +46,13 @@ class _CopyToTP(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        dy = dy.contiguous().clone()
-        dist.all_reduce(dy, group=ctx.group)
-        return dy, None
+        return comm.all_reduce_(dy.contiguous().clone(), ctx.group), None
 
 
 class _ReduceFromTP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, group):
-        x = x.contiguous().clone()
-        dist.all_reduce(x, group=group)
-        return x
+        return comm.all_reduce_(x.contiguous().clone(), group)
 
     @staticmethod
     def backward(ctx, dy):

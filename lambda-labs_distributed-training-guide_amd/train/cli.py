@@ -42,6 +42,11 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
         p.add_argument("--shard-size", default=None, type=int, help="ranks per shard group (default LOCAL_WORLD_SIZE)")
     if chapter == "07":
         p.add_argument("--tp", default=8, type=int)
+    if chapter in ("06", "07"):
+        p.add_argument("--tp-comm", default="rccl", choices=["rccl", "xgmi"],
+                       help="TP/SP all-gather / reduce-scatter / all-reduce: RCCL, or the direct-peer xGMI "
+                            "library (csrc/comm/xgmi.hip; one node per TP group)")
+        p.add_argument("--tp-comm-mb", default=256, type=int, help="xGMI workspace per rank (largest TP message)")
     if chapter == "deepspeed":
         p.add_argument("--local_rank", type=int, default=None)
         p.add_argument("--deepspeed", action="store_true", help="accepted for launcher compatibility")

@@ -23,13 +23,48 @@ def rank(group=None) -> int:
     return dist.get_rank(group) if dist.is_initialized() else 0
 
 
+# Direct-peer xGMI communicators (dtg.parallel.xgmi) registered per process group: the TP/SP
+# helpers below route GPU messages that fit the communicator's workspace through them and
+# everything else through RCCL.
+_XGMI = {}
+
+
+def register_xgmi(group, communicator):
+    _XGMI[group] = communicator
+
+
+def unregister_xgmi(group):
+    return _XGMI.pop(group, None)
+
+
+def _xgmi_for(group, x: torch.Tensor, nbytes: int):
+    c = _XGMI.get(group)
+    if c is not None and x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and c.fits(nbytes):
+        return c
+    return None
+
+
 def all_gather_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
     n = world(group)
     if n == 1:
         return x
     out = torch.empty((x.shape[0] * n,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    c = _xgmi_for(group, x, x.numel() * x.element_size())
+    if c is not None:
+        return c.all_gather_into(out, x)
     dist.all_gather_into_tensor(out, x, group=group)
     return out
+
+
+def all_reduce_(x: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place sum all-reduce (one-shot xGMI for small TP messages when registered)."""
+    if world(group) == 1:
+        return x
+    c = _xgmi_for(group, x, x.numel() * x.element_size())
+    if c is not None and x.is_contiguous():
+        return c.all_reduce_(x)
+    dist.all_reduce(x, group=group)
+    return x
 
 
 def reduce_scatter_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
@@ -44,6 +79,9 @@ def reduce_scatter_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
         r = rank(group)
         return y[r * chunk:(r + 1) * chunk].contiguous()
     out = torch.empty((chunk,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    c = _xgmi_for(group, x, x.numel() * x.element_size())
+    if c is not None:
+        return c.reduce_scatter_into(out, x)
     dist.reduce_scatter_tensor(out, x, group=group)
     return out
 

@@ -1,0 +1,77 @@
+"""Tensor + sequence parallel Llama (tp=2) on the GPU with its TP collectives on the direct-peer
+xGMI library == the same model on one device (loss and every gradient).
+
+Both ranks share the box's one GPU (see test_xgmi_gpu.py); the process group is gloo, used only
+for the handle exchange and the loss head's MAX all-reduce -- every sequence all-gather /
+reduce-scatter / TP all-reduce of the model runs through csrc/comm/xgmi.hip.
+"""
+import pytest
+import torch
+
+from _dist import run_distributed
+
+pytestmark = pytest.mark.gpu
+MODEL = "llama-tiny-d128"
+
+
+def _ids(vocab):
+    g = torch.Generator().manual_seed(0)
+    return torch.randint(0, vocab, (2, 64), generator=g)
+
+
+def _grads(model):
+    return {n: p.main_grad.detach().float().cpu().clone() for n, p in model.named_parameters()}
+
+
+def _run(model, eng, ids):
+    eng.zero_grad()
+    out = model(input_ids=ids, labels=ids)
+    eng.backward(out.loss)
+    return out.loss.item()
+
+
+def _worker(rank, world):
+    import torch.distributed as dist
+
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import DataParallel
+    from dtg.parallel.tensor_parallel import make_mesh, shard_full_state_dict
+    from dtg.parallel.xgmi import XgmiCommunicator
+    from dtg.utils import comm as dcomm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    _, tp_group, _, tp_rank, _ = make_mesh(2)
+    dcomm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=16 << 20, device=dev, timeout_s=5.0))
+    cfg = resolve_config(MODEL)
+    torch.manual_seed(0)
+    full = build_model(cfg, device="cpu", dtype=torch.bfloat16)
+    model = build_model(cfg, device=dev, tp_group=tp_group, init=False)
+    model.load_state_dict(shard_full_state_dict(full.state_dict(), cfg, tp_rank, 2))
+    eng = DataParallel(model, mode="single", tp_group=tp_group, broadcast_from_rank0=False)
+    loss = _run(model, eng, _ids(cfg.vocab_size).to(dev))
+    torch.cuda.synchronize()
+    dcomm._XGMI[tp_group].check()
+    res = (loss, _grads(model), tp_rank)
+    dist.barrier()
+    return res
+
+
+def test_tp2_xgmi_matches_single_device(cuda):
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import DataParallel
+    from dtg.parallel.tensor_parallel import unshard_state_dicts
+
+    cfg = resolve_config(MODEL)
+    torch.manual_seed(0)
+    ref = build_model(cfg, device="cpu", dtype=torch.bfloat16).to(cuda)
+    eng = DataParallel(ref, mode="single")
+    ref_loss = _run(ref, eng, _ids(cfg.vocab_size).to(cuda))
+    ref_g = _grads(ref)
+    res = run_distributed(_worker, 2)
+    assert abs(res[0][0] - ref_loss) < 2e-2 * abs(ref_loss) and res[0][0] == res[1][0]
+    shards = [r[1] for r in sorted(res, key=lambda r: r[2])]
+    full = unshard_state_dicts(shards, cfg)
+    for n, g in ref_g.items():
+        rel = ((full[n] - g).norm() / g.norm().clamp_min(1e-12)).item()
+        assert rel < 3e-2, (n, rel)

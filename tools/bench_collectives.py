@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
-"""RCCL collective bandwidth over xGMI: all_reduce, all_gather,
+"""Collective bandwidth over xGMI: all_reduce, all_gather,
 reduce_scatter and all_to_all over message sizes, reported as algorithm and bus bandwidth
 (nccl-tests conventions), so bucket sizes for DDP/ZeRO/FSDP can be chosen from measurements.
+`--impl xgmi` runs all_reduce / all_gather / reduce_scatter on the direct-peer library
+(csrc/comm/xgmi.hip) instead of RCCL, for the TP/SP message sizes.
 
     torchrun --standalone --nproc-per-node 8 tools/bench_collectives.py --json > coll.jsonl
+    torchrun --standalone --nproc-per-node 8 tools/bench_collectives.py --impl xgmi --max-mb 128
 """
 import argparse
 import json
@@ -15,20 +18,20 @@ import torch
 import torch.distributed as dist
 
 
-def bench(op, nbytes, world, device, iters, warmup):
+def bench(op, nbytes, world, device, iters, warmup, xg=None):
     n = nbytes // 2
     x = torch.randn(n, device=device).bfloat16()
     if op == "all_reduce":
-        fn = lambda: dist.all_reduce(x)
+        fn = (lambda: xg.all_reduce_(x)) if xg else (lambda: dist.all_reduce(x))
         factor = 2 * (world - 1) / world
     elif op == "all_gather":
         out = torch.empty(n * world, device=device, dtype=torch.bfloat16)
-        fn = lambda: dist.all_gather_into_tensor(out, x)
+        fn = (lambda: xg.all_gather_into(out, x)) if xg else (lambda: dist.all_gather_into_tensor(out, x))
         factor = (world - 1) / world
         nbytes = nbytes * world
     elif op == "reduce_scatter":
         out = torch.empty(n // world, device=device, dtype=torch.bfloat16)
-        fn = lambda: dist.reduce_scatter_tensor(out, x)
+        fn = (lambda: xg.reduce_scatter_into(out, x)) if xg else (lambda: dist.reduce_scatter_tensor(out, x))
         factor = (world - 1) / world
     else:
         out = torch.empty_like(x)
@@ -55,23 +58,36 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--impl", default="rccl", choices=["rccl", "xgmi"])
     a = ap.parse_args()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     dist.init_process_group("nccl", device_id=device)
     world, rank = dist.get_world_size(), dist.get_rank()
+    xg = None
+    ops = a.ops.split(",")
+    if a.impl == "xgmi":
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+        from dtg.parallel.xgmi import XgmiCommunicator
+
+        xg = XgmiCommunicator(None, capacity_bytes=int(a.max_mb * (1 << 20)) + (1 << 20), device=device)
+        ops = [o for o in ops if o != "all_to_all"]
     size = a.min_mb
     while size <= a.max_mb:
         nbytes = int(size * (1 << 20)) // (2 * world) * (2 * world)
-        for op in a.ops.split(","):
-            us, alg, bus = bench(op, nbytes, world, device, a.iters, a.warmup)
+        for op in ops:
+            us, alg, bus = bench(op, nbytes, world, device, a.iters, a.warmup, xg)
             if rank == 0:
-                rec = {"op": op, "bytes": nbytes, "world": world, "time_us": round(us, 1), "algbw_GBps": round(alg, 2),
+                rec = {"op": op, "impl": a.impl, "bytes": nbytes, "world": world, "time_us": round(us, 1),
+                       "algbw_GBps": round(alg, 2),
                        "busbw_GBps": round(bus, 2)}
                 print(json.dumps(rec) if a.json else f"{op:15s} {nbytes / 2**20:9.1f} MiB {us:10.1f} us  "
                       f"algbw {alg:7.1f} GB/s  busbw {bus:7.1f} GB/s", flush=True)
         size *= 2
+    if xg is not None:
+        xg.check()
+        xg.close()
     dist.destroy_process_group()
 
 
