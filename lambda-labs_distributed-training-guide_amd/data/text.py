@@ -61,3 +61,11 @@ def load_and_preprocess(dataset_name: str, tokenizer_name: str, seq_length, max_
     grouped = tokenized.map(group_texts, batched=True, num_proc=num_proc, desc=f"Grouping texts in chunks of {seq_length}")
     grouped = grouped.remove_columns([c for c in grouped.column_names if c not in ("input_ids", "labels")])
     return grouped.with_format("torch"), seq_length
+
+
+def add_custom_tokens(tokenizer, n: int = 28683, prefix: str = "<custom_token_"):
+    """Extend a tokenizer by `n` special tokens `<custom_token_i>` (the rime chapter adds 28,683,
+    reference 00-rime/train_llm_01-single-gpu.py:62-66); returns the new vocabulary size, to be
+    passed to `dtg.models.resize_token_embeddings` (or used as the config's vocab_size)."""
+    tokenizer.add_tokens([f"{prefix}{i}>" for i in range(n)], special_tokens=True)
+    return len(tokenizer)

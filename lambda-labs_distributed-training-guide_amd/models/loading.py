@@ -37,8 +37,16 @@ def _fused_full(hf: _LazyHF, name: str, cfg):
         p = "model." + name[: -len("gate_up_proj.weight")]
         return torch.cat([hf.get(p + "gate_proj.weight"), hf.get(p + "up_proj.weight")], 0)
     if name == "lm_head.weight":
-        return hf.get("lm_head.weight")
-    return hf.get("model." + name)
+        t = hf.get("lm_head.weight")
+    else:
+        t = hf.get("model." + name)
+    if name in ("embed_tokens.weight", "lm_head.weight") and t.shape[0] < cfg.vocab_size:
+        # pretrained vocabulary smaller than the config (rime: 128,256 -> 156,939 tokens):
+        # resize_token_embeddings semantics, new rows = mean of the pretrained rows
+        from . import mean_resized_rows
+
+        t = mean_resized_rows(t, cfg.vocab_size)
+    return t
 
 
 @torch.no_grad()

@@ -86,3 +86,15 @@ def test_resumable_sampler_skips_consumed_samples():
         assert list(s) == full[10:] and len(s) == len(full) - 10 and s.full_len() == len(full)
         s.set_epoch(4)
         assert list(s) != full and sorted(list(s)) != []
+
+
+def test_add_custom_tokens_extends_vocab(tmp_path):
+    from transformers import AutoTokenizer
+
+    from dtg.data.text import add_custom_tokens
+
+    tok = AutoTokenizer.from_pretrained(_local_tokenizer(tmp_path))
+    n0 = len(tok)
+    assert add_custom_tokens(tok, 5) == n0 + 5
+    ids = tok("<custom_token_3>", add_special_tokens=False)["input_ids"]
+    assert ids == [n0 + 3]

@@ -93,3 +93,26 @@ def test_bundled_configs_param_counts():
         assert abs(got - n) / n < 0.01, (name, got)
     assert resolve_config("meta-llama/Llama-3.1-8B").rope_scaling["rope_type"] == "llama3"
     assert resolve_config("openai-community/gpt2").n_layer == 12
+
+
+@pytest.mark.parametrize("name", ["llama-tiny-d128", "llama-tiny", "gpt2-tiny"])
+def test_resize_token_embeddings_mean_rows(name):
+    """vocabulary extension keeps old rows, new rows = mean, ties preserved, trains."""
+    from dtg.models import build_model, resize_token_embeddings
+
+    torch.manual_seed(0)
+    m = build_model(name, device="cpu", dtype=torch.float32)
+    old = m.lm_head_weight().detach().clone()
+    V = old.shape[0]
+    resize_token_embeddings(m, V + 37)
+    w = m.lm_head_weight()
+    assert w.shape[0] == V + 37 and m.config.vocab_size == V + 37
+    assert torch.equal(w[:V], old)
+    torch.testing.assert_close(w[V:], old.mean(0, keepdim=True).expand(37, -1))
+    if m.config.tie_word_embeddings:
+        emb = m.wte.weight if hasattr(m, "wte") else m.embed_tokens.weight
+        assert emb is w
+    ids = torch.randint(V, V + 37, (2, 16))
+    out = m(input_ids=ids, labels=ids)
+    out.loss.backward()
+    assert torch.isfinite(out.loss)
