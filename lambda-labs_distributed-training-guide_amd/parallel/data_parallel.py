@@ -258,8 +258,10 @@ class DataParallel:
                 w.wait()
 
     def _install_gather_hooks(self):
-        """Map modules -> buckets they read: each decoder layer waits for its own buckets, the
-        root waits for the buckets of parameters outside the layers (embedding, norm, head)."""
+        """Map modules -> buckets they read: the root waits only for the embedding's buckets,
+        each decoder layer for its own, and the final norm / untied lm_head buckets are waited
+        for after the last layer.  Gathers are issued in that order, so the first layer starts
+        as soon as the embedding has landed instead of behind the 1 GB lm_head gather."""
         bucket_of = {id(p): p._dtg_bucket.index for p in self.params}
         layers = list(getattr(self.module, "layers", []))
         in_layer = set()
@@ -270,10 +272,17 @@ class DataParallel:
                 in_layer.add(id(p))
             layer.register_forward_pre_hook(lambda m, a, _bs=bs: self.wait_param_gather(_bs))
             order.extend(bs)
-        root_bs = sorted({bucket_of[id(p)] for p in self.params if id(p) not in in_layer})
-        self.module.register_forward_pre_hook(lambda m, a: self.wait_param_gather(root_bs))
+        outside = [p for p in self.params if id(p) not in in_layer]
+        first = ("embed", "wte", "wpe")
+        pre_bs = sorted({bucket_of[id(p)] for p in outside if any(k in getattr(p, "_dtg_name", "") for k in first)})
+        post_bs = sorted({bucket_of[id(p)] for p in outside} - set(pre_bs))
+        if not layers:
+            pre_bs, post_bs = sorted(set(pre_bs) | set(post_bs)), []
+        self.module.register_forward_pre_hook(lambda m, a: self.wait_param_gather(pre_bs))
+        if post_bs:
+            layers[-1].register_forward_hook(lambda m, a, o: self.wait_param_gather(post_bs))
         seen, ag_order = set(), []
-        for i in root_bs + order + list(range(len(self.space.buckets))):
+        for i in pre_bs + order + post_bs + list(range(len(self.space.buckets))):
             if i not in seen:
                 seen.add(i)
                 ag_order.append(i)
