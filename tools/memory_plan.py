@@ -63,10 +63,22 @@ def main():
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--ac", action="store_true")
     ap.add_argument("--offload", action="store_true")
+    ap.add_argument("--exact", action="store_true",
+                    help="also print the exact FSDP unit layout (dtg.parallel.plan on a meta-device model)")
     a = ap.parse_args()
     r = plan(a.model, a.world, a.tp, a.strategy, a.batch, a.seq, a.ac, a.offload)
     for k, v in r.items():
         print(f"{k:20s} {v:.2f}" if isinstance(v, float) else f"{k:20s} {v}")
+    if a.exact and a.tp == 1:
+        from dtg.models import build_model
+        from dtg.parallel.plan import fsdp_plan
+
+        fp = fsdp_plan(build_model(a.model, device="meta", init=False), a.world)
+        print(f"{'fsdp_units':20s} {len(fp.units)} + root")
+        print(f"{'shard_elems/rank':20s} {fp.shard_numel}")
+        print(f"{'state_gb/rank':20s} {fp.per_rank_state_bytes() / 1e9:.2f}")
+        print(f"{'largest_gather_gb':20s} {fp.largest_gather_bytes() / 1e9:.3f}")
+        print(f"{'padding':20s} {100 * fp.padding_fraction():.4f} %")
 
 
 if __name__ == "__main__":
