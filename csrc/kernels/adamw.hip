@@ -68,8 +68,34 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ p, fl
   const float step_size = h.lr / h.bc1;
   const float decay = 1.f - h.lr * h.wd;
   if constexpr (VEC) {
+    // Two 8-element vectors per lane per iteration (the second one grid-stride away): eight
+    // 16-byte loads in flight per lane before the first use, which is what lifts this purely
+    // streaming kernel toward HBM bandwidth (4 in flight left it latency-bound).
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
-    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < n; i += stride) {
+    int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    for (; i + stride < n; i += 2 * stride) {
+      float pv[2][8], gv[2][8], mv[2][8], vv[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t k = i + u * stride;
+        if (MASTER) ld8<float>(master + k, pv[u]); else load8(p + k, pv[u]);
+        ld8<GT>(g + k, gv[u]);
+        ld8<ST>(m + k, mv[u]);
+        ld8<ST>(v + k, vv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t k = i + u * stride;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          adam_elem(pv[u][j], gv[u][j] * h.grad_scale, mv[u][j], vv[u][j], h, step_size, decay);
+        st8<ST>(m + k, mv[u]);
+        st8<ST>(v + k, vv[u]);
+        if (MASTER) st8<float>(master + k, pv[u]);
+        store8(p + k, pv[u]);
+      }
+    }
+    if (i < n) {
       float pv[8], gv[8], mv[8], vv[8];
       if (MASTER) ld8<float>(master + i, pv); else load8(p + i, pv);
       ld8<GT>(g + i, gv);

@@ -61,6 +61,9 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_fwd_kernel(
 
 // dx = rstd * (g - n * mean(g * n)),  g = dy * w,  n = x * rstd  (+ dres if given)
 // dw_partial[block][col] = sum over this block's rows of dy * bf16(n)
+// Rows are software-pipelined: the next row's x / dy / dres vectors are loaded (as raw 16-byte
+// words) before the current row's block reduction, so every lane keeps its loads in flight
+// across the two barriers of block_sum instead of issuing them after it.
 template <int PER, bool DRES>
 __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, int64_t x_stride,
@@ -80,38 +83,48 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
   }
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(T, r0 + rows_per_block);
+  const u16x8 z{0, 0, 0, 0, 0, 0, 0, 0};
+  u16x8 nx[PER], nd[PER], nr[PER];
+  auto fetch = [&](int row) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * kNormThreads;
+      const bool ok = c < nch && row < r1;
+      nx[i] = ok ? *reinterpret_cast<const u16x8*>(x + row * x_stride + c * 8) : z;
+      nd[i] = ok ? *reinterpret_cast<const u16x8*>(dy + (int64_t)row * H + c * 8) : z;
+      if constexpr (DRES) nr[i] = ok ? *reinterpret_cast<const u16x8*>(dres + (int64_t)row * H + c * 8) : z;
+    }
+  };
+  if (r0 < r1) fetch(r0);
   for (int row = r0; row < r1; ++row) {
     const float rstd = rstd_in[row];
+    u16x8 cr[PER];
     float xv[PER][8], g[PER][8];
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int c = threadIdx.x + i * kNormThreads;
-      if (c < nch) {
-        float d[8];
-        load8(x + row * x_stride + c * 8, xv[i]);
-        load8(dy + (int64_t)row * H + c * 8, d);
+      if constexpr (DRES) cr[i] = nr[i];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float n = xv[i][j] * rstd;
-          g[i][j] = d[j] * wv[i][j];
-          dot += g[i][j] * n;
-          dwacc[i][j] += d[j] * bf2f(f2bf(n));
-        }
+      for (int j = 0; j < 8; ++j) {
+        xv[i][j] = bf2f(nx[i][j]);
+        const float d = bf2f(nd[i][j]);
+        const float n = xv[i][j] * rstd;
+        g[i][j] = d * wv[i][j];
+        dot += g[i][j] * n;
+        dwacc[i][j] += d * bf2f(f2bf(n));
       }
     }
+    fetch(row + 1);  // in flight across the reduction below
     dot = block_sum(dot, scratch) / H;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + i * kNormThreads;
       if (c < nch) {
         float o[8];
-        float dr[8];
-        if constexpr (DRES) load8(dres + (int64_t)row * H + c * 8, dr);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           o[j] = rstd * (g[i][j] - xv[i][j] * rstd * dot);
-          if constexpr (DRES) o[j] += dr[j];
+          if constexpr (DRES) o[j] += bf2f(cr[i][j]);
         }
         store8(dx + (int64_t)row * H + c * 8, o);
       }
@@ -227,7 +240,9 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy_, const at::
   auto dx = at::empty({T, H}, x.options());
   auto dw = at::empty({H}, w.options());
   if (T == 0) { dw.zero_(); return {dx, dw}; }
-  // ~2 workgroups per CU worth of blocks keeps the partial-dw matrix small.
+  // ~2 workgroups per CU worth of blocks keeps the partial-dw matrix (and colsum) small; the
+  // kernel's row pipelining provides the memory-level parallelism (2048 blocks measured
+  // 103 us + 84 us colsum vs 128 + 18 at 512 unpipelined, Llama-8B shape).
   const int nblk = std::min(T, 512);
   const int rpb = (T + nblk - 1) / nblk;
   const int nb = (T + rpb - 1) / rpb;
