@@ -61,10 +61,19 @@ __device__ __forceinline__ void adam_elem(float& pv, float gv, float& mv, float&
 
 // Vector body: 8 elements per lane per iteration with 16/32-byte accesses (requires n % 8 == 0
 // and 16-byte aligned buffers, which the flat stores guarantee); scalar kernel otherwise.
+// `dev_hyper` (optional, f32 [3] = lr, 1 - beta1^t, sqrt(1 - beta2^t)) overrides the launch
+// arguments: a HIP-graph-captured step replays the same kernel arguments every time, so the
+// step-dependent values live in device memory the host rewrites before each replay.
 template <typename GT, typename ST, bool MASTER, bool VEC>
 __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ p, float* __restrict__ master,
                                                     const GT* __restrict__ g, ST* __restrict__ m,
-                                                    ST* __restrict__ v, int64_t n, AdamHyper h) {
+                                                    ST* __restrict__ v, int64_t n, AdamHyper h,
+                                                    const float* __restrict__ dev_hyper) {
+  if (dev_hyper != nullptr) {
+    h.lr = dev_hyper[0];
+    h.bc1 = dev_hyper[1];
+    h.bc2_sqrt = dev_hyper[2];
+  }
   const float step_size = h.lr / h.bc1;
   const float decay = 1.f - h.lr * h.wd;
   if constexpr (VEC) {
@@ -124,7 +133,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ p, fl
 
 void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g,
             const at::Tensor& m, const at::Tensor& v, double lr, double beta1, double beta2,
-            double eps, double wd, int64_t step, double grad_scale) {
+            double eps, double wd, int64_t step, double grad_scale, const c10::optional<at::Tensor>& hyper) {
   DTG_CHECK_CUDA_BF16(p);
   DTG_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(),
             "adamw_: buffers must be contiguous");
@@ -133,6 +142,12 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   DTG_CHECK(m.scalar_type() == v.scalar_type(), "adamw_: exp_avg/exp_avg_sq dtype mismatch");
   DTG_CHECK(step >= 1, "adamw_: step must be >= 1");
   const bool has_master = master.has_value() && master->defined();
+  const float* hp = nullptr;
+  if (hyper.has_value() && hyper->defined()) {
+    DTG_CHECK(hyper->is_cuda() && hyper->scalar_type() == at::kFloat && hyper->numel() >= 3 && hyper->is_contiguous(),
+              "adamw_: hyper must be a contiguous f32 GPU tensor [lr, 1-beta1^t, sqrt(1-beta2^t)]");
+    hp = hyper->data_ptr<float>();
+  }
   if (has_master)
     DTG_CHECK(master->scalar_type() == at::kFloat && master->numel() == n && master->is_contiguous(),
               "adamw_: master must be contiguous f32");
@@ -161,10 +176,10 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
 #define DTG_ADAM_LAUNCH(GT, ST, MASTER)                                                      \
   do { if (vec) adamw_kernel<GT, ST, MASTER, true><<<blocks, threads, 0, stream()>>>(            \
       bf16_mut(p), mp, reinterpret_cast<const GT*>(g.data_ptr()), reinterpret_cast<ST*>(m.data_ptr()), \
-      reinterpret_cast<ST*>(v.data_ptr()), n, h);                                           \
+      reinterpret_cast<ST*>(v.data_ptr()), n, h, hp);                                       \
   else adamw_kernel<GT, ST, MASTER, false><<<blocks, threads, 0, stream()>>>(               \
       bf16_mut(p), mp, reinterpret_cast<const GT*>(g.data_ptr()), reinterpret_cast<ST*>(m.data_ptr()), \
-      reinterpret_cast<ST*>(v.data_ptr()), n, h); } while (0)
+      reinterpret_cast<ST*>(v.data_ptr()), n, h, hp); } while (0)
   if (has_master) {
     if (gb && sb) DTG_ADAM_LAUNCH(uint16_t, uint16_t, true);
     else if (gb) DTG_ADAM_LAUNCH(uint16_t, float, true);

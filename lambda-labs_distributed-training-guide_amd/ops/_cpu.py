@@ -109,15 +109,17 @@ def ce_grad_(logits, labels, lse, vocab_start, ignore_index, grad_scale):
     logits.copy_(g.to(logits.dtype))
 
 
-def adamw_(p, master, g, m, v, lr, beta1, beta2, eps, wd, step, grad_scale):
+def adamw_(p, master, g, m, v, lr, beta1, beta2, eps, wd, step, grad_scale, hyper=None):
+    bc1 = 1 - beta1**step
+    bc2 = math.sqrt(1 - beta2**step)
+    if hyper is not None:
+        lr, bc1, bc2 = (float(x) for x in hyper[:3].tolist())
     pf = master if master is not None else p.float()
     gf = g.float() * grad_scale
     mf, vf = m.float(), v.float()
     pf = pf * (1 - lr * wd)
     mf = mf + (gf - mf) * (1 - beta1)
     vf = vf * beta2 + (1 - beta2) * gf * gf
-    bc1 = 1 - beta1**step
-    bc2 = math.sqrt(1 - beta2**step)
     pf = pf - (lr / bc1) * mf / (vf.sqrt() / bc2 + eps)
     m.copy_(mf)
     v.copy_(vf)

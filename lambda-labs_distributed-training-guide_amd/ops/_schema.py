@@ -21,7 +21,7 @@ _DEFS = [
     "ce_stats(Tensor logits, Tensor labels, int vocab_start) -> (Tensor, Tensor, Tensor)",
     "ce_grad_(Tensor(a!) logits, Tensor labels, Tensor lse, int vocab_start, int ignore_index, float grad_scale) -> ()",
     "adamw_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!) m, Tensor(d!) v, float lr, float beta1, "
-    "float beta2, float eps, float wd, int step, float grad_scale) -> ()",
+    "float beta2, float eps, float wd, int step, float grad_scale, Tensor? hyper=None) -> ()",
     "adamw_cpu_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float lr, float beta1, float beta2, "
     "float eps, float wd, int step, float grad_scale) -> ()",
     "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> (Tensor, Tensor)",

@@ -92,6 +92,9 @@ class DataParallel:
         self._hparams = None  # () -> (lr, beta1, beta2, eps, weight_decay); set by FlatAdamW
         self._opt_stream = torch.cuda.Stream(device=dev) if (overlap_optimizer and dev.type == "cuda") else None
         self._bwd_stepped = False
+        # device [lr, 1-beta1^t, sqrt(1-beta2^t)] read by AdamW instead of host scalars while a
+        # HIP graph of the step is captured / replayed (dtg.train.graph.GraphedStep)
+        self.graph_hyper = None
         # The engine owns the loss: backward(loss) uses an implicit gradient of 1 and any
         # scaling goes into AdamW's grad_scale, which lets the loss head write dW in place.
         set_direct_loss_grad(True)
@@ -165,7 +168,7 @@ class DataParallel:
             pv, gv, lo, hi = buf[b.start:b.end], self.space.grad_buf[b.start:b.end], b.start, b.end
         adamw_step(pv, gv, self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], lr=lr, step=self.step_count, beta1=beta1,
                    beta2=beta2, eps=eps, weight_decay=wd, grad_scale=scale,
-                   master=None if self.master is None else self.master[lo:hi])
+                   master=None if self.master is None else self.master[lo:hi], hyper=self.graph_hyper)
 
     def finish_grad_sync(self):
         """Call after backward (the last micro-batch): flush unlaunched buckets, wait for all."""
@@ -222,12 +225,12 @@ class DataParallel:
                 adamw_step(self.space.param_buf[s:e], self.grad_shard[o:o + n], self.exp_avg[o:o + n],
                            self.exp_avg_sq[o:o + n], lr=lr, step=self.step_count, beta1=beta1, beta2=beta2,
                            eps=eps, weight_decay=weight_decay, grad_scale=grad_scale,
-                           master=None if self.master is None else self.master[o:o + n])
+                           master=None if self.master is None else self.master[o:o + n], hyper=self.graph_hyper)
             self._allgather_params(wait=not self.overlap_param_gather)
         else:
             adamw_step(self.space.param_buf, self.space.grad_buf, self.exp_avg, self.exp_avg_sq, lr=lr,
                        step=self.step_count, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
-                       grad_scale=grad_scale, master=self.master)
+                       grad_scale=grad_scale, master=self.master, hyper=self.graph_hyper)
 
     def _allgather_params(self, wait: bool = True):
         """ZeRO: every rank updated its slice of each bucket; all-gather them in place, in the

@@ -1,0 +1,85 @@
+"""HIP-graph captured training step (dtg.train.graph) == the eager loop, step for step."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(name, dev):
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    torch.manual_seed(0)
+    model = build_model(name, device=dev)
+    eng = DataParallel(model, mode="single")
+    opt = FlatAdamW(eng, lr=1e-3)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10, eta_min=1e-4)
+    return model, eng, opt, sched
+
+
+@pytest.mark.parametrize("name", ["llama-tiny-d128", "gpt2-tiny"])
+def test_graphed_step_matches_eager(cuda, name):
+    from dtg.train.graph import GraphedStep
+
+    g = torch.Generator().manual_seed(1)
+    model, eng, opt, sched = _setup(name, cuda)
+    V = model.config.vocab_size
+    batches = [torch.randint(0, V, (2, 128), generator=g).to(cuda) for _ in range(7)]
+    nv = 2 * 127
+    if name.startswith("gpt2"):
+        model.eval()  # dropout off: eager and replay draw different RNG offsets otherwise
+    init = {n: p.detach().float().clone() for n, p in model.named_parameters()}
+    ref_losses = []
+    for b in batches:
+        opt.zero_grad()
+        out = model(input_ids=b, labels=b, num_valid=nv)
+        eng.backward(out.loss)
+        opt.step()
+        sched.step()
+        ref_losses.append(out.loss.item())
+    ref = {n: p.detach().clone() for n, p in model.named_parameters()}
+
+    model, eng, opt, sched = _setup(name, cuda)
+    if name.startswith("gpt2"):
+        model.eval()
+    step = GraphedStep(model, eng, opt, sched, warmup=2, num_valid=nv)
+    losses = [step({"input_ids": b, "labels": b}).item() for b in batches]
+    assert step.graph is not None and step.steps == 7
+    torch.cuda.synchronize()
+    # hipBLASLt may pick other (equally valid) GEMM algorithms inside a capture, so the replayed
+    # steps match the eager ones to rounding, not bitwise; a wrong step-dependent AdamW scalar
+    # (lr, bias corrections) would move the loss and the weights far outside these bounds.
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) <= 2e-3 * abs(b), (losses, ref_losses)
+    # Compare the accumulated updates: Adam turns rounding-level gradient differences of
+    # near-zero gradients into +-lr steps, so elementwise bounds are meaningless; a wrong lr or
+    # bias correction would change the update norm by tens of percent.
+    # (1-D parameters are skipped: GPT-2's key bias has an exactly-zero true gradient, so its
+    # Adam updates are the sign of rounding noise in both runs.)
+    for n, p in model.named_parameters():
+        if p.dim() < 2:
+            continue
+        d_graph = p.detach().float() - init[n]
+        d_eager = ref[n].float() - init[n]
+        rel = ((d_graph - d_eager).norm() / d_eager.norm().clamp_min(1e-12)).item()
+        assert rel < 0.05, (n, rel)
+
+
+def test_adamw_device_hyper_matches_scalars(cuda):
+    """The AdamW kernel reading [lr, 1-b1^t, sqrt(1-b2^t)] from device memory == scalar launch."""
+    import math
+
+    torch.manual_seed(0)
+    n = 4096 + 8
+    p0 = torch.randn(n, device=cuda).bfloat16()
+    g = torch.randn(n, device=cuda).bfloat16()
+    m0 = (0.1 * torch.randn(n, device=cuda)).bfloat16()
+    v0 = (0.01 * torch.rand(n, device=cuda)).bfloat16()
+    for step, lr in [(1, 1e-3), (7, 3e-4)]:
+        a = [t.clone() for t in (p0, m0, v0)]
+        b = [t.clone() for t in (p0, m0, v0)]
+        torch.ops.dtg.adamw_(a[0], None, g, a[1], a[2], lr, 0.9, 0.999, 1e-8, 0.01, step, 0.5)
+        hyper = torch.tensor([lr, 1 - 0.9 ** step, math.sqrt(1 - 0.999 ** step)], device=cuda)
+        torch.ops.dtg.adamw_(b[0], None, g, b[1], b[2], 123.0, 0.9, 0.999, 1e-8, 0.01, 99, 0.5, hyper)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
