@@ -88,17 +88,36 @@ class GraphedStep:
         self.engine.step_count = count  # capture ran the host code once: roll its counter back
 
     # ------------------------------------------------------------------ step
-    def __call__(self, batch) -> torch.Tensor:
-        """One training step on `batch` (same shapes every call); returns the device loss.
+    def _replayable(self, batch, num_valid) -> bool:
+        if num_valid is not None and num_valid != self.num_valid:
+            return False
+        return (set(batch) == set(self.static) and
+                all(v.shape == self.static[k].shape and v.dtype == self.static[k].dtype for k, v in batch.items()))
+
+    def __call__(self, batch, num_valid: Optional[int] = None) -> torch.Tensor:
+        """One training step on `batch`; returns the device loss.
 
         The first `warmup` calls run eagerly on a side stream (lazy initialisation, allocator
         warm-up, as graph capture requires); the next call captures the step and every call
-        from then on replays it.  Training semantics are those of the eager loop."""
-        if self.graph is None and self.steps < self.warmup:
+        from then on replays it.  A batch that does not fit the captured one (other shapes or
+        keys, or another `num_valid` -- the loss scale is part of the graph) runs eagerly on
+        the same stream.  Training semantics are those of the eager loop."""
+        if num_valid is not None and self.num_valid is None:
+            self.num_valid = num_valid
+        eager = self.graph is None and self.steps < self.warmup
+        if self.graph is not None and not self._replayable(batch, num_valid):
+            eager = True
+        if eager:
             s = self._stream
             s.wait_stream(torch.cuda.current_stream())
+            saved_nv = self.num_valid
+            if num_valid is not None:
+                self.num_valid = num_valid
             with torch.cuda.stream(s):
+                if self.graph is not None:
+                    self._write_hyper()  # the engine reads AdamW scalars from the device now
                 loss = self._eager(batch)
+            self.num_valid = saved_nv
             torch.cuda.current_stream().wait_stream(s)
         else:
             if self.graph is None:

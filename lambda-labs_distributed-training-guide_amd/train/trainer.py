@@ -219,6 +219,16 @@ def run(chapter: str, argv=None):
     fault_rng = random.Random(args.seed * 1000 + rank + 7 * state["global_step"])
     accum = max(1, args.grad_accum)
     model.train()
+    graphed = None
+    if getattr(args, "hip_graph", "off") == "on":
+        if device.type == "cuda" and getattr(engine, "mode", None) == "single" and accum == 1:
+            from .graph import GraphedStep
+
+            graphed = GraphedStep(model, engine, opt, scheduler=None, warmup=3)
+            LOGGER.info("HIP graph: the training step is captured after 3 eager steps and replayed "
+                        "(time/forward covers the whole step; time/backward and time/update read 0)")
+        else:
+            LOGGER.warning("--hip-graph needs one GPU, a single-process engine and --grad-accum 1; running eagerly")
     for state["epoch"] in range(state["epoch"], args.num_epochs):
         LOGGER.info(f"Begin epoch {state['epoch']} at step {state['epoch_step']}")
         sampler = dataloader.sampler
@@ -244,8 +254,18 @@ def run(chapter: str, argv=None):
                     micro.append(b)
             if args.fault_inject_prob > 0 and fault_rng.random() < args.fault_inject_prob:
                 raise RuntimeError(f"injected fault at global step {state['global_step']} on rank {rank}")
-            opt.zero_grad(set_to_none=True)
-            loss_sum = None
+            if graphed is not None and "position_ids" not in micro[0]:
+                b = dict(micro[0])
+                nv = b.pop("num_valid")
+                b.pop("max_seqlen", None)
+                with timers["forward"]:
+                    loss_sum = graphed(b, num_valid=nv).detach()
+                with timers["update"]:
+                    lr_scheduler.step()
+                micro = []
+            else:
+                opt.zero_grad(set_to_none=True)
+                loss_sum = None
             for j, b in enumerate(micro):
                 ctx = engine.no_sync() if j < accum - 1 else _null()
                 with ctx:
@@ -256,10 +276,11 @@ def run(chapter: str, argv=None):
                     with timers["backward"]:
                         engine.backward(out.loss)
                 loss_sum = out.loss.detach() if loss_sum is None else loss_sum + out.loss.detach()
-            wait_for_peers()
-            with timers["update"]:
-                opt.step()
-                lr_scheduler.step()
+            if micro:
+                wait_for_peers()
+                with timers["update"]:
+                    opt.step()
+                    lr_scheduler.step()
             state["global_step"] += 1
             state["epoch_step"] += 1
             if args.torch_profile_steps > 0:

@@ -83,3 +83,23 @@ def test_adamw_device_hyper_matches_scalars(cuda):
         torch.ops.dtg.adamw_(b[0], None, g, b[1], b[2], 123.0, 0.9, 0.999, 1e-8, 0.01, 99, 0.5, hyper)
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+def test_chapter01_trainer_hip_graph(cuda, tmp_path):
+    """Chapter 01 trainer with --hip-graph on: captured after 3 eager steps, replayed after."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "01-single-gpu", "train_llm.py"), "-e", "hg", "-d", "synthetic",
+           "-m", "llama-tiny-d128", "-s", "256", "-b", "2", "--num-samples", "64", "--save-dir", str(tmp_path),
+           "--log-freq", "4", "--ckpt-freq", "1000", "--num-workers", "0", "--max-steps", "12", "--hip-graph", "on"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=os.path.join(root, "01-single-gpu"))
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "HIP graph" in out
+    recs = [json.loads(x) for x in (tmp_path / "hg" / "metrics-rank0.jsonl").read_text().splitlines()]
+    assert len(recs) == 3 and all(x["running_loss"] == x["running_loss"] for x in recs)
+    assert recs[-1]["time/backward"] == 0.0 and recs[-1]["global_step"] == 12
