@@ -116,3 +116,23 @@ def test_resize_token_embeddings_mean_rows(name):
     out = m(input_ids=ids, labels=ids)
     out.loss.backward()
     assert torch.isfinite(out.loss)
+
+
+def test_gpt2_attention_dropout_path_matches_flash_semantics():
+    """The explicit dropout path (GPT-2 train mode) == the flash op at p=0, dense and packed."""
+    from dtg import ops
+    from dtg.models.gpt2 import _attn_with_dropout
+
+    torch.manual_seed(0)
+    B, S, nh, d = 2, 24, 3, 16
+    T = B * S
+    qkv = torch.randn(T, 3 * nh * d)
+    cu = torch.tensor([0, S, T], dtype=torch.int32)
+    ref = ops.attention(qkv, nh, nh, d, cu, S)
+    torch.testing.assert_close(_attn_with_dropout(qkv, nh, d, cu, 0.0, dense=(B, S)), ref, atol=1e-5, rtol=1e-4)
+    cu2 = torch.tensor([0, 10, 30, T], dtype=torch.int32)
+    ref2 = ops.attention(qkv, nh, nh, d, cu2, 20)
+    torch.testing.assert_close(_attn_with_dropout(qkv, nh, d, cu2, 0.0), ref2, atol=1e-5, rtol=1e-4)
+    x = qkv.clone().requires_grad_()
+    _attn_with_dropout(x, nh, d, cu, 0.1, dense=(B, S)).sum().backward()
+    assert torch.isfinite(x.grad).all()
