@@ -7,46 +7,50 @@
 // K-contiguous copies costs one streaming read + write each, far less than the GEMM time it
 // buys back on the big layers (tools/bench_gemm_layouts.py, profiles/).
 //
-// Tile: 64 rows x 64 columns (8 KB) per 256-thread workgroup.  Loads and stores are 16 B per
-// lane (8 bf16) along the contiguous dimension of each side; the LDS tile is padded by one
-// dword per row so the column-wise LDS gathers of the store phase spread over the banks.
+// Loads and stores are 16 B per lane (8 bf16) along the contiguous dimension of each side; the
+// LDS tile is padded by one dword per row so the column-wise LDS gathers of the store phase
+// spread over the banks.
 #include "common.h"
+
+#include <cstdlib>
 
 namespace dtg {
 
-namespace {
-constexpr int kTile = 64;
-constexpr int kPitch = kTile + 2;  // halfwords per LDS row (33 dwords: odd -> conflict-free columns)
-}  // namespace
-
+// Tiles are TR (input rows = tokens) x TC (input columns) with 256 threads; each side moves
+// 16-byte vectors along its contiguous dimension.  The default 128 x 128 tile makes every
+// output row segment 256 B (64 x 64 writes only 128 B per row at a power-of-two stride of
+// 2*T bytes, which concentrates a launch's stores on few HBM channels).
+template <int TR, int TC>
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ x, int64_t ldx,
                                                              uint16_t* __restrict__ out, int64_t R, int64_t C) {
-  __shared__ uint16_t tile[kTile * kPitch];
-  const int64_t r0 = (int64_t)blockIdx.y * kTile;
-  const int64_t c0 = (int64_t)blockIdx.x * kTile;
+  constexpr int P = TC + 2;             // LDS pitch in halfwords (odd dword count)
+  constexpr int LV = TR * TC / 8 / 256; // 16-byte vectors per thread, each phase
+  __shared__ uint16_t tile[TR * P];
+  const int64_t r0 = (int64_t)blockIdx.y * TR;
+  const int64_t c0 = (int64_t)blockIdx.x * TC;
   const int tid = threadIdx.x;
-  // Load phase: 64 rows x 8 vectors of 8; thread -> (row = tid / 8 + 32 * i, vec = tid % 8).
+  constexpr int VPR = TC / 8;  // vectors per input row
+  constexpr int VPC = TR / 8;  // vectors per output row
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int lr = (tid >> 3) + 32 * i;
-    const int lc = (tid & 7) * 8;
+  for (int i = 0; i < LV; ++i) {
+    const int id = tid + 256 * i;
+    const int lr = id / VPR, lc = (id % VPR) * 8;
     const int64_t r = r0 + lr, c = c0 + lc;
     u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
     if (r < R && c < C) v = *reinterpret_cast<const u16x8*>(x + r * ldx + c);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(tile + lr * kPitch + lc);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(tile + lr * P + lc);
 #pragma unroll
     for (int j = 0; j < 4; ++j) dst[j] = (uint32_t)v[2 * j] | ((uint32_t)v[2 * j + 1] << 16);
   }
   __syncthreads();
-  // Store phase: output row = input column (64 of them), 8 vectors of 8 input rows each.
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int oc = (tid >> 3) + 32 * i;   // input column within the tile
-    const int orr = (tid & 7) * 8;        // first input row of this vector
+  for (int i = 0; i < LV; ++i) {
+    const int id = tid + 256 * i;
+    const int oc = id / VPC, orr = (id % VPC) * 8;  // input column -> output row; first input row
     const int64_t c = c0 + oc, r = r0 + orr;
     u16x8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = tile[(orr + j) * kPitch + oc];
+    for (int j = 0; j < 8; ++j) v[j] = tile[(orr + j) * P + oc];
     if (c < C && r < R) *reinterpret_cast<u16x8*>(out + c * R + r) = v;
   }
 }
@@ -61,9 +65,19 @@ at::Tensor transpose2d(const at::Tensor& x) {
   const c10::DeviceGuard g(x.device());
   auto out = at::empty({C, R}, x.options());
   if (R == 0 || C == 0) return out;
-  const dim3 grid((C + kTile - 1) / kTile, (R + kTile - 1) / kTile);
-  DTG_CHECK(grid.y <= 65535, "transpose2d: too many rows");
-  transpose_bf16_kernel<<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C);
+  static const int tile = [] {
+    const char* e = std::getenv("DTG_TRANSPOSE_TILE");
+    return e ? std::atoi(e) : 128;
+  }();
+  if (tile == 64) {
+    const dim3 grid((C + 63) / 64, (R + 63) / 64);
+    DTG_CHECK(grid.y <= 65535, "transpose2d: too many rows");
+    transpose_bf16_kernel<64, 64><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C);
+  } else {
+    const dim3 grid((C + 127) / 128, (R + 127) / 128);
+    DTG_CHECK(grid.y <= 65535, "transpose2d: too many rows");
+    transpose_bf16_kernel<128, 128><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C);
+  }
   DTG_LAUNCH_CHECK();
   return out;
 }
