@@ -49,9 +49,28 @@ def rng_state(device):
 
 def save_rng(path):
     st = rng_state(None)
-    torch.save({"python": repr(st["python"]), "numpy_keys": torch.from_numpy(st["numpy"][1].astype(np.int64)),
-                "numpy_pos": st["numpy"][2], "torch": st["torch"],
-                "cuda": torch.stack(st["cuda"]) if "cuda" in st else torch.empty(0)}, path)
+    obj = {"python": repr(st["python"]), "numpy_keys": torch.from_numpy(st["numpy"][1].astype(np.int64)),
+           "numpy_pos": st["numpy"][2], "torch": st["torch"],
+           "cuda": torch.stack(st["cuda"]) if "cuda" in st else torch.empty(0)}
+    if isinstance(path, _RngBox):
+        path.obj = obj
+    else:
+        torch.save(obj, path)
+
+
+class _RngBox:
+    """save_rng target that keeps the state object in memory (async checkpoints)."""
+    obj = None
+
+
+def _to_cpu(obj):
+    if torch.is_tensor(obj):
+        return obj.detach().to("cpu", copy=True)
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj
 
 
 def load_rng(path, local_rank: int = 0):
@@ -73,14 +92,11 @@ def _tp_rank(engine):
     return (tp.rank, tp.size) if tp is not None and tp.enabled else (0, 1)
 
 
-def save_sharded(ckpt_dir, engine):
-    """All ranks: write this rank's parameter + optimizer-state slices; rank 0 writes metadata."""
-    ckpt_dir = Path(ckpt_dir)
+def snapshot_sharded(engine):
+    """Collective: copy this rank's parameter + AdamW-moment slices to host memory and gather
+    the slice index of every rank.  Returns (tensors, entry, metadata-or-None) for
+    write_sharded; after it returns the device state may change (async checkpointing)."""
     rank, world = get_rank(), get_world_size()
-    barrier()
-    if rank == 0:
-        ckpt_dir.mkdir(parents=True, exist_ok=True)
-    barrier()
     pieces = engine.ckpt_pieces()
     tensors, index = {}, []
     for j, (name, start, n, pview, sidx) in enumerate(pieces):
@@ -90,21 +106,38 @@ def save_sharded(ckpt_dir, engine):
         index.append([name, int(start), int(n)])
     tp_rank, tp_size = _tp_rank(engine)
     fname = f"__{rank}_0.distcp"
-    torch.save(tensors, ckpt_dir / fname)
     entry = {"file": fname, "rank": rank, "tp_rank": tp_rank, "index": index}
     if dist.is_initialized() and world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, entry)
     else:
         gathered = [entry]
+    meta = None
     if rank == 0:
-        shapes = {}
-        for n, p in engine.module.named_parameters():
-            shapes[n] = list(p.shape)
+        shapes = {n: list(p.shape) for n, p in engine.module.named_parameters()}
         meta = {"world_size": world, "tp_size": tp_size, "step": int(engine.step_count), "files": gathered,
                 "param_shapes_tp_local": shapes, "format": "dtg-sharded-v1"}
+    return tensors, entry, meta
+
+
+def write_sharded(ckpt_dir, tensors, entry, meta):
+    """Local file writes only (no collectives): safe on a background thread."""
+    ckpt_dir = Path(ckpt_dir)
+    ckpt_dir.mkdir(parents=True, exist_ok=True)
+    torch.save(tensors, ckpt_dir / entry["file"])
+    if meta is not None:
         with open(ckpt_dir / ".metadata", "w") as fp:
             json.dump(meta, fp)
+
+
+def save_sharded(ckpt_dir, engine):
+    """All ranks: write this rank's parameter + optimizer-state slices; rank 0 writes metadata."""
+    ckpt_dir = Path(ckpt_dir)
+    barrier()
+    if get_rank() == 0:
+        ckpt_dir.mkdir(parents=True, exist_ok=True)
+    barrier()
+    write_sharded(ckpt_dir, *snapshot_sharded(engine))
     barrier()
 
 
@@ -151,15 +184,100 @@ def load_sharded(ckpt_dir, engine, load_optimizer: bool = True):
 
 # ------------------------------------------------------------------------------ high level
 class CheckpointManager:
-    """Save/resume in the reference's layout. `style` in {"full", "dp", "sharded"}."""
+    """Save/resume in the reference's layout. `style` in {"full", "dp", "sharded"}.
 
-    def __init__(self, exp_dir, engine, optimizer, lr_scheduler, style: str, local_rank: int = 0):
+    `async_save=True`: `save()` only snapshots the state to host memory (device
+    -> host copies plus the small metadata collectives) and returns; a background thread
+    writes the files into `{exp_dir}/.pending/`.  The next `save()` or `finalize()` joins the
+    writer on every rank, meets at a barrier, and rank 0 moves the finished files into place and
+    writes `state.json` LAST -- resume keys on state.json, so an interrupted write is never
+    mistaken for a checkpoint."""
+
+    PENDING = ".pending"
+
+    def __init__(self, exp_dir, engine, optimizer, lr_scheduler, style: str, local_rank: int = 0,
+                 async_save: bool = False):
         self.exp_dir = Path(exp_dir)
         self.engine, self.optimizer, self.lr_scheduler = engine, optimizer, lr_scheduler
         self.style = style
         self.local_rank = local_rank
+        self.async_save = async_save
+        self._writer = None   # background thread of the pending save
+        self._pending = None  # (state, lr_scheduler state, rng state) to publish on finalize
+        self._error = None
+
+    # ------------------------------------------------------------------ async path
+    def _snapshot_host(self):
+        """Collective part of a save: everything the writer thread needs, on the host."""
+        jobs = []  # (relative path, object) for torch.save; sharded handled separately
+        shard = None
+        if self.style == "full":
+            if get_rank() == 0:
+                jobs.append(("model.pt", self.engine.full_state_dict()))
+                jobs.append(("optimizer.pt", _to_cpu(self.optimizer.state_dict())))
+        else:
+            if self.style == "dp":
+                sd = self.engine.full_state_dict()
+                if get_rank() == 0:
+                    jobs.append(("model.pt", sd))
+            shard = snapshot_sharded(self.engine)
+        return jobs, shard
+
+    def _write_pending(self, jobs, shard):
+        try:
+            pend = self.exp_dir / self.PENDING
+            pend.mkdir(parents=True, exist_ok=True)
+            for rel, obj in jobs:
+                torch.save(obj, pend / rel)
+            if shard is not None:
+                write_sharded(pend / "checkpoint", *shard)
+        except BaseException as e:  # surfaced by finalize() on the main thread
+            self._error = e
+
+    def finalize(self):
+        """Publish the pending async save (collective: call on every rank)."""
+        if self._writer is None:
+            return
+        self._writer.join()
+        self._writer = None
+        err, self._error = self._error, None
+        if err is not None:
+            raise RuntimeError("async checkpoint write failed") from err
+        barrier()
+        if get_rank() == 0:
+            import shutil
+
+            pend, d = self.exp_dir / self.PENDING, self.exp_dir
+            state, sched_sd, rng = self._pending
+            for item in pend.iterdir():
+                dst = d / item.name
+                if dst.is_dir():
+                    shutil.rmtree(dst)
+                os.replace(item, dst)
+            torch.save(sched_sd, d / "lr_scheduler.pt")
+            torch.save(rng, d / "rng.pt")
+            with open(d / "state.json", "w") as fp:
+                json.dump(state, fp)
+            shutil.rmtree(pend, ignore_errors=True)
+        self._pending = None
+        barrier()
 
     def save(self, state: dict):
+        if self.async_save:
+            import threading
+
+            self.finalize()
+            barrier()
+            jobs, shard = self._snapshot_host()
+            if get_rank() == 0:
+                box = _RngBox()
+                save_rng(box)
+                self._pending = (dict(state), _to_cpu(self.lr_scheduler.state_dict()), box.obj)
+            else:
+                self._pending = (None, None, None)
+            self._writer = threading.Thread(target=self._write_pending, args=(jobs, shard), daemon=False)
+            self._writer.start()
+            return
         rank = get_rank()
         d = self.exp_dir
         barrier()

@@ -77,6 +77,9 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     g.add_argument("--determinism", default="off", choices=["on", "off"])
     g.add_argument("--init-from", default=None, help="HF safetensors directory to load pretrained weights from")
     g.add_argument("--tunableop", default="use", choices=["off", "use", "tune"])
+    g.add_argument("--async-ckpt", default="off", choices=["on", "off"],
+                   help="snapshot checkpoints to host memory and write them on a background thread; published "
+                        "(state.json written last) at the next save or at the end of training")
     g.add_argument("--hip-graph", default="off", choices=["on", "off"],
                    help="single GPU: capture the whole step (fwd+bwd+AdamW) in a HIP graph and replay it "
                         "(launch-bound small models; dense fixed-shape batches)")

@@ -189,7 +189,8 @@ def run(chapter: str, argv=None):
     exp_dir = Path(args.save_dir) / args.experiment_name
     state = new_state()
     resumed = False
-    mgr = CheckpointManager(exp_dir, engine, opt, lr_scheduler, style, local_rank)
+    mgr = CheckpointManager(exp_dir, engine, opt, lr_scheduler, style, local_rank,
+                            async_save=getattr(args, "async_ckpt", "off") == "on")
     if has_checkpoint(exp_dir):
         LOGGER.info(f"Resuming from {exp_dir}")
         state = mgr.load()
@@ -317,8 +318,10 @@ def run(chapter: str, argv=None):
                 mgr.save(state)
             if args.max_steps and state["global_step"] >= args.max_steps:
                 LOGGER.info(f"Reached --max-steps {args.max_steps}")
+                mgr.finalize()
                 return state
         state["epoch_step"] = 0
+    mgr.finalize()
     return state
 
 

@@ -47,3 +47,47 @@ def test_fsdp_chapter_checkpoint_resume(tmp_path):
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "Resuming" in out, out[-3000:]
     assert json.loads((tmp_path / "fs" / "state.json").read_text())["global_step"] == 4
+
+
+@pytest.mark.slow
+def test_fsdp_async_checkpoint_resume(tmp_path):
+    """--async-ckpt: files are written on a background thread into .pending/ and published
+    (state.json last) at the next save / end of training; a resumed run continues from it."""
+    base = ["-e", "fa", "-d", "synthetic", "-m", "llama-tiny", "-s", "32", "--num-samples", "64",
+            "--save-dir", str(tmp_path), "--log-freq", "1", "--ckpt-freq", "2", "--num-workers", "0",
+            "--numel-to-wrap", "1000", "--async-ckpt", "on"]
+    r = _torchrun("04-fully-sharded-data-parallel", base + ["--max-steps", "4"])
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    d = tmp_path / "fa"
+    assert not (d / ".pending").exists()
+    assert json.loads((d / "state.json").read_text())["global_step"] == 4
+    assert (d / "checkpoint" / ".metadata").exists() and (d / "rng.pt").exists() and (d / "lr_scheduler.pt").exists()
+    r = _torchrun("04-fully-sharded-data-parallel", base + ["--max-steps", "6"])
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "Resuming" in out, out[-3000:]
+    assert json.loads((d / "state.json").read_text())["global_step"] == 6
+
+
+def test_async_pending_save_is_not_a_checkpoint(tmp_path):
+    """An async save that has not been finalized leaves no state.json behind."""
+    import torch
+
+    import dtg  # noqa: F401
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+    from dtg.train.checkpoint import CheckpointManager, has_checkpoint, new_state
+
+    m = build_model("llama-tiny", device="cpu", dtype=torch.float32)
+    eng = DataParallel(m, mode="single")
+    opt = FlatAdamW(eng, lr=1e-3)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10)
+    mgr = CheckpointManager(tmp_path, eng, opt, sched, "full", async_save=True)
+    st = new_state()
+    st["global_step"] = 3
+    mgr.save(st)
+    assert not has_checkpoint(tmp_path)
+    mgr.finalize()
+    assert has_checkpoint(tmp_path) and (tmp_path / "model.pt").exists() and not (tmp_path / ".pending").exists()
+    assert json.loads((tmp_path / "state.json").read_text())["global_step"] == 3
+    mgr2 = CheckpointManager(tmp_path, eng, opt, sched, "full")
+    assert mgr2.load()["global_step"] == 3
