@@ -16,6 +16,9 @@ def free_port():
 def _entry(rank, world, port, fn, args, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    # c10d's collective-consistency checks (every collective's op / shape / dtype is
+    # fingerprinted and compared across ranks) catch mismatched collectives in the engines.
+    os.environ.setdefault("TORCH_DISTRIBUTED_DEBUG", "DETAIL")
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
