@@ -70,6 +70,12 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     ] + [f"-I{i}" for i in incs] + [f"-I{CSRC}", f"-I{sysconfig.get_paths()['include']}"]
     hip_flags = common + [f"--offload-arch={ARCH}", "-fno-gpu-rdc", "-munsafe-fp-atomics"]
     cpu_flags = common + ["-march=x86-64-v3", "-fopenmp", "-x", "c++"]
+    # Per-file codegen options.  flash_attn.hip: MFMA results in ArchVGPRs.  Its backward kernels
+    # keep 128 f32 dK/dV (or dQ) accumulators live across the loop; in the default AGPR form the
+    # allocator placed the S / dP tiles in the same AGPRs and copied 32-64 accumulator registers
+    # out and back (v_accvgpr_read/write) every item -- 96-128 extra VALU per 32-96 MFMAs in
+    # the loop (ISA counted with llvm-objdump).  The VGPR form removes all of them, no spills.
+    per_file = {"flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) + glob.glob(os.path.join(CSRC, "comm", "*.hip")))
     cpu_srcs = sorted(glob.glob(os.path.join(CSRC, "cpu", "*.cpp")))
     hdr_t = _newest_header()
@@ -81,7 +87,8 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
         objs.append(obj)
         stale = force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t)
         if stale:
-            jobs_list.append(([hipcc] + flags + ["-c", src, "-o", obj], src, obj))
+            extra = per_file.get(os.path.basename(src), [])
+            jobs_list.append(([hipcc] + flags + extra + ["-c", src, "-o", obj], src, obj))
     jobs = jobs or min(8, os.cpu_count() or 4)
     if jobs_list:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
