@@ -17,9 +17,9 @@
 namespace dtg {
 
 // Tiles are TR (input rows = tokens) x TC (input columns) with 256 threads; each side moves
-// 16-byte vectors along its contiguous dimension.  The default 128 x 128 tile makes every
-// output row segment 256 B (64 x 64 writes only 128 B per row at a power-of-two stride of
-// 2*T bytes, which concentrates a launch's stores on few HBM channels).
+// 16-byte vectors along its contiguous dimension.  64 x 64 (default) and 128 x 128 tiles
+// (DTG_TRANSPOSE_TILE=128: 256-B output row segments) measured equal on the full 8B step
+// (same-box A/B, profiles/r1_s36_*); the wide [T, 2I] case alone favours 128 by ~3 %.
 template <int TR, int TC>
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ x, int64_t ldx,
                                                              uint16_t* __restrict__ out, int64_t R, int64_t C) {
@@ -67,7 +67,7 @@ at::Tensor transpose2d(const at::Tensor& x) {
   if (R == 0 || C == 0) return out;
   static const int tile = [] {
     const char* e = std::getenv("DTG_TRANSPOSE_TILE");
-    return e ? std::atoi(e) : 128;
+    return e ? std::atoi(e) : 64;
   }();
   if (tile == 64) {
     const dim3 grid((C + 63) / 64, (R + 63) / 64);
