@@ -58,12 +58,16 @@ def _compile(cmd, src, obj, verbose):
     return obj
 
 
-def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -> str:
+def build(jobs: int | None = None, force: bool = False, verbose: bool = False, out: str | None = None,
+          per_file_flags: bool = True) -> str:
+    """Compile + link; `out` / `per_file_flags=False` build an A/B variant (own object dir)."""
+    OUT_ = out or OUT
+    BUILD_ = BUILD if out is None else os.path.join(ROOT, "build", "obj_" + os.path.basename(out).replace(".so", ""))
     tdir, incs, abi = _torch_paths()
     hipcc = _hipcc()
     if hipcc is None:
         raise RuntimeError("hipcc not found (set ROCM_PATH)")
-    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(BUILD_, exist_ok=True)
     common = [
         "-O3", "-std=c++17", "-fPIC", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
         "-DTORCH_EXTENSION_NAME=_C", "-Wno-unused-result", "-Wno-deprecated-declarations",
@@ -75,7 +79,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     # allocator placed the S / dP tiles in the same AGPRs and copied 32-64 accumulator registers
     # out and back (v_accvgpr_read/write) every item -- 96-128 extra VALU per 32-96 MFMAs in
     # the loop (ISA counted with llvm-objdump).  The VGPR form removes all of them, no spills.
-    per_file = {"flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+    per_file = {"flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]} if per_file_flags else {}
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) + glob.glob(os.path.join(CSRC, "comm", "*.hip")))
     cpu_srcs = sorted(glob.glob(os.path.join(CSRC, "cpu", "*.cpp")))
     hdr_t = _newest_header()
@@ -83,7 +87,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     objs = []
     for src, flags in [(s, hip_flags) for s in srcs] + [(s, cpu_flags) for s in cpu_srcs]:
         rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
-        obj = os.path.join(BUILD, rel + ".o")
+        obj = os.path.join(BUILD_, rel + ".o")
         objs.append(obj)
         stale = force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t)
         if stale:
@@ -95,15 +99,15 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
             futs = [ex.submit(_compile, c, s, o, verbose) for c, s, o in jobs_list]
             for f in cf.as_completed(futs):
                 f.result()
-    need_link = force or bool(jobs_list) or not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(o) for o in objs)
+    need_link = force or bool(jobs_list) or not os.path.exists(OUT_) or os.path.getmtime(OUT_) < max(os.path.getmtime(o) for o in objs)
     if need_link:
         lib = os.path.join(tdir, "lib")
-        link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-fopenmp", "-o", OUT + ".tmp"] + objs + [
+        link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-fopenmp", "-o", OUT_ + ".tmp"] + objs + [
             f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{lib}",
         ]
-        _compile(link, "link", OUT, verbose)
-        os.replace(OUT + ".tmp", OUT)
-    return OUT
+        _compile(link, "link", OUT_, verbose)
+        os.replace(OUT_ + ".tmp", OUT_)
+    return OUT_
 
 
 if __name__ == "__main__":
@@ -111,6 +115,8 @@ if __name__ == "__main__":
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--out", default=None, help="A/B variant: link to this path (objects in build/obj_<name>)")
+    ap.add_argument("--no-per-file-flags", action="store_true")
     a = ap.parse_args()
-    print(build(a.j, a.force, a.verbose))
+    print(build(a.j, a.force, a.verbose, a.out, not a.no_per_file_flags))
     sys.exit(0)

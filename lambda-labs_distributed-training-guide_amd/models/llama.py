@@ -58,10 +58,11 @@ class TPInfo:
 class RunCtx:
     """Per-forward runtime data shared by all layers."""
 
-    __slots__ = ("cos", "sin", "pos", "cu_seqlens", "max_seqlen")
+    __slots__ = ("cos", "sin", "pos", "cu_seqlens", "max_seqlen", "cp_group", "rows")
 
-    def __init__(self, cos, sin, pos, cu_seqlens, max_seqlen):
+    def __init__(self, cos, sin, pos, cu_seqlens, max_seqlen, cp_group=None, rows=0):
         self.cos, self.sin, self.pos, self.cu_seqlens, self.max_seqlen = cos, sin, pos, cu_seqlens, max_seqlen
+        self.cp_group, self.rows = cp_group, rows
 
 
 class LlamaAttention(nn.Module):
@@ -78,7 +79,17 @@ class LlamaAttention(nn.Module):
 
     def forward(self, x, rc: RunCtx):
         qkv = ops.linear(x, self.qkv_proj.weight)
-        o = ops.attention(qkv, self.nq, self.nkv, self.d, rc.cu_seqlens, rc.max_seqlen, rc.cos, rc.sin, rc.pos)
+        if rc.cp_group is not None:  # context parallel: zig-zag sequence shards
+            from ..parallel.context_parallel import cp_attention
+
+            T, d = qkv.shape[0], self.d
+            qkv = ops.rope(qkv, rc.cos, rc.sin, rc.pos, self.nq + self.nkv, d)
+            q = qkv[:, :self.nq * d].reshape(T, self.nq, d)
+            k = qkv[:, self.nq * d:(self.nq + self.nkv) * d].reshape(T, self.nkv, d)
+            v = qkv[:, (self.nq + self.nkv) * d:].reshape(T, self.nkv, d)
+            o = cp_attention(q, k, v, rc.cp_group, rc.rows).reshape(T, self.nq * d)
+        else:
+            o = ops.attention(qkv, self.nq, self.nkv, self.d, rc.cu_seqlens, rc.max_seqlen, rc.cos, rc.sin, rc.pos)
         return ops.linear(o, self.o_proj.weight)
 
 
@@ -150,10 +161,14 @@ class _VocabParallelEmbedding(torch.autograd.Function):
 
 
 class LlamaForCausalLM(nn.Module):
-    def __init__(self, cfg: LlamaConfig, tp_group=None, device=None, dtype=torch.bfloat16):
+    def __init__(self, cfg: LlamaConfig, tp_group=None, device=None, dtype=torch.bfloat16, cp_group=None):
         super().__init__()
         self.config = cfg
         self.tp = TPInfo(tp_group)
+        # context parallel (parallel/context_parallel.py): inputs are zig-zag sequence shards with
+        # global position_ids and labels already shifted on the full sequence (cp_batch)
+        self.cp_group = cp_group
+        assert cp_group is None or tp_group is None, "context parallel and tensor parallel are not combined"
         tp = self.tp
         assert cfg.vocab_size % tp.size == 0 or not tp.enabled, "vocab must divide by the TP degree"
         self.vocab_local = cfg.vocab_size // tp.size
@@ -216,7 +231,9 @@ class LlamaForCausalLM(nn.Module):
         T = B * S
         dev = input_ids.device
         ids = input_ids.reshape(-1)
-        if position_ids is None:
+        if self.cp_group is not None:  # attention is block-wise over zig-zag chunks: no cu_seqlens
+            pos, cu, max_seqlen = position_ids.reshape(-1).to(torch.long), None, 0
+        elif position_ids is None:
             pos, cu = self._dense_meta(B, S, dev)
             max_seqlen = S
         else:
@@ -231,8 +248,13 @@ class LlamaForCausalLM(nn.Module):
                 cu = cu_seqlens.to(device=dev, dtype=torch.int32)
                 if max_seqlen is None:
                     max_seqlen = int((cu[1:] - cu[:-1]).max().item())
-        cos, sin = self._rope_tables(S, dev)
-        rc = RunCtx(cos, sin, pos, cu, int(max_seqlen))
+        cp = self.cp_group is not None
+        if cp:
+            assert position_ids is not None, "context parallel needs the global position_ids (cp_batch)"
+            cos, sin = self._rope_tables(int(position_ids.max()) + 1, dev)
+        else:
+            cos, sin = self._rope_tables(S, dev)
+        rc = RunCtx(cos, sin, pos, cu, int(max_seqlen), self.cp_group if cp else None, B)
         tp = self.tp
         if tp.enabled:
             x = _VocabParallelEmbedding.apply(ids, self.embed_tokens.weight, self.vocab_start)
@@ -248,9 +270,12 @@ class LlamaForCausalLM(nn.Module):
         out = CausalLMOutput()
         w = self.lm_head_weight()
         if labels is not None:
-            shifted = torch.full_like(labels, -100)
-            shifted[:, :-1] = labels[:, 1:]
-            shifted = shifted.reshape(-1)
+            if cp:  # shifted on the full sequence before sharding
+                shifted = labels.reshape(-1)
+            else:
+                shifted = torch.full_like(labels, -100)
+                shifted[:, :-1] = labels[:, 1:]
+                shifted = shifted.reshape(-1)
             if num_valid is None:
                 num_valid = int((shifted != -100).sum().item())
             if tp.enabled:

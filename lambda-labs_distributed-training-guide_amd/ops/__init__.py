@@ -22,6 +22,7 @@ from .functional import (  # noqa: E402
     fused_linear_cross_entropy,
     linear,
     rms_norm,
+    rope,
     rope_tables,
     swiglu,
     swiglu_mlp,
@@ -31,6 +32,6 @@ from .grad_routing import route_param_grad  # noqa: E402
 from .adamw import adamw_step  # noqa: E402
 
 __all__ = [
-    "add_rms_norm", "attention", "embedding", "fused_linear_cross_entropy", "linear", "rms_norm",
+    "add_rms_norm", "attention", "rope", "embedding", "fused_linear_cross_entropy", "linear", "rms_norm",
     "rope_tables", "swiglu", "swiglu_mlp", "vocab_parallel_fused_linear_cross_entropy", "route_param_grad", "adamw_step",
 ]

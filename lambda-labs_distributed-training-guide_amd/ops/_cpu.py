@@ -161,12 +161,39 @@ def flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal):
 
 
 def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal):
-    with torch.enable_grad():
-        qf = q.detach().float().requires_grad_()
-        kf = k.detach().float().requires_grad_()
-        vf = v.detach().float().requires_grad_()
-        of, _ = _attn_ref(qf, kf, vf, cu_seqlens, scale, causal)
-        dq, dk, dv = torch.autograd.grad(of, (qf, kf, vf), dout.float())
+    """The kernel's semantics: P = exp(S*scale - lse) with the GIVEN lse, delta = rowsum(dO*O)
+    with the GIVEN o (so a block of a larger softmax -- context parallelism -- gets the
+    gradient of the full softmax)."""
+    T, hq, d = q.shape
+    hkv = k.shape[1]
+    rep = hq // hkv
+    dq = torch.zeros(T, hq, d, dtype=torch.float32)
+    dk = torch.zeros(T, hkv, d, dtype=torch.float32)
+    dv = torch.zeros(T, hkv, d, dtype=torch.float32)
+    cu = cu_seqlens.tolist()
+    for i in range(len(cu) - 1):
+        a, b = cu[i], cu[i + 1]
+        if b <= a:
+            continue
+        qs = q[a:b].float().transpose(0, 1)                               # [hq, s, d]
+        ks = k[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        vs = v[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        dos = dout[a:b].float().transpose(0, 1)
+        os_ = o[a:b].float().transpose(0, 1)
+        sc = qs @ ks.transpose(1, 2) * scale
+        if causal:
+            n = b - a
+            sc = sc.masked_fill(torch.ones(n, n, dtype=torch.bool).triu(1), float("-inf"))
+        p = torch.exp(sc - lse[:, a:b].float()[..., None])
+        dvh = p.transpose(1, 2) @ dos
+        dp = dos @ vs.transpose(1, 2)
+        delta = (dos * os_).sum(-1, keepdim=True)
+        ds = p * (dp - delta)
+        dqh = ds @ ks * scale
+        dkh = ds.transpose(1, 2) @ qs * scale
+        dq[a:b] = dqh.transpose(0, 1)
+        dk[a:b] = dkh.view(hkv, rep, b - a, d).sum(1).transpose(0, 1)
+        dv[a:b] = dvh.view(hkv, rep, b - a, d).sum(1).transpose(0, 1)
     return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
 
 

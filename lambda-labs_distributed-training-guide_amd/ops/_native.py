@@ -9,7 +9,8 @@ import os
 import torch
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO_PATH = os.path.join(_PKG, "_C.so")
+# DTG_NATIVE_SO: load an A/B build variant instead (csrc/build.py --out ...)
+SO_PATH = os.environ.get("DTG_NATIVE_SO") or os.path.join(_PKG, "_C.so")
 LOADED = False
 LOAD_ERROR = None
 

@@ -200,6 +200,29 @@ class _AttentionQKV(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
+class _Rope(torch.autograd.Function):
+    """Out-of-place RoPE on the q and k heads of a fused QKV activation (v untouched)."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, pos, nheads, head_dim):
+        y = qkv.contiguous().clone()
+        ops.rope_(y, cos, sin, pos, nheads, head_dim, False)
+        ctx.save_for_backward(cos, sin, pos)
+        ctx.meta = (nheads, head_dim)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin, pos = ctx.saved_tensors
+        dx = dy.contiguous().clone()
+        ops.rope_(dx, cos, sin, pos, ctx.meta[0], ctx.meta[1], True)
+        return dx, None, None, None, None, None
+
+
+def rope(qkv, cos, sin, pos, nheads, head_dim):
+    return _Rope.apply(qkv, cos, sin, pos, int(nheads), int(head_dim))
+
+
 def attention(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos=None, sin=None, pos=None, causal=True, scale=None):
     """Causal (varlen) GQA attention on a fused [T, (nq+2nkv)*d] QKV activation -> [T, nq*d].
 

@@ -41,7 +41,7 @@ class DataParallel:
     def __init__(self, model: nn.Module, mode: str = "ddp", group=None, tp_group=None,
                  bucket_mb: int = 256, broadcast_from_rank0: bool = True, state_dtype=torch.bfloat16,
                  master_weights: bool = False, overlap_param_gather: bool = True,
-                 overlap_optimizer: bool = False):
+                 overlap_optimizer: bool = False, grad_divisor: Optional[int] = None):
         assert mode in ("single", "ddp", "zero")
         self.module = model
         self.group = group
@@ -95,6 +95,10 @@ class DataParallel:
         # device [lr, 1-beta1^t, sqrt(1-beta2^t)] read by AdamW instead of host scalars while a
         # HIP graph of the step is captured / replayed (dtg.train.graph.GraphedStep)
         self.graph_hyper = None
+        # gradients are averaged over `grad_divisor` ranks (default: the whole group).  Context
+        # parallelism uses the CP degree's complement: each CP rank's loss is already a share of
+        # the global mean, so its gradients are summed over CP and averaged over data parallel.
+        self.grad_divisor = grad_divisor or self.world
         # The engine owns the loss: backward(loss) uses an implicit gradient of 1 and any
         # scaling goes into AdamW's grad_scale, which lets the loss head write dW in place.
         set_direct_loss_grad(True)
@@ -144,7 +148,7 @@ class DataParallel:
             self.step_count += 1
         if self.mode == "zero":
             self.wait_param_gather([b.index])  # last step's gather of this bucket (normally long done)
-        scale = 1.0 / (self.world * (self.accum_count + 1))  # this backward is micro-batch accum_count+1
+        scale = 1.0 / (self.grad_divisor * (self.accum_count + 1))  # this backward is micro-batch accum_count+1
         st = self._opt_stream
         if st is not None:
             st.wait_stream(torch.cuda.current_stream())  # this bucket's gradients are written
@@ -217,7 +221,7 @@ class DataParallel:
             return
         self.step_count += 1
         if grad_scale is None:
-            grad_scale = 1.0 / (self.world * max(1, self.accum_count))
+            grad_scale = 1.0 / (self.grad_divisor * max(1, self.accum_count))
         if self.mode == "zero":
             self.wait_param_gather()  # never update a slice an all-gather may still be reading
             for (s, e), o in zip(self.shard_ranges, self.shard_offsets):
