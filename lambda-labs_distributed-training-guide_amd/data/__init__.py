@@ -1,6 +1,8 @@
 """Data pipeline: datasets, packed collation, distributed loaders."""
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.utils.data import DataLoader, DistributedSampler
 
@@ -82,8 +84,12 @@ def build_dataloader(dataset, batch_size: int, collate_fn, *, dp_size: int = 1, 
     kw = {}
     if num_workers > 0:
         kw = dict(prefetch_factor=prefetch_factor, worker_init_fn=seed_worker, persistent_workers=False)
+        ctx = os.environ.get("DTG_LOADER_CTX")
+        if ctx:
+            kw["multiprocessing_context"] = ctx
+    pin = pin_memory and torch.cuda.is_available() and os.environ.get("DTG_LOADER_PIN", "1") == "1"
     return DataLoader(dataset, batch_size=batch_size, sampler=sampler, drop_last=drop_last, collate_fn=collate_fn,
-                      num_workers=num_workers, generator=g, pin_memory=pin_memory and torch.cuda.is_available(), **kw)
+                      num_workers=num_workers, generator=g, pin_memory=pin, **kw)
 
 
 __all__ = ["ResumableSampler", "PackedCollator", "dense_collate", "packed_position_ids", "SyntheticPacked", "SyntheticTokens",
