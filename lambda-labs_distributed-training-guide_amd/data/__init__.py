@@ -83,8 +83,12 @@ def build_dataloader(dataset, batch_size: int, collate_fn, *, dp_size: int = 1, 
     g.manual_seed(seed)
     kw = {}
     if num_workers > 0:
-        kw = dict(prefetch_factor=prefetch_factor, worker_init_fn=seed_worker, persistent_workers=False)
-        ctx = os.environ.get("DTG_LOADER_CTX")
+        # GPU runs start workers with "spawn": forking a process that holds a HIP context and
+        # tens of GB of pinned host memory (FSDP CPU offload) stalled the parent's first device
+        # synchronize indefinitely on MI355X boxes (chapter 05 with --num-workers 2; fine with
+        # spawn or 0 workers).  Persistent workers pay the interpreter start-up once per run.
+        ctx = os.environ.get("DTG_LOADER_CTX") or ("spawn" if torch.cuda.is_available() else None)
+        kw = dict(prefetch_factor=prefetch_factor, worker_init_fn=seed_worker, persistent_workers=ctx == "spawn")
         if ctx:
             kw["multiprocessing_context"] = ctx
     pin = pin_memory and torch.cuda.is_available() and os.environ.get("DTG_LOADER_PIN", "1") == "1"
