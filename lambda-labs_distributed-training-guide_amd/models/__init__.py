@@ -6,14 +6,15 @@ from .gpt2 import GPT2LMHeadModel
 from .llama import CausalLMOutput, LlamaForCausalLM, count_valid_labels
 
 
-def build_model(name_or_cfg, device=None, dtype=torch.bfloat16, tp_group=None, init=True, cp_group=None, **overrides):
+def build_model(name_or_cfg, device=None, dtype=torch.bfloat16, tp_group=None, init=True, cp_group=None, sp_group=None,
+                **overrides):
     """Random-init causal LM from a bundled/HF name or a config object (D1: pure bf16 weights)."""
     cfg = resolve_config(name_or_cfg, **overrides) if isinstance(name_or_cfg, str) else name_or_cfg
     if isinstance(cfg, GPT2Config):
-        assert tp_group is None, "GPT-2 is the single-GPU/DDP plumbing model; TP is Llama-only"
+        assert tp_group is None and cp_group is None and sp_group is None, "GPT-2 is the single-GPU/DDP plumbing model; TP is Llama-only"
         m = GPT2LMHeadModel(cfg, device=device, dtype=dtype)
     else:
-        m = LlamaForCausalLM(cfg, tp_group=tp_group, device=device, dtype=dtype, cp_group=cp_group)
+        m = LlamaForCausalLM(cfg, tp_group=tp_group, device=device, dtype=dtype, cp_group=cp_group, sp_group=sp_group)
     if init:
         m.init_weights()
     return m

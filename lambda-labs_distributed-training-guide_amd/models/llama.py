@@ -58,11 +58,11 @@ class TPInfo:
 class RunCtx:
     """Per-forward runtime data shared by all layers."""
 
-    __slots__ = ("cos", "sin", "pos", "cu_seqlens", "max_seqlen", "cp_group", "rows")
+    __slots__ = ("cos", "sin", "pos", "cu_seqlens", "max_seqlen", "cp_group", "rows", "sp_group")
 
-    def __init__(self, cos, sin, pos, cu_seqlens, max_seqlen, cp_group=None, rows=0):
+    def __init__(self, cos, sin, pos, cu_seqlens, max_seqlen, cp_group=None, rows=0, sp_group=None):
         self.cos, self.sin, self.pos, self.cu_seqlens, self.max_seqlen = cos, sin, pos, cu_seqlens, max_seqlen
-        self.cp_group, self.rows = cp_group, rows
+        self.cp_group, self.rows, self.sp_group = cp_group, rows, sp_group
 
 
 class LlamaAttention(nn.Module):
@@ -88,6 +88,11 @@ class LlamaAttention(nn.Module):
             k = qkv[:, self.nq * d:(self.nq + self.nkv) * d].reshape(T, self.nkv, d)
             v = qkv[:, (self.nq + self.nkv) * d:].reshape(T, self.nkv, d)
             o = cp_attention(q, k, v, rc.cp_group, rc.rows).reshape(T, self.nq * d)
+        elif rc.sp_group is not None:  # Ulysses: all-to-all to full sequences x local heads
+            from ..parallel.ulysses import ulysses_attention
+
+            o = ulysses_attention(qkv, self.nq, self.nkv, self.d, rc.sp_group, rc.rows, rc.cu_seqlens,
+                                  rc.max_seqlen, rc.cos, rc.sin, rc.pos)
         else:
             o = ops.attention(qkv, self.nq, self.nkv, self.d, rc.cu_seqlens, rc.max_seqlen, rc.cos, rc.sin, rc.pos)
         return ops.linear(o, self.o_proj.weight)
@@ -161,14 +166,19 @@ class _VocabParallelEmbedding(torch.autograd.Function):
 
 
 class LlamaForCausalLM(nn.Module):
-    def __init__(self, cfg: LlamaConfig, tp_group=None, device=None, dtype=torch.bfloat16, cp_group=None):
+    def __init__(self, cfg: LlamaConfig, tp_group=None, device=None, dtype=torch.bfloat16, cp_group=None,
+                 sp_group=None):
         super().__init__()
         self.config = cfg
         self.tp = TPInfo(tp_group)
         # context parallel (parallel/context_parallel.py): inputs are zig-zag sequence shards with
         # global position_ids and labels already shifted on the full sequence (cp_batch)
         self.cp_group = cp_group
-        assert cp_group is None or tp_group is None, "context parallel and tensor parallel are not combined"
+        # Ulysses sequence parallel (parallel/ulysses.py): inputs are contiguous sequence slices,
+        # labels shifted on the full rows (ulysses_batch), position_ids (packed rows) local slices
+        self.sp_group = sp_group
+        assert sum(g is not None for g in (cp_group, tp_group, sp_group)) <= 1, \
+            "context, Ulysses and tensor parallelism are not combined"
         tp = self.tp
         assert cfg.vocab_size % tp.size == 0 or not tp.enabled, "vocab must divide by the TP degree"
         self.vocab_local = cfg.vocab_size // tp.size
@@ -227,10 +237,32 @@ class LlamaForCausalLM(nn.Module):
         Packed sequences: pass position_ids (restarting at 0 per document) and ideally
         cu_seqlens (int32 [ndocs+1]) + max_seqlen from the collator (else derived, 1 sync).
         `num_valid` (host int) = number of non-ignored shifted labels (avoids a sync)."""
+        rc = self.run_context(input_ids, position_ids, cu_seqlens, max_seqlen)
+        x, res = self.embed(input_ids), None
+        for layer in self.layers:
+            x, res = layer(x, res, rc)
+        return self.head(x, res, labels, num_valid, return_logits, input_ids.shape[0])
+
+    # The three pieces of forward, also driven one by one by the pipeline-parallel stages
+    # (parallel/pipeline.py): run_context -> embed -> layers -> head.
+    def run_context(self, input_ids, position_ids=None, cu_seqlens=None, max_seqlen=None) -> RunCtx:
+        """Per-forward attention metadata (positions, varlen boundaries, RoPE tables)."""
         B, S = input_ids.shape
         T = B * S
         dev = input_ids.device
-        ids = input_ids.reshape(-1)
+        sp = self.sp_group is not None
+        if sp:  # attention sees the full rows: describe them (positions gathered from the slices)
+            from ..parallel.ulysses import sp_world
+
+            n = sp_world(self.sp_group)
+            if position_ids is not None:
+                from ..utils import comm
+
+                loc = position_ids.to(device=dev, dtype=torch.long).contiguous()
+                position_ids = comm.all_gather_dim0(loc.t().contiguous(), self.sp_group).t()  # [B, n*S]
+                cu_seqlens = None
+            S = S * n
+            T = B * S
         if self.cp_group is not None:  # attention is block-wise over zig-zag chunks: no cu_seqlens
             pos, cu, max_seqlen = position_ids.reshape(-1).to(torch.long), None, 0
         elif position_ids is None:
@@ -254,23 +286,28 @@ class LlamaForCausalLM(nn.Module):
             cos, sin = self._rope_tables(int(position_ids.max()) + 1, dev)
         else:
             cos, sin = self._rope_tables(S, dev)
-        rc = RunCtx(cos, sin, pos, cu, int(max_seqlen), self.cp_group if cp else None, B)
+        return RunCtx(cos, sin, pos, cu, int(max_seqlen), self.cp_group if cp else None, B,
+                      self.sp_group if sp else None)
+
+    def embed(self, input_ids):
+        ids = input_ids.reshape(-1)
         tp = self.tp
         if tp.enabled:
             x = _VocabParallelEmbedding.apply(ids, self.embed_tokens.weight, self.vocab_start)
-            x = tp_comm.scatter_seq(x, tp.group)
-        else:
-            x = ops.embedding(ids, self.embed_tokens.weight)
-        res = None
-        for layer in self.layers:
-            x, res = layer(x, res, rc)
+            return tp_comm.scatter_seq(x, tp.group)
+        return ops.embedding(ids, self.embed_tokens.weight)
+
+    def head(self, x, res, labels=None, num_valid=None, return_logits=False, batch_rows=1):
+        """Final norm (with the last residual add) and the fused loss head / logits."""
+        tp = self.tp
         h, _ = ops.add_rms_norm(x, res, self.norm.weight, self.config.rms_norm_eps)
         if tp.enabled:
             h = tp_comm.gather_seq(h, tp.group)
         out = CausalLMOutput()
         w = self.lm_head_weight()
         if labels is not None:
-            if cp:  # shifted on the full sequence before sharding
+            cp, sp = self.cp_group is not None, self.sp_group is not None
+            if cp or sp:  # shifted on the full sequence before sharding
                 shifted = labels.reshape(-1)
             else:
                 shifted = torch.full_like(labels, -100)
@@ -278,6 +315,12 @@ class LlamaForCausalLM(nn.Module):
                 shifted = shifted.reshape(-1)
             if num_valid is None:
                 num_valid = int((shifted != -100).sum().item())
+                if cp or sp:  # the loss is a share of the mean over the full rows
+                    import torch.distributed as dist
+
+                    t = torch.tensor([num_valid], device=h.device)
+                    dist.all_reduce(t, group=self.cp_group if cp else self.sp_group)
+                    num_valid = int(t.item())
             if tp.enabled:
                 out.loss = ops.vocab_parallel_fused_linear_cross_entropy(
                     h, w, shifted, self.vocab_start, tp.group, num_valid=num_valid)
@@ -287,7 +330,7 @@ class LlamaForCausalLM(nn.Module):
             logits = ops.linear(h, w)
             if tp.enabled:
                 logits = tp_comm.gather_seq(logits.t().contiguous(), tp.group).t()
-            out.logits = logits.view(B, S, -1)
+            out.logits = logits.view(batch_rows, -1, logits.shape[-1])
         return out
 
 

@@ -56,7 +56,7 @@ def unshard_zigzag(shards: List[torch.Tensor], cp: int) -> torch.Tensor:
     return torch.cat(chunks, dim=1)
 
 
-def cp_batch(input_ids: torch.Tensor, rank: int, cp: int, ignore_index: int = -100):
+def cp_batch(input_ids: torch.Tensor, rank: int, cp: int, ignore_index: int = -100, labels=None):
     """Shard a full [B, S] batch for context parallelism.
 
     Returns (ids, shifted_labels, position_ids, num_valid_total): labels are shifted on the
@@ -64,7 +64,7 @@ def cp_batch(input_ids: torch.Tensor, rank: int, cp: int, ignore_index: int = -1
     positions are the global ones (RoPE), and num_valid_total is the global label count."""
     B, S = input_ids.shape
     shifted = torch.full_like(input_ids, ignore_index)
-    shifted[:, :-1] = input_ids[:, 1:]
+    shifted[:, :-1] = (input_ids if labels is None else labels)[:, 1:]
     pos = torch.arange(S, device=input_ids.device).expand(B, S)
     n_valid = int((shifted != ignore_index).sum())
     return (shard_zigzag(input_ids, rank, cp), shard_zigzag(shifted, rank, cp), shard_zigzag(pos, rank, cp), n_valid)

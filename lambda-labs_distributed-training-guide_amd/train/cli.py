@@ -61,6 +61,12 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                    help="record N steps (after the first 3) with torch.profiler; chrome trace in the exp dir")
     g.add_argument("--sync-timers", default="on", choices=["on", "off"],
                    help="on: reference LocalTimer (device sync around every phase); off: HIP-event timers")
+    if chapter in ("rime", "01", "02"):
+        g.add_argument("--sp", default=1, type=int,
+                       help="Ulysses sequence parallel degree: each row is split over this many ranks, "
+                            "all-to-all seq<->heads around attention (packed rows supported)")
+        g.add_argument("--cp", default=1, type=int,
+                       help="context parallel degree: zig-zag row shards, all-gathered K/V (dense rows)")
     g.add_argument("--grad-accum", default=1, type=int, help="micro-batches per optimizer step (no_sync)")
     g.add_argument("--bucket-mb", default=256, type=int, help="gradient bucket size for DDP/ZeRO")
     if chapter == "02":

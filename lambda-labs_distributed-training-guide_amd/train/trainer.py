@@ -100,6 +100,15 @@ def _build(args, chapter, device, world):
 
             _comm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=args.tp_comm_mb << 20, device=device))
             LOGGER.info(f"tp collectives: direct-peer xGMI ({args.tp_comm_mb} MiB workspace per rank)")
+    seq = None  # (kind, group, rank, degree): Ulysses / context parallel over each row
+    nseq = max(getattr(args, "sp", 1), getattr(args, "cp", 1))
+    if nseq > 1:
+        assert min(getattr(args, "sp", 1), getattr(args, "cp", 1)) == 1, "--sp and --cp are alternatives"
+        from ..parallel.tensor_parallel import make_mesh
+
+        dp_group, seq_group, dp_rank, seq_rank, dp_size = make_mesh(nseq)
+        seq = ("sp" if args.sp > 1 else "cp", seq_group, seq_rank, nseq)
+        LOGGER.info(f"mesh: dp={dp_size} x {seq[0]}={nseq} (dp_rank={dp_rank}, {seq[0]}_rank={seq_rank})")
     replicate_group = None
     if getattr(args, "sharding", "full") == "hybrid" and world > 1:
         from ..parallel.tensor_parallel import make_mesh
@@ -113,8 +122,11 @@ def _build(args, chapter, device, world):
     if fsdp:
         with torch.device("meta"):
             model = build_model(cfg, tp_group=tp_group, init=False)
+    elif seq is not None:
+        model = build_model(cfg, device=device, **{f"{seq[0]}_group": seq[1]})
     else:
         model = build_model(cfg, device=device, tp_group=tp_group)
+    model._dtg_seq = seq
     if args.activation_checkpointing == "on":
         apply_activation_checkpointing(model)
     LOGGER.info(f"{sum(p.numel() for p in model.parameters()) / 1e9:.3f}B parameters (this rank's shard of TP)")
@@ -130,7 +142,11 @@ def _build(args, chapter, device, world):
                             replicate_group=replicate_group)
         style = "sharded"
     else:
-        if chapter in ("01", "rime") or world == 1:
+        if world == 1:
+            mode = "single"
+        elif seq is not None:  # parameters replicated on every rank; the row's loss is split over seq ranks
+            mode = args.dp_mode if chapter == "02" else "ddp"
+        elif chapter in ("01", "rime"):
             mode = "single"
         elif chapter == "02":
             mode = args.dp_mode
@@ -138,8 +154,9 @@ def _build(args, chapter, device, world):
             mode = "ddp" if args.zero_stage == 0 else "zero"
         else:  # 06: data parallel across TP groups
             mode = "ddp"
-        engine = DataParallel(model, mode=mode, group=dp_group, tp_group=tp_group, bucket_mb=args.bucket_mb,
-                              broadcast_from_rank0=tp_group is None)
+        engine = DataParallel(model, mode=mode, group=None if seq is not None else dp_group, tp_group=tp_group,
+                              bucket_mb=args.bucket_mb, broadcast_from_rank0=tp_group is None,
+                              grad_divisor=dp_size if seq is not None else None)
         style = "full" if mode == "single" and chapter in ("01", "rime") else ("dp" if chapter == "02" else "sharded")
     LOGGER.info(f"After engine ({engine.mode}): {get_mem_stats(device)}")
     if args.init_from:
@@ -219,6 +236,7 @@ def run(chapter: str, argv=None):
     mem_suffix = "_in_gb" if chapter in ("05", "deepspeed") else "_gb"
     fault_rng = random.Random(args.seed * 1000 + rank + 7 * state["global_step"])
     accum = max(1, args.grad_accum)
+    seq_shard = _seq_sharder(model._dtg_seq)
     model.train()
     graphed = None
     if getattr(args, "hip_graph", "off") == "on":
@@ -250,6 +268,8 @@ def run(chapter: str, argv=None):
                     mx = b.pop("max_seqlen", None)
                     b = {k: v.to(device=device, non_blocking=True) for k, v in b.items()}
                     b["num_valid"] = nv
+                    if seq_shard is not None:
+                        b = seq_shard(b)
                     if mx is not None:
                         b["max_seqlen"] = mx
                     micro.append(b)
@@ -282,6 +302,9 @@ def run(chapter: str, argv=None):
                 with timers["update"]:
                     opt.step()
                     lr_scheduler.step()
+            if seq_shard is not None:  # each sequence rank holds its share of the row losses
+                loss_sum = loss_sum.clone()
+                torch.distributed.all_reduce(loss_sum, group=model._dtg_seq[1])
             state["global_step"] += 1
             state["epoch_step"] += 1
             if args.torch_profile_steps > 0:
@@ -323,6 +346,31 @@ def run(chapter: str, argv=None):
         state["epoch_step"] = 0
     mgr.finalize()
     return state
+
+
+def _seq_sharder(seq):
+    """Batch transform for --sp / --cp: this rank's slice of every row, labels shifted on the full
+    rows, the global label count."""
+    if seq is None:
+        return None
+    kind, _, r, n = seq
+
+    def shard(b):
+        if kind == "sp":
+            from ..parallel.ulysses import ulysses_batch
+
+            ids, lab, pos, nv = ulysses_batch(b["input_ids"], r, n, b.get("position_ids"), labels=b.get("labels"))
+        else:
+            assert "position_ids" not in b, "--cp takes dense rows (use --sp for packed sequences)"
+            from ..parallel.context_parallel import cp_batch
+
+            ids, lab, pos, nv = cp_batch(b["input_ids"], r, n, labels=b.get("labels"))
+        out = {"input_ids": ids, "labels": lab, "num_valid": nv}
+        if pos is not None:
+            out["position_ids"] = pos
+        return out
+
+    return shard
 
 
 def _profile_tick(prof, step, start, stop, exp_dir, rank, device):

@@ -86,6 +86,27 @@ def reduce_scatter_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
     return out
 
 
+def all_to_all_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
+    """x [n * c, ...]: chunk j goes to rank j; returns [n * c, ...] whose chunk i came from rank i.
+
+    RCCL runs it as one all-to-all (every pair of MI355X GPUs in a node has its own xGMI link,
+    so the n-1 peer transfers proceed in parallel).  gloo with device tensors (the 1-GPU test
+    rehearsals) is emulated by an all-gather and a local pick."""
+    n = world(group)
+    if n == 1:
+        return x
+    assert x.shape[0] % n == 0, f"dim 0 ({x.shape[0]}) must divide by group size {n}"
+    x = x.contiguous()
+    if backend_of(group) == "gloo" and x.is_cuda:
+        c = x.shape[0] // n
+        r = rank(group)
+        full = all_gather_dim0(x, group).view(n, n, c, *x.shape[1:])  # [src, dst, c, ...]
+        return full[:, r].reshape(x.shape).contiguous()
+    out = torch.empty_like(x)
+    dist.all_to_all_single(out, x, group=group)
+    return out
+
+
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group=None, async_op=False):
     """Flat all-gather: out.numel() == shard.numel() * world."""
     return dist.all_gather_into_tensor(out, shard, group=group, async_op=async_op)

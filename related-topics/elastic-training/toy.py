@@ -9,6 +9,7 @@ restart, so a restarted job does not replay the same failure.
     torchrun --nnodes 1 --nproc-per-node 4 --max-restarts 3 toy.py
 """
 import argparse
+import datetime
 import json
 import os
 import random
@@ -26,8 +27,11 @@ def main():
     ap.add_argument("--state", default="./toy-state.json")
     ap.add_argument("--sleep", type=float, default=0.0)
     ap.add_argument("--fail-at-step", type=int, default=-1, help="deterministic failure of rank 1 on the first attempt")
+    ap.add_argument("--pg-timeout", type=float, default=60.0, help="process-group timeout (s)")
     a = ap.parse_args()
-    dist.init_process_group("gloo")
+    # a bounded rendezvous/connect: a worker whose mesh connect fails must exit (and let torchrun
+    # restart the group) instead of waiting out the 30-minute default
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=a.pg_timeout))
     rank, world = dist.get_rank(), dist.get_world_size()
     state = {"num_steps": 0}
     if os.path.exists(a.state):

@@ -22,7 +22,7 @@ def test_toy_restarts_and_resumes(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--max-restarts", "4", "--rdzv-backend", "c10d", "--rdzv-endpoint", f"127.0.0.1:{free_port()}",
            os.path.join(ROOT, "related-topics", "elastic-training", "toy.py"), "--steps", "40", "--fail-prob", "0",
-           "--fail-at-step", "15", "--state", str(state)]
+           "--fail-at-step", "15", "--state", str(state), "--pg-timeout", "20"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]

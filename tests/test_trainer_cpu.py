@@ -91,3 +91,24 @@ def test_async_pending_save_is_not_a_checkpoint(tmp_path):
     assert json.loads((tmp_path / "state.json").read_text())["global_step"] == 3
     mgr2 = CheckpointManager(tmp_path, eng, opt, sched, "full")
     assert mgr2.load()["global_step"] == 3
+
+
+def _losses(path):
+    return [json.loads(line)["running_loss"] for line in path.read_text().splitlines()]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("flag,dataset", [("--sp", "synthetic:packed"), ("--cp", "synthetic")])
+def test_sequence_parallel_chapter_matches_single_process(tmp_path, flag, dataset):
+    """rime chapter with each row split over 2 ranks (Ulysses on packed rows, context parallel on
+    dense rows) logs the same losses as one process reading the same batches."""
+    base = ["-d", dataset, "-m", "llama-tiny-d128", "-s", "64", "--num-samples", "16", "--log-freq", "1",
+            "--ckpt-freq", "100", "--num-workers", "0", "--max-steps", "3", "--lr", "1e-3"]
+    one = _torchrun("00-rime", ["-e", "one", "--save-dir", str(tmp_path)] + base, nproc=1)
+    assert one.returncode == 0, (one.stdout + one.stderr)[-3000:]
+    two = _torchrun("00-rime", ["-e", "two", "--save-dir", str(tmp_path), flag, "2"] + base, nproc=2)
+    assert two.returncode == 0, (two.stdout + two.stderr)[-3000:]
+    a, b = _losses(tmp_path / "one" / "metrics-rank0.jsonl"), _losses(tmp_path / "two" / "metrics-rank0.jsonl")
+    assert len(a) == len(b) == 3
+    for x, y in zip(a, b):
+        assert abs(x - y) < 2e-2 * abs(x), (a, b)
