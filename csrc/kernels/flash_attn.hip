@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 // double-buffered in LDS.  S and dP start from the row constants
 // (-lse/scale, -delta) so p = exp2(c2 S') and dS = p dP' need no per-element subtraction;
 // only the causal diagonal is masked (padded query rows carry Q = dO = 0 and contribute 0).
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int PF>
 __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int NC = D / 16;
@@ -565,37 +565,40 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
   const int nitems = per_head * group;
   const float inv_scale = 1.f / P.scale;
 
-  Stager<kKvBQ, D, 256> sq, sdo;
-  float rc = 0.f;
-  auto load_item = [&](int it) {
+  // Register-staged items: with PF = 2, item j is loaded into set j % 2 two items ahead of its
+  // use, so its global loads have a whole item of compute to land in (PF = 1: one set, loads
+  // issued one item ahead and waited for at the end of the current item).
+  struct Item {
+    Stager<kKvBQ, D, 256> q, dout;
+    uint32_t lse, dlt;  // raw f32 bits of this lane's row (lane & 31)
+  };
+  Item ia, ib;
+  auto load_item = [&](Item& X, int it) {
     const int hqi = kvh * group + it / per_head;
     const int qs = (first_slice + it % per_head) * kKvBQ;
     const int nv = seqlen - qs;
-    sq.load(P.q + (int64_t)(s0 + qs) * P.sq + (int64_t)hqi * D, P.sq, nv);
-    sdo.load(P.dout + ((int64_t)(s0 + qs) * P.hq + hqi) * D, (int64_t)P.hq * D, nv);
-    if (threadIdx.x < 64) {
-      const int qi = qs + (threadIdx.x & 31);
-      const bool ok = qi < seqlen;
-      if (threadIdx.x < 32) rc = ok ? -P.lse[(int64_t)hqi * P.T + s0 + qi] * inv_scale : 0.f;
-      else rc = ok ? -P.delta[(int64_t)hqi * P.T + s0 + qi] : 0.f;
+    X.q.load(P.q + (int64_t)(s0 + qs) * P.sq + (int64_t)hqi * D, P.sq, nv);
+    X.dout.load(P.dout + ((int64_t)(s0 + qs) * P.hq + hqi) * D, (int64_t)P.hq * D, nv);
+    // The rows' lse / delta through range-checked buffer loads (rows past the sequence end read
+    // 0), issued by every lane, kept raw and combined only in store_item.  A lane-divergent load
+    // (or math on it here) made hipcc put an s_waitcnt vmcnt(0) right behind it -- which also
+    // waits for the Q/dO prefetch just issued, exposing its whole latency in every item.  The
+    // volatile bit (aux bit 31) keeps the loads from being sunk into store_item's branch.
+    const int nrow = min(kKvBQ, seqlen - qs);
+    const int64_t ro = (int64_t)hqi * P.T + s0 + qs;
+    const int vo = (threadIdx.x & 31) * 4;
+    X.lse = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(P.lse + ro, nrow * 4), vo, 0, (int)(1u << 31));
+    X.dlt = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(P.delta + ro, nrow * 4), vo, 0, (int)(1u << 31));
+  };
+  auto store_item = [&](const Item& X, int buf) {
+    X.q.store(qd + buf * 2 * SLICE);
+    X.dout.store(qd + buf * 2 * SLICE + SLICE);
+    if (threadIdx.x < 64) {  // wave 0: lanes 0-31 -lse/scale, lanes 32-63 -delta
+      const float l = __builtin_bit_cast(float, X.lse), dl = __builtin_bit_cast(float, X.dlt);
+      rowc[buf * 64 + threadIdx.x] = (threadIdx.x & 32) ? -dl : -l * inv_scale;
     }
   };
-  auto store_item = [&](int buf) {
-    sq.store(qd + buf * 2 * SLICE);
-    sdo.store(qd + buf * 2 * SLICE + SLICE);
-    if (threadIdx.x < 64) rowc[buf * 64 + threadIdx.x] = rc;
-  };
-
-  if (nitems > 0) {
-    load_item(0);
-    store_item(0);
-  }
-  __syncthreads();
-
-  for (int it = 0; it < nitems; ++it) {
-    const int buf = it & 1;
-    const bool more = it + 1 < nitems;
-    if (more) load_item(it + 1);
+  auto compute = [&](int it, int buf) {
     const int qs = (first_slice + it % per_head) * kKvBQ;
     // No skip of the (at most 3 per head) slices whose queries all precede this wave's keys:
     // a branch around the dK/dV updates makes hipcc carry the accumulators through VGPR copies
@@ -653,8 +656,52 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
       pipeline_reads<4 * ND, 2, 3>();
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (more) store_item(buf ^ 1);
+  };
+
+  // Settle this lane's K/V fragment loads before the item loop, on every path into it.  Left
+  // pending, hipcc's wait-count analysis carried them around the loop's back edge and put an
+  // s_waitcnt vmcnt(1) / vmcnt(0) in front of the first S MFMA of every item -- a wait on the
+  // Q/dO loads just issued for a later item (ISA: llvm-objdump of bwd_dkdv_kernel).
+#pragma unroll
+  for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(kf[c]), "+v"(vf[c]));
+
+  if constexpr (PF == 2) {
+    // Prefetch loads are issued unconditionally (a finished tail re-reads its last item): with
+    // a branch around them hipcc's wait counting must assume they may be absent and drains
+    // every outstanding load at the next store, i.e. the prefetch stops being two items deep.
+    load_item(ia, 0);
+    load_item(ib, min(1, nitems - 1));
+    store_item(ia, 0);
     __syncthreads();
+    auto step = [&](int it, auto par) {
+      constexpr int S = decltype(par)::value;  // == it % 2: LDS buffer of item it
+      Item& cur = S == 0 ? ia : ib;            // item it: already in LDS, its registers are free
+      Item& nxt = S == 0 ? ib : ia;            // item it + 1, loaded one step ago
+      load_item(cur, min(it + 2, nitems - 1));
+      compute(it, S);
+      if (it + 1 < nitems) store_item(nxt, S ^ 1);
+      __syncthreads();
+    };
+    int it = 0;
+    for (; it + 1 < nitems; it += 2) {
+      step(it, std::integral_constant<int, 0>{});
+      step(it + 1, std::integral_constant<int, 1>{});
+    }
+    if (it < nitems) step(it, std::integral_constant<int, 0>{});
+  } else {
+    if (nitems > 0) {
+      load_item(ia, 0);
+      store_item(ia, 0);
+    }
+    __syncthreads();
+    for (int it = 0; it < nitems; ++it) {
+      const int buf = it & 1;
+      const bool more = it + 1 < nitems;
+      if (more) load_item(ia, it + 1);
+      compute(it, buf);
+      if (more) store_item(ia, buf ^ 1);
+      __syncthreads();
+    }
   }
 
   if (key < seqlen) {
@@ -766,6 +813,13 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
     const char* e = std::getenv("DTG_FA_OCC");
     return (e != nullptr && e[0] == '2') ? 2 : 1;
   }();
+  // Items the dK/dV kernel stages ahead (DTG_FA_KV_PF=1|2).  Equal on MI355X once the kernel's
+  // false vmcnt waits were gone (bwd 0.767 vs 0.768 ms at the 8B shape, profiles/r1_s51_*), so
+  // the single-set form with fewer registers is the default.
+  static const int kv_pf = [] {
+    const char* e = std::getenv("DTG_FA_KV_PF");
+    return (e != nullptr && e[0] == '2') ? 2 : 1;
+  }();
   {
     dim3 grid(hq, nseq, (max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ);
     const size_t lds = 4 * fa::kDqBK * D * 2;
@@ -782,11 +836,16 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   {
     dim3 grid(hkv, nseq, (max_seqlen + fa::kKvBK - 1) / fa::kKvBK);
     const size_t lds = 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
-#define DTG_BWD_KV(DD, C)                                                                 \
-  do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C>, lds);                         \
-       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C>), grid, dim3(256), lds, stream(), P); } while (0)
-    if (D == 128) { if (causal) DTG_BWD_KV(128, true); else DTG_BWD_KV(128, false); }
-    else { if (causal) DTG_BWD_KV(64, true); else DTG_BWD_KV(64, false); }
+#define DTG_BWD_KV(DD, C, PF)                                                             \
+  do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF>, lds);                     \
+       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C, PF>), grid, dim3(256), lds, stream(), P); } while (0)
+    if (kv_pf == 2) {
+      if (D == 128) { if (causal) DTG_BWD_KV(128, true, 2); else DTG_BWD_KV(128, false, 2); }
+      else { if (causal) DTG_BWD_KV(64, true, 2); else DTG_BWD_KV(64, false, 2); }
+    } else {
+      if (D == 128) { if (causal) DTG_BWD_KV(128, true, 1); else DTG_BWD_KV(128, false, 1); }
+      else { if (causal) DTG_BWD_KV(64, true, 1); else DTG_BWD_KV(64, false, 1); }
+    }
 #undef DTG_BWD_KV
     DTG_LAUNCH_CHECK();
   }
