@@ -25,6 +25,7 @@ import time
 from pathlib import Path
 
 import torch
+from tqdm import tqdm
 
 from .. import data as dtg_data
 from ..models import build_model, count_valid_labels, resolve_config
@@ -257,7 +258,12 @@ def run(chapter: str, argv=None):
         sampler.set_epoch(state["epoch"], skip=state["epoch_step"] * per_step)
         batches = iter(dataloader)
         n_steps = (sampler.full_len() // args.batch_size) // accum
+        # progress bar: rank 0 only, resumable; chapters 05-07 keep it off as the
+        # reference does (their logs are per-rank files)
+        progress = tqdm(total=n_steps, initial=state["epoch_step"], dynamic_ncols=True,
+                        disable=rank > 0 or chapter in ("05", "06", "07"))
         for i_step in range(state["epoch_step"], n_steps):
+            progress.update(1)
             micro = []
             with timers["data"], torch.no_grad():
                 for _ in range(accum):
@@ -341,8 +347,10 @@ def run(chapter: str, argv=None):
                 mgr.save(state)
             if args.max_steps and state["global_step"] >= args.max_steps:
                 LOGGER.info(f"Reached --max-steps {args.max_steps}")
+                progress.close()
                 mgr.finalize()
                 return state
+        progress.close()
         state["epoch_step"] = 0
     mgr.finalize()
     return state
