@@ -59,6 +59,18 @@ def test_data_parallel_matches_single(model_name, mode):
             torch.testing.assert_close(params[n], ref[n], atol=3e-4, rtol=1e-3, msg=f"rank {r} {n}")
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_zero_wide_world_matches_single(world):
+    """The bench's N=4 / N=8 layout: every bucket split 4 or 8 ways (padded tails, ranks whose
+    slice of a small bucket is all padding), one sequence per rank."""
+    batches = _batches(512, 8, 16)
+    ref, _ = _train("llama-tiny", "single", 0, 1, batches)
+    res = run_distributed(_worker, world, "llama-tiny", "zero", batches, 1)
+    for r in (0, world - 1):
+        for n in ref:
+            torch.testing.assert_close(res[r][0][n], ref[n], atol=3e-4, rtol=1e-3, msg=f"rank {r} {n}")
+
+
 def test_ddp_gradient_accumulation_no_sync():
     """2 ranks x 2 micro-batches with no_sync == 1 process on the full batch."""
     batches = _batches(512, 8, 16)
