@@ -1,0 +1,126 @@
+"""Auxiliary subsystems that PARITY.md listed without a covering test: the cluster monitor
+(reference top-cluster.py), LR scaling (F4), the JSONL metric sink (H3/H4),
+the launcher environment contract (I3) and the packed data-loader benchmark (E8)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import dtg  # noqa: E402,F401
+
+
+def _amd_smi_metric(n, power, util=90):
+    return json.dumps([
+        {"gpu": i,
+         "usage": {"gfx_activity": {"value": util, "unit": "%"}},
+         "power": {"socket_power": {"value": power, "unit": "W"},
+                   "power_limit": {"value": 1400, "unit": "W"}},
+         "mem_usage": {"used_vram": {"value": 144 * 1024, "unit": "MB"},
+                       "total_vram": {"value": 288 * 1024, "unit": "MB"}}}
+        for i in range(n)])
+
+
+def _amd_smi_process(n, per_gpu):
+    return json.dumps([{"gpu": i, "process_list": [{"process_info": {"pid": 100 + j}}
+                                                   for j in range(per_gpu)]} for i in range(n)])
+
+
+def test_cluster_monitor_parses_amd_smi_and_summarizes():
+    import top_cluster as tc
+
+    gpus = tc.parse_amd_smi(_amd_smi_metric(8, 1120), _amd_smi_process(8, 1))
+    assert len(gpus) == 8
+    assert gpus[0]["util"] == 90 and gpus[0]["power"] == 1120 and gpus[0]["nprocs"] == 1
+    s = tc.summarize(gpus)
+    assert s["power"] == pytest.approx(80.0)
+    assert s["mem"] == pytest.approx(50.0)
+    assert s["nprocs"] == 8
+    # the hang signature: processes present, power near idle
+    idle = tc.summarize(tc.parse_amd_smi(_amd_smi_metric(8, 140, util=100), _amd_smi_process(8, 1)))
+    assert idle["power"] < 20 and idle["nprocs"] > 0
+    # missing / malformed tool output degrades to "no data", not an exception
+    assert tc.summarize(tc.parse_amd_smi("", "")) is None
+    assert tc.parse_amd_smi(_amd_smi_metric(2, 500), "not json")[1]["nprocs"] == 0
+
+
+def test_cluster_monitor_dict_layout_and_defaults():
+    import top_cluster as tc
+
+    data = json.dumps({"gpu_data": [{"usage": {"gfx_usage": 12}, "power": {"current_socket_power": 700},
+                                     "vram": {"vram_used": 1024}}]})
+    (g,) = tc.parse_amd_smi(data, "[]")
+    assert g["util"] == 12 and g["power"] == 700
+    assert g["power_cap"] == 1400.0 and g["mem_total"] == 288 * 1024.0
+
+
+def test_lr_scaling_rules():
+    from dtg.utils.lr_scaling import effective_batch, scale_lr
+
+    assert effective_batch(16, 8, 4) == 512
+    assert scale_lr(3e-5, 16, 128, "linear") == pytest.approx(2.4e-4)
+    assert scale_lr(3e-5, 16, 64, "sqrt") == pytest.approx(6e-5)
+    assert scale_lr(1e-3, 32, 32) == pytest.approx(1e-3)
+    with pytest.raises(ValueError):
+        scale_lr(1e-3, 1, 2, "cubic")
+
+
+def test_metric_sink_writes_per_rank_jsonl(tmp_path, monkeypatch):
+    from dtg.utils.metrics import MetricSink
+
+    monkeypatch.setenv("DTG_NO_WANDB", "1")
+    sink = MetricSink(tmp_path, rank=3)
+    assert sink.wandb is None
+    sink.log({"loss": 2, "lr": 3e-5, "tag": "x"}, step=1)
+    sink.log({"loss": 1.5}, step=2)
+    lines = (tmp_path / "metrics-rank3.jsonl").read_text().splitlines()
+    recs = [json.loads(l) for l in lines]
+    assert recs[0] == {"loss": 2.0, "lr": 3e-5, "tag": "x"} and isinstance(recs[0]["loss"], float)
+    assert recs[1]["loss"] == 1.5
+
+
+@pytest.mark.parametrize("script", ["torchrun_single_node.sh", "launch_ssh_tmux.sh", "mpirun.sh", "job.sbatch"])
+def test_launchers_export_env_contract(script):
+    import re
+
+    text = open(os.path.join(ROOT, "03-job-launchers", script)).read()
+    # dmabuf IPC is the only mode the ROCm driver supports for RCCL / tensor sharing
+    assert re.search(r"HSA_ENABLE_IPC_MODE_LEGACY(=|:-)0", text)
+    assert re.search(r"OMP_NUM_THREADS(=|:-)1", text)
+
+
+def test_torchrun_launcher_env_and_command(tmp_path):
+    """Runs the single-node launcher with a stub `python` on PATH that records its env/argv."""
+    stub = tmp_path / "python"
+    stub.write_text("#!/bin/bash\n"
+                    "echo \"$TORCHELASTIC_ERROR_FILE|$OMP_NUM_THREADS|$HSA_ENABLE_IPC_MODE_LEGACY\" > \"$STUB_OUT\"\n"
+                    "echo \"$@\" >> \"$STUB_OUT\"\n")
+    stub.chmod(0o755)
+    out = tmp_path / "rec.txt"
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("TORCHELASTIC_ERROR_FILE", "OMP_NUM_THREADS", "HSA_ENABLE_IPC_MODE_LEGACY")}
+    env.update(PATH=f"{tmp_path}:{env.get('PATH', '')}", STUB_OUT=str(out))
+    r = subprocess.run(["bash", "torchrun_single_node.sh", "02-distributed-data-parallel", "-e", "x", "-b", "4"],
+                       cwd=os.path.join(ROOT, "03-job-launchers"), env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    envline, argv = out.read_text().splitlines()
+    assert envline == "../error.json|1|0"
+    assert "torch.distributed.run" in argv and "--nproc-per-node gpu" in argv
+    assert argv.endswith("../02-distributed-data-parallel/train_llm.py -e x -b 4")
+
+
+def test_dataloader_bench_runs_and_reports(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_dataloader.py"),
+                        "--batches", "20", "--seq-length", "1024", "--num-workers", "0", "--json"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["world"] == 1 and rec["tokens"] == 20 * 1024
+    assert rec["tok_per_s_total"] > 0
