@@ -9,6 +9,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -98,5 +99,45 @@ inline uint16_t* bf16_mut(const at::Tensor& t) { return reinterpret_cast<uint16_
 #define DTG_CHECK_CUDA_BF16(t)                                                     \
   DTG_CHECK((t).is_cuda() && (t).scalar_type() == at::kBFloat16, #t " must be a bf16 GPU tensor")
 #define DTG_LAUNCH_CHECK() C10_HIP_KERNEL_LAUNCH_CHECK()
+
+// Workgroup -> (row tile, column tile) for the tile-transposing streaming kernels.  gc == 0:
+// the 2-D grid's own (blockIdx.y, blockIdx.x).  gc > 0: a 1-D grid walked in bands of gc
+// column tiles, row tiles fastest inside a band, so the workgroups resident at one time read
+// gc * TC-wide row segments and write long contiguous runs of each transposed output row
+// (a wide [T, 28672] source otherwise has every resident workgroup writing 128 B into a
+// different output row).
+__device__ __forceinline__ void tile_coords(int gc, int64_t n_row_tiles, int64_t n_col_tiles, int64_t& rt,
+                                            int64_t& ct) {
+  if (gc <= 0) {
+    rt = blockIdx.y;
+    ct = blockIdx.x;
+    return;
+  }
+  const int64_t pid = blockIdx.x;
+  const int64_t per_band = (int64_t)gc * n_row_tiles;
+  const int64_t band = pid / per_band;
+  const int64_t first = band * gc;
+  const int64_t width = n_col_tiles - first < gc ? n_col_tiles - first : gc;
+  const int64_t in = pid - band * per_band;
+  rt = in / width;
+  ct = first + in % width;
+}
+
+constexpr int kDefaultTileGroup = 0;
+
+// Column-band width for tile_coords (DTG_TILE_GROUP, read per call; 0 = 2-D grid).
+inline int tile_group_env(int dflt) {
+  const char* e = std::getenv("DTG_TILE_GROUP");
+  return e ? std::atoi(e) : dflt;
+}
+
+inline dim3 tile_grid(int gc, int64_t n_row_tiles, int64_t n_col_tiles) {
+  if (gc <= 0) {
+    DTG_CHECK(n_row_tiles <= 65535, "tile grid: too many row tiles");
+    return dim3((unsigned)n_col_tiles, (unsigned)n_row_tiles);
+  }
+  DTG_CHECK(n_row_tiles * n_col_tiles < (int64_t(1) << 31), "tile grid: too many tiles");
+  return dim3((unsigned)(n_row_tiles * n_col_tiles));
+}
 
 }  // namespace dtg

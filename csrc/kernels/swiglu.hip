@@ -5,6 +5,8 @@
 //
 // One fused GEMM replaces the two HF Linear calls; this kernel reads gu once and writes h
 // once (forward) and reads dh + gu once to write dgu (backward).  f32 math, one rounding.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dtg {
@@ -56,21 +58,27 @@ __global__ void swiglu_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_
 // One workgroup owns a 64-token x 64-feature tile: 16-byte row loads of g, u, dh; the three
 // transposed tiles are staged through LDS (pitch 66 halfwords) and stored as 16-byte columns.
 namespace {
-constexpr int kSgTile = 64;
+constexpr int kSgTile = 64;  // features per workgroup
 constexpr int kSgPitch = kSgTile + 2;
 }  // namespace
 
+// TT tokens x 64 features per workgroup.  TT = 64 stores the transposed tiles as 128-byte
+// row segments, TT = 128 as 256-byte segments (twice the LDS: 3 x 128 x 66 halfwords).
+template <int TT>
 __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
     const uint16_t* __restrict__ dh, const uint16_t* __restrict__ gu, int64_t gu_stride,
-    uint16_t* __restrict__ dgu, uint16_t* __restrict__ dguT, uint16_t* __restrict__ hT, int64_t T, int I) {
-  __shared__ uint16_t s_dg[kSgTile * kSgPitch];
-  __shared__ uint16_t s_du[kSgTile * kSgPitch];
-  __shared__ uint16_t s_h[kSgTile * kSgPitch];
-  const int64_t t0 = (int64_t)blockIdx.y * kSgTile;
-  const int c0 = blockIdx.x * kSgTile;
+    uint16_t* __restrict__ dgu, uint16_t* __restrict__ dguT, uint16_t* __restrict__ hT, int64_t T, int I, int gc) {
+  static_assert(TT == 64 || TT == 128, "token tile");
+  __shared__ uint16_t s_dg[TT * kSgPitch];
+  __shared__ uint16_t s_du[TT * kSgPitch];
+  __shared__ uint16_t s_h[TT * kSgPitch];
+  int64_t rt, ct;
+  tile_coords(gc, (T + TT - 1) / TT, (I + kSgTile - 1) / kSgTile, rt, ct);
+  const int64_t t0 = rt * TT;
+  const int c0 = (int)ct * kSgTile;
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < TT / 32; ++i) {
     const int lt = (tid >> 3) + 32 * i;
     const int lc = (tid & 7) * 8;
     const int64_t t = t0 + lt;
@@ -103,10 +111,12 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
     }
   }
   __syncthreads();
+  constexpr int kVecPerRow = TT / 8;          // 16-byte vectors per transposed row segment
+  constexpr int kRowsPerIter = 256 / kVecPerRow;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int oc = (tid >> 3) + 32 * i;  // feature within the tile -> output row
-    const int ot = (tid & 7) * 8;        // first token of this 8-token vector
+  for (int i = 0; i < kSgTile / kRowsPerIter; ++i) {
+    const int oc = tid / kVecPerRow + kRowsPerIter * i;  // feature within the tile -> output row
+    const int ot = (tid % kVecPerRow) * 8;               // first token of this 8-token vector
     const int c = c0 + oc;
     const int64_t t = t0 + ot;
     if (c >= I || t >= T) continue;
@@ -137,10 +147,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& dh
   auto dguT = at::empty({2 * I, T}, gu.options());
   auto hT = at::empty({I, T}, gu.options());
   if (T == 0 || I == 0) return {dgu, dguT, hT};
-  const dim3 grid((I + kSgTile - 1) / kSgTile, (T + kSgTile - 1) / kSgTile);
-  DTG_CHECK(grid.y <= 65535, "swiglu_bwd_t: too many tokens");
-  swiglu_bwd_t_kernel<<<grid, 256, 0, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu),
-                                                  bf16_mut(dguT), bf16_mut(hT), T, I);
+  // DTG_SWIGLU_TT=64|128: token tile (A/B knob; see the kernel comment)
+  const char* tt_env = std::getenv("DTG_SWIGLU_TT");  // read per call: tests switch it in-process
+  const int tt = (tt_env && std::atoi(tt_env) == 128) ? 128 : 64;
+  const int gc = tile_group_env(kDefaultTileGroup);
+  const dim3 grid = tile_grid(gc, (T + tt - 1) / tt, (I + kSgTile - 1) / kSgTile);
+  if (tt == 128)
+    swiglu_bwd_t_kernel<128><<<grid, 256, 0, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu),
+                                                         bf16_mut(dguT), bf16_mut(hT), T, I, gc);
+  else
+    swiglu_bwd_t_kernel<64><<<grid, 256, 0, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu),
+                                                        bf16_mut(dguT), bf16_mut(hT), T, I, gc);
   DTG_LAUNCH_CHECK();
   return {dgu, dguT, hT};
 }

@@ -22,12 +22,15 @@ namespace dtg {
 // (same-box A/B, profiles/r1_s36_*); the wide [T, 2I] case alone favours 128 by ~3 %.
 template <int TR, int TC>
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ x, int64_t ldx,
-                                                             uint16_t* __restrict__ out, int64_t R, int64_t C) {
+                                                             uint16_t* __restrict__ out, int64_t R, int64_t C,
+                                                             int gc) {
   constexpr int P = TC + 2;             // LDS pitch in halfwords (odd dword count)
   constexpr int LV = TR * TC / 8 / 256; // 16-byte vectors per thread, each phase
   __shared__ uint16_t tile[TR * P];
-  const int64_t r0 = (int64_t)blockIdx.y * TR;
-  const int64_t c0 = (int64_t)blockIdx.x * TC;
+  int64_t rt, ct;
+  tile_coords(gc, (R + TR - 1) / TR, (C + TC - 1) / TC, rt, ct);
+  const int64_t r0 = rt * TR;
+  const int64_t c0 = ct * TC;
   const int tid = threadIdx.x;
   constexpr int VPR = TC / 8;  // vectors per input row
   constexpr int VPC = TR / 8;  // vectors per output row
@@ -69,14 +72,13 @@ at::Tensor transpose2d(const at::Tensor& x) {
     const char* e = std::getenv("DTG_TRANSPOSE_TILE");
     return e ? std::atoi(e) : 64;
   }();
+  const int gc = tile_group_env(kDefaultTileGroup);
   if (tile == 64) {
-    const dim3 grid((C + 63) / 64, (R + 63) / 64);
-    DTG_CHECK(grid.y <= 65535, "transpose2d: too many rows");
-    transpose_bf16_kernel<64, 64><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C);
+    const dim3 grid = tile_grid(gc, (R + 63) / 64, (C + 63) / 64);
+    transpose_bf16_kernel<64, 64><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C, gc);
   } else {
-    const dim3 grid((C + 127) / 128, (R + 127) / 128);
-    DTG_CHECK(grid.y <= 65535, "transpose2d: too many rows");
-    transpose_bf16_kernel<128, 128><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C);
+    const dim3 grid = tile_grid(gc, (R + 127) / 128, (C + 127) / 128);
+    transpose_bf16_kernel<128, 128><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C, gc);
   }
   DTG_LAUNCH_CHECK();
   return out;

@@ -82,16 +82,22 @@ def test_swiglu(cuda):
     _close(dops.swiglu_bwd(dh.to(cuda), gu.to(cuda)), dops.swiglu_bwd(dh, gu), 3e-2, 2e-2, "swiglu bwd")
 
 
+@pytest.mark.parametrize("group", ["0", "3", "16"])
 @pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (4096, 6144, 6144), (1000, 520, 528), (8, 8, 8), (136, 7000, 7000)])
-def test_transpose2d(cuda, R, C, ld):
+def test_transpose2d(cuda, R, C, ld, group, monkeypatch):
+    monkeypatch.setenv("DTG_TILE_GROUP", group)  # 2-D grid, and banded 1-D grids (ragged last band)
     x = torch.randn(R, ld).bfloat16()[:, :C]
     y = dops.transpose2d(x.to(cuda))
     assert y.shape == (C, R) and y.is_contiguous()
     assert torch.equal(y.cpu(), x.t().contiguous())
 
 
+@pytest.mark.parametrize("group", ["0", "3", "16"])
+@pytest.mark.parametrize("tt", ["64", "128"])
 @pytest.mark.parametrize("T,I", [(64, 64), (4096, 1792), (520, 136)])
-def test_swiglu_bwd_t(cuda, T, I):
+def test_swiglu_bwd_t(cuda, T, I, tt, group, monkeypatch):
+    monkeypatch.setenv("DTG_SWIGLU_TT", tt)
+    monkeypatch.setenv("DTG_TILE_GROUP", group)
     torch.manual_seed(0)
     gu = (2 * torch.randn(T, 2 * I)).bfloat16()
     dh = torch.randn(T, I).bfloat16()
