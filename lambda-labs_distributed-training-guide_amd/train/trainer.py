@@ -249,6 +249,7 @@ def run(chapter: str, argv=None):
                         "(time/forward covers the whole step; time/backward and time/update read 0)")
         else:
             LOGGER.warning("--hip-graph needs one GPU, a single-process engine and --grad-accum 1; running eagerly")
+    run_loss = None  # device-side running-loss accumulator (flushed into state at log / ckpt steps)
     for state["epoch"] in range(state["epoch"], args.num_epochs):
         LOGGER.info(f"Begin epoch {state['epoch']} at step {state['epoch_step']}")
         sampler = dataloader.sampler
@@ -315,8 +316,13 @@ def run(chapter: str, argv=None):
             state["epoch_step"] += 1
             if args.torch_profile_steps > 0:
                 prof = _profile_tick(prof, state["global_step"], prof_start, prof_stop, exp_dir, rank, device)
-            state["running_loss"] += (loss_sum / accum).item()
+            # summed on the device; one host sync per --log-freq window / checkpoint instead of the
+            # reference's `.item()` every step
+            run_loss = loss_sum / accum if run_loss is None else run_loss + loss_sum / accum
 
+            if state["global_step"] % args.log_freq == 0 or state["global_step"] % args.ckpt_freq == 0:
+                state["running_loss"] += float(run_loss.item())
+                run_loss = None
             if state["global_step"] % args.log_freq == 0:
                 ms_per_step = sum(t.avg_elapsed_ms() for t in timers.values())
                 tps = 1000 * tok_per_step / ms_per_step if ms_per_step > 0 else 0.0
@@ -346,12 +352,16 @@ def run(chapter: str, argv=None):
                 LOGGER.info("Saving checkpoint.")
                 mgr.save(state)
             if args.max_steps and state["global_step"] >= args.max_steps:
+                if run_loss is not None:
+                    state["running_loss"] += float(run_loss.item())
                 LOGGER.info(f"Reached --max-steps {args.max_steps}")
                 progress.close()
                 mgr.finalize()
                 return state
         progress.close()
         state["epoch_step"] = 0
+    if run_loss is not None:
+        state["running_loss"] += float(run_loss.item())
     mgr.finalize()
     return state
 
