@@ -112,3 +112,23 @@ def test_sequence_parallel_chapter_matches_single_process(tmp_path, flag, datase
     assert len(a) == len(b) == 3
     for x, y in zip(a, b):
         assert abs(x - y) < 2e-2 * abs(x), (a, b)
+
+
+@pytest.mark.slow
+def test_running_loss_window_means_match_per_step_losses(tmp_path):
+    """The running loss is summed on the device and read only at log / checkpoint steps: a
+    --log-freq 2 run with a checkpoint mid-window (--ckpt-freq 3) logs the pairwise means of the
+    per-step losses of an otherwise identical --log-freq 1 run."""
+    def run(name, log_freq, ckpt_freq):
+        r = _torchrun("02-distributed-data-parallel",
+                      ["-e", name, "-d", "synthetic", "-m", "llama-tiny", "-s", "32", "--num-samples", "64",
+                       "--save-dir", str(tmp_path), "--log-freq", str(log_freq), "--ckpt-freq", str(ckpt_freq),
+                       "--num-workers", "0", "--max-steps", "6"], nproc=1)
+        assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+        return [json.loads(l)["running_loss"] for l in (tmp_path / name / "metrics-rank0.jsonl").read_text().splitlines()]
+
+    per_step = run("l1", 1, 100)
+    windows = run("l2", 2, 3)
+    assert len(per_step) == 6 and len(windows) == 3
+    for k in range(3):
+        assert windows[k] == pytest.approx((per_step[2 * k] + per_step[2 * k + 1]) / 2, rel=1e-5)
