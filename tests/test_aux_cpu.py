@@ -124,3 +124,22 @@ def test_dataloader_bench_runs_and_reports(tmp_path):
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["world"] == 1 and rec["tokens"] == 20 * 1024
     assert rec["tok_per_s_total"] > 0
+
+
+def test_collectives_bench_gloo_rehearsal():
+    """tools/bench_collectives.py harness at world 2 on gloo: every op reports
+    nccl-tests style algbw / busbw with the right bus factor."""
+    from _dist import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tools", "bench_collectives.py"), "--backend", "gloo", "--json",
+           "--min-mb", "0.25", "--max-mb", "0.5", "--iters", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert {x["op"] for x in recs} == {"all_reduce", "all_gather", "reduce_scatter", "all_to_all"}
+    assert len(recs) == 8 and all(x["world"] == 2 and x["time_us"] > 0 for x in recs)
+    for x in recs:
+        factor = 1.0 if x["op"] == "all_reduce" else 0.5  # 2(n-1)/n and (n-1)/n at n = 2
+        assert x["busbw_GBps"] == pytest.approx(x["algbw_GBps"] * factor, rel=0.02, abs=0.02)

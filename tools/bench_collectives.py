@@ -18,19 +18,26 @@ import torch
 import torch.distributed as dist
 
 
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+
+
 def bench(op, nbytes, world, device, iters, warmup, xg=None):
-    n = nbytes // 2
-    x = torch.randn(n, device=device).bfloat16()
+    # gloo (CPU rehearsal) has no bf16 reductions: fp32 elements there, same byte count
+    dt_ = torch.bfloat16 if device.type == "cuda" else torch.float32
+    n = nbytes // (2 if dt_ == torch.bfloat16 else 4)
+    x = torch.randn(n, device=device).to(dt_)
     if op == "all_reduce":
         fn = (lambda: xg.all_reduce_(x)) if xg else (lambda: dist.all_reduce(x))
         factor = 2 * (world - 1) / world
     elif op == "all_gather":
-        out = torch.empty(n * world, device=device, dtype=torch.bfloat16)
+        out = torch.empty(n * world, device=device, dtype=dt_)
         fn = (lambda: xg.all_gather_into(out, x)) if xg else (lambda: dist.all_gather_into_tensor(out, x))
         factor = (world - 1) / world
         nbytes = nbytes * world
     elif op == "reduce_scatter":
-        out = torch.empty(n // world, device=device, dtype=torch.bfloat16)
+        out = torch.empty(n // world, device=device, dtype=dt_)
         fn = (lambda: xg.reduce_scatter_into(out, x)) if xg else (lambda: dist.reduce_scatter_tensor(out, x))
         factor = (world - 1) / world
     else:
@@ -39,12 +46,12 @@ def bench(op, nbytes, world, device, iters, warmup, xg=None):
         factor = (world - 1) / world
     for _ in range(warmup):
         fn()
-    torch.cuda.synchronize()
+    _sync(device)
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
         fn()
-    torch.cuda.synchronize()
+    _sync(device)
     dt = (time.perf_counter() - t0) / iters
     algbw = nbytes / dt / 1e9
     return dt * 1e6, algbw, algbw * factor
@@ -59,11 +66,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--json", action="store_true")
     ap.add_argument("--impl", default="rccl", choices=["rccl", "xgmi"])
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: CPU rehearsal of the harness (fp32 elements, no GPU)")
     a = ap.parse_args()
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-    dist.init_process_group("nccl", device_id=device)
+    if a.backend == "gloo":
+        assert a.impl == "rccl", "--impl xgmi needs GPUs"
+        device = torch.device("cpu")
+        dist.init_process_group("gloo")
+    else:
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+        dist.init_process_group("nccl", device_id=device)
     world, rank = dist.get_world_size(), dist.get_rank()
     xg = None
     ops = a.ops.split(",")
@@ -75,7 +89,7 @@ def main():
         ops = [o for o in ops if o != "all_to_all"]
     size = a.min_mb
     while size <= a.max_mb:
-        nbytes = int(size * (1 << 20)) // (2 * world) * (2 * world)
+        nbytes = int(size * (1 << 20)) // (4 * world) * (4 * world)
         for op in ops:
             us, alg, bus = bench(op, nbytes, world, device, a.iters, a.warmup, xg)
             if rank == 0:
