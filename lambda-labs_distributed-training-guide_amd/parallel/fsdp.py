@@ -19,7 +19,11 @@ Design (MI355X-first, not a wrapper around torch FSDP):
     `reshard_after_forward=False` the gathered units stay resident until backward (ZeRO-2-like
     traffic, 2/3 of the all-gathers) when memory allows.
   * `cpu_offload=True` keeps parameter shards, gradient shards and optimizer state in pinned
-    host memory and runs the native C++ AdamW on the CPU (chapter 05).
+    host memory and runs the native C++ AdamW on the CPU (chapter 05).  With
+    `overlap_cpu_step` (default) the host update of each unit starts on a worker thread as soon
+    as that unit's gradient shard has landed in host memory during the last micro-batch's
+    backward, so the CPU optimizer runs under the rest of the backward instead of after it
+    (same kernel, same inputs: bit-identical to the post-backward update).
   * Meta-device init: units are materialised one at a time on the GPU, initialised with the
     same seed on every rank, and only the local shard is kept (peak = one unit).
 """
@@ -123,7 +127,8 @@ class FullyShard:
     def __init__(self, model: nn.Module, group=None, policy: str = "transformer", min_num_params: int = 100_000_000,
                  device=None, reshard_after_forward: bool = True, cpu_offload: bool = False,
                  state_dtype=torch.bfloat16, init_fn: Optional[Callable] = None, seed: int = 0,
-                 prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None, replicate_group=None):
+                 prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None, replicate_group=None,
+                 overlap_cpu_step: bool = True):
         self.module = model
         self.group = group
         # HYBRID_SHARD (ZeRO++-style): shard inside `group` (one node's xGMI island), replicate
@@ -137,6 +142,13 @@ class FullyShard:
         self.mode = "fsdp" if self.replicas == 1 else "hybrid"
         self.reshard_after_forward = reshard_after_forward
         self.cpu_offload = cpu_offload
+        self.overlap_cpu_step = overlap_cpu_step
+        self._hparams = None  # bound by FlatAdamW: () -> (lr, beta1, beta2, eps, weight_decay)
+        self._in_no_sync = False
+        self._bwd_step = None  # (step, grad_scale, hparams) while a backward updates units in flight
+        self._cpu_pool = None
+        self._cpu_futs = []
+        self._bwd_stepped = False
         self.prefetch = prefetch
         self.max_inflight_rs = max_inflight_rs
         p0 = next(model.parameters())
@@ -337,6 +349,9 @@ class FullyShard:
         if u.full_grad is not None:
             return
         u.full_grad = torch.empty(u.numel, dtype=self.dtype, device=self.device)
+        # a fresh (uninitialised) full gradient per micro-batch: the first write of every param
+        # must overwrite, not accumulate (micro-batches are summed in the gradient shard)
+        reset_grad_state(u.params)
         for i, p in enumerate(u.params):
             n = math.prod(u.shapes[i])
             p.main_grad = u.full_grad[u.offsets[i]:u.offsets[i] + n].view(u.shapes[i])
@@ -386,6 +401,8 @@ class FullyShard:
                 gs.copy_(out)
             else:
                 gs.add_(out.to(gs.device))
+        if self._bwd_step is not None:
+            self._submit_host_step(u)
         u.full_grad = None
         for p in u.params:
             p.main_grad = None
@@ -406,16 +423,48 @@ class FullyShard:
     @contextlib.contextmanager
     def no_sync(self):
         """Gradient accumulation: FSDP still reduce-scatters each micro-batch (memory stays
-        sharded) and accumulates into the gradient shard; this context only defers nothing
-        and exists for API parity with DataParallel."""
-        yield
+        sharded) and accumulates into the gradient shard; inside this context a backward is
+        known not to be the last micro-batch (no host optimizer overlap)."""
+        prev, self._in_no_sync = self._in_no_sync, True
+        try:
+            yield
+        finally:
+            self._in_no_sync = prev
+
+    def _submit_host_step(self, u):
+        import concurrent.futures as cf
+
+        from ..ops.adamw import adamw_step_cpu
+
+        if self._cpu_pool is None:  # one worker: units update in order, OpenMP inside the kernel
+            self._cpu_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="dtg-host-adamw")
+        step, scale, (lr, b1, b2, eps, wd) = self._bwd_step
+        sl = slice(u.shard_off, u.shard_off + u.shard_numel)
+        self._cpu_futs.append(self._cpu_pool.submit(
+            adamw_step_cpu, self.shard_params[sl], self.shard_grads[sl], self.exp_avg[sl], self.exp_avg_sq[sl],
+            lr=lr, step=step, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, grad_scale=scale))
 
     def backward(self, loss):
-        loss.backward()
-        self.accum_count += 1
-        self.finish_grad_sync()
+        overlap = (self.cpu_offload and self.overlap_cpu_step and self._hparams is not None
+                   and self.replicas == 1 and not self._in_no_sync)
+        if overlap:  # the last micro-batch: its per-unit gradient shards are final on arrival
+            scale = 1.0 / (self.world * self.replicas * (self.accum_count + 1))
+            self._bwd_step = (self.step_count + 1, scale, self._hparams())
+        try:
+            loss.backward()
+            self.accum_count += 1
+            self.finish_grad_sync()
+        finally:
+            self._bwd_step = None
+        self._bwd_stepped = overlap
+
+    def _join_host_steps(self):
+        futs, self._cpu_futs = self._cpu_futs, []
+        for f in futs:
+            f.result()
 
     def zero_grad(self):
+        self._join_host_steps()  # never let a host update race the next forward's shard reads
         for u in self.all_units:
             reset_grad_state(u.params)
             u.pending = u.expected
@@ -425,6 +474,10 @@ class FullyShard:
     # ------------------------------------------------------------------ optimizer
     def step(self, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, grad_scale=None):
         self.step_count += 1
+        if self._bwd_stepped:  # overlap_cpu_step: every unit was updated during backward
+            self._bwd_stepped = False
+            self._join_host_steps()
+            return
         if grad_scale is None:
             grad_scale = 1.0 / (self.world * self.replicas * max(1, self.accum_count))
         if self.replicas > 1:

@@ -121,3 +121,53 @@ def test_hybrid_shard_matches_single():
         assert (mode, w, reps) == ("hybrid", 2, 2)
         for n in ref:
             torch.testing.assert_close(sd[n], ref[n], **TOL, msg=f"rank {r} {n}")
+
+
+def _offload_train(rank, world, batches, overlap, accum, offload=True):
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+
+    torch.manual_seed(0)
+    model = build_model("llama-tiny", device="cpu", dtype=torch.float32)
+    eng = FullyShard(model, cpu_offload=offload, device="cpu", overlap_cpu_step=overlap)
+    opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))  # lr changes every step
+    stepped_in_bwd = []
+    for ids in batches:
+        per = ids.shape[0] // world
+        mine = ids[rank * per:(rank + 1) * per]
+        opt.zero_grad()
+        micro = mine.chunk(accum)
+        for j, mb in enumerate(micro):
+            ctx = eng.no_sync() if j < accum - 1 else torch.enable_grad()
+            with ctx:
+                eng.backward(model(input_ids=mb, labels=mb).loss)
+        stepped_in_bwd.append(eng._bwd_stepped)
+        opt.step()
+        sched.step()
+    return eng.full_state_dict(rank0_only=False), stepped_in_bwd
+
+
+@pytest.mark.parametrize("accum", [1, 2])
+def test_fsdp_offload_overlapped_host_step_is_bit_identical(accum):
+    """overlap_cpu_step: host AdamW per unit during the last micro-batch's backward gives exactly
+    the post-backward update (world 2, changing lr, with and without gradient accumulation)."""
+    batches = _batches(512, 4, 32, n=3)  # 2 rows per rank -> accum micro-batches of 1 row
+    on = run_distributed(_offload_train, 2, batches, True, accum)
+    off = run_distributed(_offload_train, 2, batches, False, accum)
+    for r in range(2):
+        assert all(on[r][1]) and not any(off[r][1])
+        for n, t in off[r][0].items():
+            assert torch.equal(on[r][0][n], t), f"rank {r} {n}"
+
+
+@pytest.mark.parametrize("offload", [False, True])
+def test_fsdp_grad_accumulation_matches_full_batch(offload):
+    """Two micro-batches (first under no_sync) == one full batch: every micro-batch's fresh full
+    gradient is overwritten, not accumulated into (regression: uninitialised memory was summed)."""
+    batches = _batches(512, 4, 32, n=2)
+    one = run_distributed(_offload_train, 2, batches, False, 1, offload)
+    two = run_distributed(_offload_train, 2, batches, False, 2, offload)
+    for n, t in one[0][0].items():
+        torch.testing.assert_close(two[0][0][n], t, **TOL, msg=n)  # pre-fix error: ~2 x lr = 2e-2
