@@ -1,30 +1,45 @@
 #!/usr/bin/env python3
 """Headline benchmark: causal-LM pretraining throughput on MI355X (BASELINE.json metric).
 
-    python bench.py --gpus N --steps K --warmup W            (N=1)
-    torchrun --nproc-per-node N bench.py --gpus N ...         (N>1, one rank per GPU, RCCL)
+    python bench.py --gpus N --steps K --warmup W
+        N=1: runs in this process.
+        N>1 without a launcher: starts `torch.distributed.run --nproc-per-node N` as a CHILD
+        process (nothing in this parent touches the GPU) and exits with its code, so the same
+        command measures N ranks, one per GPU, over RCCL.
+    torchrun --nproc-per-node N bench.py --gpus N ...
+        one rank per GPU; the process group must see exactly N ranks (asserted).
 
 Config: Llama-3-8B (bundled config, random init, pure bf16 params/grads/AdamW states as in the
-reference), synthetic token data, seq 1024, fixed per-GPU micro-batch (weak scaling). Every
+reference), synthetic token data, seq 1024, fixed per-GPU micro-batch (weak scaling).  Every
 timed step does the full work: forward, backward with overlapped bucketed gradient
 reduce-scatter, fused AdamW on the local shard, parameter all-gather and the cosine LR step.
 K steps are bracketed by barrier + device synchronize on both sides; the slowest rank's time is
 reported.  Rank 0 prints one JSON line (value = whole-job tokens/s).
+
+"FSDP peak-mem" half of the metric: after the timed throughput phase the ZeRO model is freed
+and a short FSDP (FULL_SHARD, size-based wrap at --numel-to-wrap) phase runs the reference's
+memory-table config (Llama-2-7B, batch 10, seq 1024: /root/reference/04-fully-sharded-data-parallel/
+README.md:271-281) over the same ranks; its per-rank valley (allocated at the end of an
+iteration) and peak (max allocated during it) are reported, max over ranks.  That phase is
+outside the timed region and does not affect `value`.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "tokens/sec/GPU (causal-LM pretrain) at 1/2/4/8 MI355X; FSDP peak-mem"
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -42,45 +57,44 @@ def parse():
     ap.add_argument("--tunableop", choices=["off", "use", "tune"], default="use",
                     help="PyTorch TunableOp for the hipBLASLt GEMMs: 'use' loads the committed per-shape "
                          "solution table (tunableop/), 'tune' benchmarks new shapes during warmup and writes it")
-    return ap.parse_args()
+    # FSDP memory phase (not timed into `value`)
+    ap.add_argument("--fsdp-mem-model", default="llama-2-7b")
+    ap.add_argument("--fsdp-mem-batch", type=int, default=10)
+    ap.add_argument("--fsdp-mem-seq", type=int, default=1024)
+    ap.add_argument("--fsdp-mem-steps", type=int, default=3, help="0 skips the FSDP memory phase")
+    ap.add_argument("--numel-to-wrap", type=int, default=100_000_000)
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    import dtg  # noqa: F401
+
+def self_launch(args, argv) -> int:
+    """N ranks without an external launcher: torchrun as a child process (never exec from a
+    process that may have touched the GPU), one rank per GPU, rendezvous on 127.0.0.1."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def _sync(dist, world, cuda):
+    if world > 1:
+        dist.barrier()
+    if cuda:
+        import torch
+
+        torch.cuda.synchronize()
+
+
+def throughput_phase(args, torch, dist, device, world, rank, cuda):
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
-
-    if args.tunableop != "off" and torch.cuda.is_available():
-        from dtg.utils.gemm_tuning import enable_tunableop
-
-        enable_tunableop(tune=args.tunableop == "tune")
-    if args.tunableop == "tune":
-        import threading
-
-        def _heartbeat():  # tuning can run minutes inside one step: keep the job visibly alive
-            t0 = time.time()
-            while True:
-                time.sleep(30)
-                print(f"[bench] tuning GEMMs... {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
-
-        threading.Thread(target=_heartbeat, daemon=True).start()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    cuda = torch.cuda.is_available()
-    # DTG_SHARED_DEVICE=1: every rank on cuda:0 (engine tests with the gloo backend on a 1-GPU box)
-    dev_idx = 0 if os.environ.get("DTG_SHARED_DEVICE") == "1" else local_rank
-    device = torch.device(f"cuda:{dev_idx}" if cuda else "cpu")
-    if cuda:
-        torch.cuda.set_device(device)
-    if world > 1:
-        backend = args.backend or ("nccl" if cuda else "gloo")
-        dist.init_process_group(backend, device_id=device if (cuda and backend == "nccl") else None)
-    torch.manual_seed(0)
 
     cfg = resolve_config(args.model)
     model = build_model(cfg, device=device)
@@ -108,35 +122,25 @@ def main():
         sched.step()
         return out.loss
 
-    def sync():
-        if world > 1:
-            dist.barrier()
-        if cuda:
-            torch.cuda.synchronize()
-
     loss = None
     for i in range(args.warmup):
         tw = time.perf_counter()
         loss = step(i)
         if cuda:
             torch.cuda.synchronize()
-        print(f"[bench] warmup step {i}: {time.perf_counter() - tw:.2f}s", file=sys.stderr, flush=True)
-    sync()
+        print(f"[bench] rank {rank} warmup step {i}: {time.perf_counter() - tw:.2f}s", file=sys.stderr, flush=True)
+    _sync(dist, world, cuda)
     if cuda:
         torch.cuda.reset_peak_memory_stats(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(args.warmup + i)
-    sync()
+    _sync(dist, world, cuda)
     elapsed = time.perf_counter() - t0
     if args.tunableop == "tune" and cuda and rank == 0:
         from dtg.utils.gemm_tuning import save_tunableop
 
         save_tunableop()
-    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
     peak_gb = torch.cuda.max_memory_allocated(device) / 2**30 if cuda else 0.0
 
     if args.profile_steps > 0 and cuda:
@@ -150,7 +154,128 @@ def main():
             os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
             with open(os.path.join(ROOT, "gpurun_out", "torch_profile.txt"), "w") as fp:
                 fp.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+    res = dict(elapsed=elapsed, peak_gb=peak_gb, loss=float(loss.item()), cfg=cfg,
+               mode=getattr(engine, "mode", args.parallel))
+    if hasattr(engine, "wait_param_gather"):
+        engine.wait_param_gather()
+    del model, engine, opt, sched, batches, loss
+    return res
 
+
+def fsdp_memory_phase(args, torch, dist, device, world, rank, cuda):
+    """Valley / peak allocated GB per rank of FSDP FULL_SHARD on the reference's memory-table
+    config (chapter 04).  Meta-device init: units are materialised one at a time."""
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+
+    cfg = resolve_config(args.fsdp_mem_model)
+    with torch.device("meta"):
+        model = build_model(cfg, init=False)
+    engine = FullyShard(model, policy="size", min_num_params=args.numel_to_wrap, device=device)
+    opt = FlatAdamW(engine, lr=args.lr)
+    B, S = args.fsdp_mem_batch, args.fsdp_mem_seq
+    g = torch.Generator(device=device).manual_seed(99 + rank)
+    ids = torch.randint(0, cfg.vocab_size, (B, S), device=device, generator=g)
+    gb = 2**30
+    valley = peak = 0.0
+    _sync(dist, world, cuda)
+    t0 = time.perf_counter()
+    for i in range(args.fsdp_mem_steps):
+        if cuda:
+            torch.cuda.synchronize()
+            torch.cuda.reset_peak_memory_stats(device)
+        out = model(input_ids=ids, labels=ids, num_valid=B * (S - 1))
+        engine.backward(out.loss)
+        opt.step()
+        opt.zero_grad()
+        del out
+        if cuda:
+            torch.cuda.synchronize()
+            peak = torch.cuda.max_memory_allocated(device) / gb
+            valley = torch.cuda.memory_allocated(device) / gb
+    _sync(dist, world, cuda)
+    ms = 1000 * (time.perf_counter() - t0) / max(1, args.fsdp_mem_steps)
+    del model, engine, opt, ids
+    return dict(valley=valley, peak=peak, ms=ms, model=cfg.hf_name or args.fsdp_mem_model)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args, argv)
+
+    import gc
+
+    import torch
+    import torch.distributed as dist
+
+    import dtg  # noqa: F401
+
+    if args.tunableop != "off" and torch.cuda.is_available():
+        from dtg.utils.gemm_tuning import enable_tunableop
+
+        enable_tunableop(tune=args.tunableop == "tune")
+    if args.tunableop == "tune":
+        import threading
+
+        def _heartbeat():  # tuning can run minutes inside one step: keep the job visibly alive
+            t0 = time.time()
+            while True:
+                time.sleep(30)
+                print(f"[bench] tuning GEMMs... {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+
+        threading.Thread(target=_heartbeat, daemon=True).start()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    cuda = torch.cuda.is_available()
+    # DTG_SHARED_DEVICE=1: every rank on cuda:0 (engine tests with the gloo backend on a 1-GPU box)
+    dev_idx = 0 if os.environ.get("DTG_SHARED_DEVICE") == "1" else local_rank
+    if cuda and os.environ.get("DTG_SHARED_DEVICE") != "1":
+        assert local_rank < torch.cuda.device_count(), \
+            f"local rank {local_rank} has no GPU (device_count={torch.cuda.device_count()})"
+    device = torch.device(f"cuda:{dev_idx}" if cuda else "cpu")
+    if cuda:
+        torch.cuda.set_device(device)
+    backend = None
+    if world > 1:
+        backend = args.backend or ("nccl" if cuda else "gloo")
+        dist.init_process_group(backend, device_id=device if (cuda and backend == "nccl") else None)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    pg_world = dist.get_world_size() if dist.is_initialized() else 1
+    torch.manual_seed(0)
+
+    res = throughput_phase(args, torch, dist, device, world, rank, cuda)
+    gc.collect()
+    if cuda:
+        torch.cuda.empty_cache()
+    mem = None
+    if args.fsdp_mem_steps > 0:
+        mem = fsdp_memory_phase(args, torch, dist, device, world, rank, cuda)
+        gc.collect()
+
+    # per-rank facts, gathered to rank 0: elapsed, device ordinal, PCI bus, peaks
+    me = [res["elapsed"], float(dev_idx), float(res["peak_gb"]),
+          mem["valley"] if mem else 0.0, mem["peak"] if mem else 0.0, mem["ms"] if mem else 0.0]
+    mine = torch.tensor(me, dtype=torch.float64, device=device)
+    if world > 1:
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        rows = [v.cpu().tolist() for v in allv]
+    else:
+        rows = [mine.cpu().tolist()]
+    bus = None
+    if cuda:
+        p = torch.cuda.get_device_properties(device)
+        bus = getattr(p, "pci_bus_id", None)
+    elapsed = max(r[0] for r in rows)  # the slowest rank bounds the job
+
+    cfg = res["cfg"]
+    B, S = args.batch_size, args.seq_len
     tokens = world * B * S * args.steps
     tps = tokens / elapsed
     ms = 1000 * elapsed / args.steps
@@ -158,7 +283,7 @@ def main():
     mfu = tps * flops_tok / (world * 2.5e15) if cuda else 0.0
     if rank == 0:
         rec = {
-            "metric": "tokens/sec/GPU (causal-LM pretrain) at 1/2/4/8 MI355X; FSDP peak-mem",
+            "metric": METRIC,
             "value": round(tps, 1),
             "unit": "tokens/s (whole job)",
             "n_gpus": world,
@@ -171,16 +296,32 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": cfg.hf_name or args.model, "global_batch": world * B, "seq_len": S,
-                       "parallelism": f"dp{world}-{engine.mode if hasattr(engine, 'mode') else args.parallel}"},
+                       "parallelism": f"dp{world}-{res['mode']}"},
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
-            "peak_mem_gb": round(peak_gb, 2),
-            "final_loss": round(float(loss.item()), 4),
+            "peak_mem_gb": round(max(r[2] for r in rows), 2),
+            "final_loss": round(res["loss"], 4),
+            "world_size_seen_by_pg": pg_world,
+            "backend": backend or "none",
+            "rank_devices": [int(r[1]) for r in rows],
+            "rank0_pci_bus_id": bus,
+            "rank_ms_per_step": {"max": round(1000 * elapsed / args.steps, 2),
+                                 "min": round(1000 * min(r[0] for r in rows) / args.steps, 2)},
         }
+        if mem is not None:
+            rec["fsdp_mem"] = {"model": mem["model"], "batch_per_gpu": args.fsdp_mem_batch,
+                               "seq_len": args.fsdp_mem_seq, "wrap": f"size>={args.numel_to_wrap}",
+                               "valley_gb_max_rank": round(max(r[3] for r in rows), 2),
+                               "peak_gb_max_rank": round(max(r[4] for r in rows), 2),
+                               "ms_per_step": round(max(r[5] for r in rows), 1),
+                               "reference_a100x8": {"valley_gb": 8, "peak_gb": 74}}
+            rec["fsdp_peak_mem_gb"] = rec["fsdp_mem"]["peak_gb_max_rank"]
         print(json.dumps(rec), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

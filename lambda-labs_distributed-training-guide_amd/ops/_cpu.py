@@ -216,10 +216,16 @@ def transpose2d(x):
     return x.t().contiguous()
 
 
+def embedding_bwd_(out, ids, dy):
+    acc = torch.zeros(out.shape, dtype=torch.float32)
+    acc.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).float())
+    out.copy_((out.float() + acc).to(out.dtype))
+
+
 for _name, _fn in list(globals().items()):
     if _name in (
         "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "flash_attn_fwd", "flash_attn_bwd",
-        "flash_attn_bwd_qkv", "transpose2d", "swiglu_bwd_t",
+        "flash_attn_bwd_qkv", "transpose2d", "swiglu_bwd_t", "embedding_bwd_",
     ):
         LIB.impl(_name, _fn, "CPU")

@@ -30,6 +30,7 @@ _DEFS = [
     "flash_attn_bwd_qkv(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
     "Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> Tensor",
     "transpose2d(Tensor x) -> Tensor",
+    "embedding_bwd_(Tensor(a!) out, Tensor ids, Tensor dy) -> ()",
 ]
 
 for _d in _DEFS:

@@ -90,14 +90,17 @@ def route_weight_grad_mm(param, a, b, a_t=None, b_t=None):
 
 
 def route_embedding_grad(param, ids, dy, num_weights):
+    """Embedding backward through the deterministic sorted segment-sum (dtg::embedding_bwd_):
+    bitwise reproducible, f32 sums rounded once per row (ATen's index_add_ uses bf16 atomics)."""
     mg = getattr(param, "main_grad", None)
+    dy2 = dy.reshape(-1, dy.shape[-1])
     if mg is None:
         g = torch.zeros(num_weights, dy.shape[-1], dtype=dy.dtype, device=dy.device)
-        g.index_add_(0, ids, dy)
+        torch.ops.dtg.embedding_bwd_(g, ids.reshape(-1), dy2)
         return g
     if _fresh(param):
         mg.zero_()
-    mg.index_add_(0, ids, dy)
+    torch.ops.dtg.embedding_bwd_(mg, ids.reshape(-1), dy2)
     _mark(param)
     return None
 

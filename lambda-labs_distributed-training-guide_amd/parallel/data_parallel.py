@@ -41,14 +41,19 @@ class DataParallel:
     def __init__(self, model: nn.Module, mode: str = "ddp", group=None, tp_group=None,
                  bucket_mb: int = 256, broadcast_from_rank0: bool = True, state_dtype=torch.bfloat16,
                  master_weights: bool = False, overlap_param_gather: bool = True,
-                 overlap_optimizer: bool = False, grad_divisor: Optional[int] = None):
+                 overlap_optimizer: bool = False, grad_divisor: Optional[int] = None,
+                 force_collectives: bool = False):
         assert mode in ("single", "ddp", "zero")
         self.module = model
         self.group = group
         self.tp_group = tp_group
         self.world = comm.world(group) if mode != "single" and dist.is_initialized() else 1
         self.rank = comm.rank(group) if self.world > 1 else 0
-        self.mode = mode if self.world > 1 else "single"
+        # force_collectives: keep ddp/zero (and every RCCL call they make) even in a world of one,
+        # so the 1-GPU box exercises the async work objects, stream waits and in-place gathers of
+        # the multi-GPU path over a real RCCL communicator (tests/test_engines_rccl_gpu.py).
+        force = force_collectives and mode != "single" and dist.is_initialized()
+        self.mode = mode if (self.world > 1 or force) else "single"
         dev = next(model.parameters()).device
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         for n, p in named:
@@ -58,7 +63,7 @@ class DataParallel:
         self.params = rebind_parameters(model, self.space, copy_data=True, notify=self._on_grad)
         self._sync_enabled = True
         self._inflight = []
-        if self.world > 1 and broadcast_from_rank0:
+        if self.mode != "single" and broadcast_from_rank0:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             dist.broadcast(self.space.param_buf, src=src, group=group)
         # Optimizer state over what this rank updates.

@@ -128,7 +128,7 @@ class FullyShard:
                  device=None, reshard_after_forward: bool = True, cpu_offload: bool = False,
                  state_dtype=torch.bfloat16, init_fn: Optional[Callable] = None, seed: int = 0,
                  prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None, replicate_group=None,
-                 overlap_cpu_step: bool = True):
+                 overlap_cpu_step: bool = True, force_collectives: bool = False):
         self.module = model
         self.group = group
         # HYBRID_SHARD (ZeRO++-style): shard inside `group` (one node's xGMI island), replicate
@@ -140,6 +140,8 @@ class FullyShard:
         self.world = comm.world(group) if dist.is_initialized() else 1
         self.rank = comm.rank(group) if self.world > 1 else 0
         self.mode = "fsdp" if self.replicas == 1 else "hybrid"
+        # collectives even at world 1 (RCCL rehearsal of the multi-GPU path on one GPU)
+        self._coll = self.world > 1 or (force_collectives and dist.is_initialized())
         self.reshard_after_forward = reshard_after_forward
         self.cpu_offload = cpu_offload
         self.overlap_cpu_step = overlap_cpu_step
@@ -149,6 +151,8 @@ class FullyShard:
         self._cpu_pool = None
         self._cpu_futs = []
         self._bwd_stepped = False
+        self._bwd_snapshot = None
+        self._poisoned = False
         self.prefetch = prefetch
         self.max_inflight_rs = max_inflight_rs
         p0 = next(model.parameters())
@@ -217,7 +221,7 @@ class FullyShard:
                     mm._parameters[pn] = np_
                 new.append(np_)
             u.params = new
-            if self.world > 1 and all(p.device.type != "meta" for p in u.params_src):
+            if self._coll and all(p.device.type != "meta" for p in u.params_src):
                 # identical init on every rank is assumed; keep rank 0 authoritative (sync_module_states)
                 dist.broadcast(full, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
             my = full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel]
@@ -263,7 +267,7 @@ class FullyShard:
         if self.cpu_offload:
             shard = shard.to(self.device, non_blocking=True)
         with torch.autograd._unsafe_preserve_version_counter(u.full):
-            if self.world == 1:
+            if not self._coll:
                 u.full.copy_(shard)
                 u.gather_work = None
                 u.gathered = True
@@ -381,7 +385,7 @@ class FullyShard:
         first = self._first_micro
         direct = not (self.cpu_offload or not first)  # reduce-scatter straight into the grad shard
         out = gs if direct else torch.empty(u.shard_numel, dtype=self.dtype, device=self.device)
-        if self.world == 1:
+        if not self._coll:
             out.copy_(u.full_grad)
             work = None
         else:
@@ -444,19 +448,42 @@ class FullyShard:
             adamw_step_cpu, self.shard_params[sl], self.shard_grads[sl], self.exp_avg[sl], self.exp_avg_sq[sl],
             lr=lr, step=step, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, grad_scale=scale))
 
-    def backward(self, loss):
+    def backward(self, loss, last_microbatch: Optional[bool] = None):
+        """Backward of one micro-batch.  With CPU offload and `overlap_cpu_step`, the host AdamW
+        of each unit runs during the backward that is known to be the last micro-batch of the
+        step: `last_microbatch=True`, or None outside `no_sync()`.  Pass False (or use
+        `no_sync()`) for earlier micro-batches.  A second backward after an overlapped one
+        without step()/zero_grad() in between is an error (it would update twice)."""
+        if self._poisoned:
+            raise RuntimeError("FullyShard: a previous backward failed after host updates started; "
+                               "parameters are partially updated -- reload a checkpoint")
+        if self._bwd_stepped:
+            raise RuntimeError("FullyShard.backward: the previous backward already applied the optimizer "
+                               "update (overlap_cpu_step); call step()/zero_grad() first, or mark earlier "
+                               "micro-batches with no_sync() / last_microbatch=False")
+        final = (not self._in_no_sync) if last_microbatch is None else bool(last_microbatch)
         overlap = (self.cpu_offload and self.overlap_cpu_step and self._hparams is not None
-                   and self.replicas == 1 and not self._in_no_sync)
+                   and self.replicas == 1 and final)
         if overlap:  # the last micro-batch: its per-unit gradient shards are final on arrival
             scale = 1.0 / (self.world * self.replicas * (self.accum_count + 1))
             self._bwd_step = (self.step_count + 1, scale, self._hparams())
+        ok = False
         try:
             loss.backward()
             self.accum_count += 1
             self.finish_grad_sync()
+            ok = True
         finally:
-            self._bwd_step = None
+            snap, self._bwd_step = self._bwd_step, None
+            if not ok and self._cpu_futs:
+                # host updates of some units were submitted: let them finish, then refuse to
+                # step on a half-updated model (a retry would apply AdamW twice to those units)
+                try:
+                    self._join_host_steps()
+                finally:
+                    self._poisoned = True
         self._bwd_stepped = overlap
+        self._bwd_snapshot = snap if overlap else None
 
     def _join_host_steps(self):
         futs, self._cpu_futs = self._cpu_futs, []
@@ -465,6 +492,10 @@ class FullyShard:
 
     def zero_grad(self):
         self._join_host_steps()  # never let a host update race the next forward's shard reads
+        if self._bwd_stepped:
+            # the update already ran during backward (a skipped step() still counts as a step)
+            self._bwd_stepped = False
+            self.step_count += 1
         for u in self.all_units:
             reset_grad_state(u.params)
             u.pending = u.expected
@@ -473,11 +504,20 @@ class FullyShard:
 
     # ------------------------------------------------------------------ optimizer
     def step(self, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, grad_scale=None):
-        self.step_count += 1
+        if self._poisoned:
+            raise RuntimeError("FullyShard.step: a failed backward left units partially updated")
         if self._bwd_stepped:  # overlap_cpu_step: every unit was updated during backward
+            step, scale, hp = self._bwd_snapshot
+            if grad_scale is not None or tuple(hp) != (lr, beta1, beta2, eps, weight_decay):
+                raise RuntimeError("FullyShard.step: the update already ran during backward with "
+                                   f"{hp} and grad_scale={scale}; step() got different hyper-parameters "
+                                   f"{(lr, beta1, beta2, eps, weight_decay)} / grad_scale={grad_scale}. "
+                                   "Change them before backward(), or pass overlap_cpu_step=False")
+            self.step_count += 1
             self._bwd_stepped = False
             self._join_host_steps()
             return
+        self.step_count += 1
         if grad_scale is None:
             grad_scale = 1.0 / (self.world * self.replicas * max(1, self.accum_count))
         if self.replicas > 1:

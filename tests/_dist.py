@@ -13,7 +13,7 @@ def free_port():
         return s.getsockname()[1]
 
 
-def _entry(rank, world, port, fn, args, outdir):
+def _entry(rank, world, port, fn, args, outdir, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     # c10d's collective-consistency checks (every collective's op / shape / dtype is
@@ -28,7 +28,11 @@ def _entry(rank, world, port, fn, args, outdir):
     import torch.distributed as dist
 
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: one rank per device (the 1-GPU box runs world 1)
+        torch.cuda.set_device(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         res = fn(rank, world, *args)
         torch.save(res, os.path.join(outdir, f"r{rank}.pt"))
@@ -36,7 +40,8 @@ def _entry(rank, world, port, fn, args, outdir):
         dist.destroy_process_group()
 
 
-def run_distributed(fn, world, *args):
+def run_distributed(fn, world, *args, backend="gloo"):
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_entry, args=(world, free_port(), fn, args, d), nprocs=world, join=True, start_method="spawn")
+        mp.start_processes(_entry, args=(world, free_port(), fn, args, d, backend), nprocs=world, join=True,
+                           start_method="spawn")
         return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]

@@ -12,7 +12,8 @@ from _dist import free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--batch-size", "2", "--seq-len", "64",
-        "--tunableop", "off"]
+        "--tunableop", "off", "--fsdp-mem-model", "llama-tiny", "--fsdp-mem-batch", "2", "--fsdp-mem-seq", "64",
+        "--fsdp-mem-steps", "1", "--numel-to-wrap", "10000"]
 
 
 def _json_lines(out):
@@ -25,6 +26,9 @@ def _check(rec, n):
     assert rec["config"]["global_batch"] == 2 * n and rec["config"]["seq_len"] == 64
     assert rec["scaling"] == "weak" and rec["higher_is_better"] is True and rec["dtype"] == "bf16"
     assert rec["value"] > 0 and abs(rec["value"] - 2 * n * 64 * 2 / (rec["ms_per_step"] * 2 / 1000)) < 0.02 * rec["value"]
+    assert rec["world_size_seen_by_pg"] == n and len(rec["rank_devices"]) == n
+    assert rec["rank_ms_per_step"]["max"] >= rec["rank_ms_per_step"]["min"] > 0
+    assert rec["fsdp_mem"]["peak_gb_max_rank"] >= rec["fsdp_mem"]["valley_gb_max_rank"] >= 0
 
 
 @pytest.mark.slow
@@ -48,3 +52,25 @@ def test_bench_torchrun_two_ranks():
     assert len(recs) == 1, r.stdout  # rank 0 only
     _check(recs[0], 2)
     assert recs[0]["config"]["parallelism"] == "dp2-zero"
+
+
+@pytest.mark.slow
+def test_bench_self_launches_n_ranks():
+    """`python bench.py --gpus 2` with no launcher starts the 2 ranks itself (the driver's
+    N=1 command form must not silently measure one rank at N>1)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + ARGS,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    _check(recs[0], 2)
+    assert recs[0]["backend"] == "gloo"
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + ARGS,
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)

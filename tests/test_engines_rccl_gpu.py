@@ -1,0 +1,155 @@
+"""The multi-GPU engine paths over a REAL RCCL communicator on the 1-GPU box.
+
+RCCL refuses two ranks on one device, so the engines run in a world of one with
+`force_collectives=True`: DDP's async bucket all-reduce, ZeRO's reduce-scatter into the grad
+shard plus the in-place parameter all-gather left in flight into the next forward, and FSDP's
+per-unit all-gather / reduce-scatter with storage `resize_(0)` of gathered buffers all run
+through `ProcessGroupNCCL` work objects and their stream waits.  Results must be BIT-identical
+to the collective-free single-device engine.
+
+Delay injection: every async collective is issued from a side stream that first spins for
+~`SPIN` GPU cycles (`torch.cuda._sleep`).  A consumer that reads a collective's output without
+waiting on its work object then reads stale memory and the bitwise comparison fails."""
+import pytest
+import torch
+
+from _dist import run_distributed
+
+pytestmark = pytest.mark.gpu
+MODEL = "llama-tiny-d128"
+STEPS = 3
+SPIN = 20_000_000  # ~10 ms at ~2 GHz
+
+
+def _batches(vocab):
+    g = torch.Generator().manual_seed(0)
+    return [torch.randint(0, vocab, (4, 128), generator=g) for _ in range(STEPS)]
+
+
+def _install_delay():
+    import torch.distributed as dist
+
+    side = torch.cuda.Stream()
+
+    def wrap(fn):
+        def delayed(*a, **kw):
+            if not kw.get("async_op", False):
+                return fn(*a, **kw)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                torch.cuda._sleep(SPIN)
+                work = fn(*a, **kw)  # RCCL's stream waits for `side`, i.e. for the spin
+            return work
+
+        return delayed
+
+    for name in ("all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor"):
+        setattr(dist, name, wrap(getattr(dist, name)))
+
+
+def _train(kind, force, delay, accum=1):
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    if delay:
+        _install_delay()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    cfg = resolve_config(MODEL)
+    torch.manual_seed(0)
+    model = build_model(cfg, device=dev)
+    if kind == "fsdp":
+        from dtg.parallel.fsdp import FullyShard
+
+        eng = FullyShard(model, device=dev, force_collectives=force)
+    else:
+        eng = DataParallel(model, mode=kind, bucket_mb=1, force_collectives=force)
+    opt = FlatAdamW(eng, lr=1e-3)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))
+    losses = []
+    for ids in _batches(cfg.vocab_size):
+        ids = ids.to(dev)
+        opt.zero_grad()
+        for j, mb in enumerate(ids.chunk(accum)):
+            ctx = eng.no_sync() if j < accum - 1 else torch.enable_grad()
+            with ctx:
+                out = model(input_ids=mb, labels=mb)
+                eng.backward(out.loss)
+        opt.step()
+        sched.step()
+        losses.append(out.loss.item())
+    mode = eng.mode
+    if kind == "fsdp":
+        sd = eng.full_state_dict(rank0_only=False)
+        return {k: v.cpu() for k, v in sd.items()}, losses, mode
+    eng.wait_param_gather() if hasattr(eng, "wait_param_gather") else None
+    torch.cuda.synchronize()
+    return {n: p.detach().cpu().clone() for n, p in model.named_parameters()}, losses, mode
+
+
+def _worker(rank, world, kind, delay, accum):
+    return _train(kind, True, delay, accum)
+
+
+def _single(kind, accum):
+    torch.cuda.set_device(0)
+    return _train("single" if kind != "fsdp" else "fsdp", False, False, accum)
+
+
+@pytest.mark.parametrize("kind", ["ddp", "zero", "fsdp"])
+@pytest.mark.parametrize("delay", [False, True])
+def test_rccl_world1_engine_bit_identical(cuda, kind, delay):
+    ref, ref_losses, ref_mode = _single(kind, 1)
+    (params, losses, mode), = run_distributed(_worker, 1, kind, delay, 1, backend="nccl")
+    assert mode == kind and ref_mode in ("single", "fsdp"), (mode, ref_mode)
+    assert losses == ref_losses
+    for n, v in ref.items():
+        assert torch.equal(params[n], v), (kind, delay, n)
+
+
+@pytest.mark.parametrize("kind", ["ddp", "zero"])
+def test_rccl_world1_grad_accumulation(cuda, kind):
+    ref, ref_losses, _ = _single(kind, 2)
+    (params, losses, mode), = run_distributed(_worker, 1, kind, True, 2, backend="nccl")
+    assert mode == kind and losses == ref_losses
+    for n, v in ref.items():
+        assert torch.equal(params[n], v), (kind, n)
+
+
+def _offload_worker(rank, world, overlap, accum):
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    cfg = resolve_config(MODEL)
+    torch.manual_seed(0)
+    model = build_model(cfg, device=dev)
+    eng = FullyShard(model, device=dev, cpu_offload=True, overlap_cpu_step=overlap)
+    opt = FlatAdamW(eng, lr=1e-3)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))  # lr changes every step
+    stepped = []
+    for ids in _batches(cfg.vocab_size):
+        per = ids.shape[0] // world
+        mine = ids[rank * per:(rank + 1) * per].to(dev)
+        opt.zero_grad()
+        for j, mb in enumerate(mine.chunk(accum)):
+            ctx = eng.no_sync() if j < accum - 1 else torch.enable_grad()
+            with ctx:
+                eng.backward(model(input_ids=mb, labels=mb).loss)
+        stepped.append(eng._bwd_stepped)
+        opt.step()
+        sched.step()
+    return {k: v.cpu() for k, v in eng.full_state_dict(rank0_only=False).items()}, stepped
+
+
+@pytest.mark.parametrize("accum", [1, 2])
+def test_fsdp_cpu_offload_overlap_bit_identical_on_gpu(cuda, accum):
+    """pinned host shards, non_blocking H2D gathers, reduce-scatter -> D2H and the
+    host-AdamW worker thread running while GPU streams are live: overlapped == post-backward."""
+    on = run_distributed(_offload_worker, 2, True, accum)
+    off = run_distributed(_offload_worker, 2, False, accum)
+    for r in range(2):
+        assert all(on[r][1]) and not any(off[r][1])
+        for n, t in off[r][0].items():
+            assert torch.equal(on[r][0][n], t), (r, n)

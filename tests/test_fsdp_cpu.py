@@ -171,3 +171,38 @@ def test_fsdp_grad_accumulation_matches_full_batch(offload):
     two = run_distributed(_offload_train, 2, batches, False, 2, offload)
     for n, t in one[0][0].items():
         torch.testing.assert_close(two[0][0][n], t, **TOL, msg=n)  # pre-fix error: ~2 x lr = 2e-2
+
+
+def test_fsdp_overlapped_host_step_guards_misuse():
+    """with overlap_cpu_step the update runs inside the final backward, so (a) a second
+    backward without step()/no_sync() must raise instead of updating twice, (b) step() with
+    hyper-parameters that differ from the ones the in-backward update used must raise, and
+    (c) last_microbatch=False accumulates with no host update."""
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+
+    torch.manual_seed(0)
+    model = build_model("llama-tiny", device="cpu", dtype=torch.float32)
+    eng = FullyShard(model, cpu_offload=True, device="cpu", overlap_cpu_step=True)
+    opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
+    ids = torch.randint(0, 512, (2, 16), generator=torch.Generator().manual_seed(0))
+    opt.zero_grad()
+    eng.backward(model(input_ids=ids, labels=ids).loss)
+    assert eng._bwd_stepped
+    with pytest.raises(RuntimeError, match="already applied"):
+        eng.backward(model(input_ids=ids, labels=ids).loss)
+    opt.param_groups[0]["lr"] = 5e-3
+    with pytest.raises(RuntimeError, match="different hyper-parameters"):
+        opt.step()
+    opt.param_groups[0]["lr"] = 1e-2
+    opt.step()
+    assert eng.step_count == 1 and not eng._bwd_stepped
+    opt.zero_grad()
+    before = eng.shard_params.clone()
+    eng.backward(model(input_ids=ids, labels=ids).loss, last_microbatch=False)
+    assert not eng._bwd_stepped and torch.equal(before, eng.shard_params)
+    eng.backward(model(input_ids=ids, labels=ids).loss)  # final micro-batch: overlapped update
+    assert eng._bwd_stepped and not torch.equal(before, eng.shard_params)
+    opt.step()
+    assert eng.step_count == 2

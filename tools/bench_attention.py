@@ -30,8 +30,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="llama8b", choices=list(SHAPES))
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sweep", action="store_true",
+                    help="constant 16k tokens, S = 512..8192, causal and non-causal (Hq32/Hkv8/D128)")
     a = ap.parse_args()
-    c = SHAPES[a.shape]
+    if a.sweep:
+        for S in (512, 1024, 2048, 4096, 8192):
+            for causal in (True, False):
+                run(a, dict(B=16384 // S, S=S, hq=32, hkv=8, d=128, docs=None), f"sweep_S{S}", causal)
+        return
+    run(a, SHAPES[a.shape], a.shape, True)
+
+
+def run(a, c, name, causal):
     dev = torch.device("cuda:0")
     B, S, hq, hkv, d = c["B"], c["S"], c["hq"], c["hkv"], c["d"]
     T = B * S
@@ -47,7 +57,7 @@ def main():
         causal_flops = sum(l * l / 2 for l in lens) * 4 * d * hq
     else:
         cu = torch.arange(0, T + 1, S, dtype=torch.int32)
-        causal_flops = B * S * S / 2 * 4 * d * hq
+        causal_flops = B * S * S / (2 if causal else 1) * 4 * d * hq
     cu = cu.to(dev)
     maxlen = int((cu[1:] - cu[:-1]).max())
     qkv = torch.randn(T, (hq + 2 * hkv) * d, device=dev).bfloat16()
@@ -57,7 +67,7 @@ def main():
     do = torch.randn(T, hq, d, device=dev).bfloat16()
     ops = torch.ops.dtg
     scale = 1 / math.sqrt(d)
-    o, lse = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, True)
+    o, lse = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal)
 
     def timeit(fn):
         for _ in range(3):
@@ -69,9 +79,9 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / a.iters
 
-    tf = timeit(lambda: ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, True))
-    tb = timeit(lambda: ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, True))
-    rec = {"shape": a.shape, "fwd_ms": tf * 1e3, "bwd_ms": tb * 1e3, "fwd_TFLOPs": causal_flops / tf / 1e12,
+    tf = timeit(lambda: ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal))
+    tb = timeit(lambda: ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, causal))
+    rec = {"shape": name, "causal": causal, "fwd_ms": tf * 1e3, "bwd_ms": tb * 1e3, "fwd_TFLOPs": causal_flops / tf / 1e12,
            "bwd_TFLOPs": 2.5 * causal_flops / tb / 1e12, "bwd_variant": os.environ.get("DTG_FA_BWD", "split"), "occ": os.environ.get("DTG_FA_OCC", "1")}
     print(json.dumps(rec), flush=True)
 
