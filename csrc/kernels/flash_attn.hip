@@ -174,6 +174,36 @@ __device__ __forceinline__ int grid_head(int x, int hq, int hkv) {
   return (x % hkv) * group + x / hkv;
 }
 
+// Row-per-lane epilogue of a transposed 32x32 accumulator (lane = output row, registers =
+// columns 32d + 8g + 4h + e) widened per CDNA guide T21: v_permlane32_swap pairs column groups
+// (2j, 2j+1) so that lanes 0-31 hold 16 contiguous bytes of group 2j and lanes 32-63 those of
+// group 2j+1 -- 8 dwordx4 stores per lane instead of 16 dwordx2 (the store tail is issue-bound).
+// Must run with all 64 lanes active; `ok` only masks the stores.
+template <int ND>
+__device__ __forceinline__ void store_rows_wide(const f32x16* acc, float scale, uint16_t* row, bool ok) {
+  const int h = (threadIdx.x & 63) >> 5;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint32_t w[4];  // packed bf16 pairs: w[0..1] group 2j, w[2..3] group 2j+1
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int base = 4 * (2 * j + u);
+        w[2 * u + 0] = (uint32_t)f2bf(acc[d][base + 0] * scale) | ((uint32_t)f2bf(acc[d][base + 1] * scale) << 16);
+        w[2 * u + 1] = (uint32_t)f2bf(acc[d][base + 2] * scale) | ((uint32_t)f2bf(acc[d][base + 3] * scale) << 16);
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const auto r = __builtin_amdgcn_permlane32_swap(w[x], w[2 + x], false, false);
+        w[x] = r[0];
+        w[2 + x] = r[1];
+      }
+      if (ok) *reinterpret_cast<uint4*>(row + 32 * d + 16 * j + 8 * h) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
 struct FwdParams {
   const uint16_t *q, *k, *v;
   int64_t sq, sk, sv;  // token strides (elements)
@@ -183,12 +213,25 @@ struct FwdParams {
   int64_t T;
   int hq, hkv;
   float c2;  // softmax scale * log2(e)
+  long long* stamps;  // diagnostic path only (flash_attn_fwd_stamped): 6 words per workgroup
 };
 
-constexpr int kFwdBQ = 128;  // query rows per workgroup (4 waves x 32)
+// In-kernel timeline stamps (CDNA guide §7 'In-kernel stamps'): constant-rate 100 MHz clock,
+// one lane per workgroup, plus the hardware wave id / XCC id of the workgroup's wave 0.
+__device__ __forceinline__ void fa_stamp(long long* st, int slot, int k) {
+  if (st != nullptr && threadIdx.x == 0) {
+    st[slot * 6 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (k == 0) {
+      st[slot * 6 + 4] = (long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_REG_HW_ID
+      st[slot * 6 + 5] = (long long)__builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+    }
+  }
+}
+
+constexpr int kFwdBQ = 128;  // query rows per work item (4 waves x 32)
 constexpr int kFwdBK = 64;   // keys per K/V tile
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool WIDE, bool QLDS>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int TILE = kFwdBK * RB;
@@ -196,6 +239,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   constexpr int ND = D / 32;  // 32-wide d tiles of the output
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1]
 
+  fa_stamp(P.stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), 0);
   const int seq = blockIdx.y, head = grid_head(blockIdx.x, P.hq, P.hkv);
   const int s0 = P.cu[seq];
   const int seqlen = P.cu[seq + 1] - s0;
@@ -208,7 +252,12 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   const int qrow = q0 + 32 * w + r;  // this lane's query (sequence-relative)
 
   bf16x8 qf[NC];  // Q^T fragments for all k-steps
-  load_row_frags<NC>(P.q + (int64_t)(s0 + min(qrow, seqlen - 1)) * P.sq + (int64_t)head * D, qrow < seqlen, h, qf);
+  // QLDS: Q rows arrive as whole 256-B lines (the K/V stager's coalesced buffer loads) and are
+  // turned into fragments through LDS, instead of fragment-shaped loads (32 rows x 32 B per
+  // instruction) straight to registers.
+  Stager<kFwdBQ, D, 256> sq;
+  if constexpr (QLDS) sq.load(P.q + (int64_t)(s0 + q0) * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
+  else load_row_frags<NC>(P.q + (int64_t)(s0 + min(qrow, seqlen - 1)) * P.sq + (int64_t)head * D, qrow < seqlen, h, qf);
   int koff[NC], toa[ND], tob[ND];
 #pragma unroll
   for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
@@ -228,9 +277,16 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   Stager<kFwdBK, D, 256> sk, sv;
   sk.load(kbase, P.sk, seqlen);
   sv.load(vbase, P.sv, seqlen);
+  if constexpr (QLDS) sq.store(smem + 2 * TILE);  // the second K/V buffer is free until tile 0 ends
   sk.store(smem);
   sv.store(smem + TILE);
   __syncthreads();
+  if constexpr (QLDS) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) qf[c] = lds_frag(smem + 2 * TILE + 32 * w * RB + koff[c]);
+    __syncthreads();  // every wave holds its Q before tile 0 restages that buffer
+  }
+  fa_stamp(P.stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), 1);
 
   const int wave_q0 = q0 + 32 * w, wave_qmax = wave_q0 + 31;
   // Tile loop unrolled by two so the double-buffer offsets are compile-time immediates.
@@ -324,11 +380,14 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
     tile_step(t + 1, std::integral_constant<int, 1>{});
   }
   if (t < ntiles) tile_step(t, std::integral_constant<int, 0>{});
+  fa_stamp(P.stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), 2);
 
   const float lt = l + __shfl_xor(l, 32, 64);
-  if (qrow < seqlen) {
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    uint16_t* op = P.o + ((int64_t)(s0 + qrow) * P.hq + head) * D;
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  uint16_t* op = P.o + ((int64_t)(s0 + min(qrow, seqlen - 1)) * P.hq + head) * D;
+  if constexpr (WIDE) {
+    store_rows_wide<ND>(acc, inv, op, qrow < seqlen);
+  } else if (qrow < seqlen) {
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
 #pragma unroll
@@ -341,7 +400,13 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
         *reinterpret_cast<ushort4*>(op + 32 * d + 8 * g4 + 4 * h) = v;
       }
     }
-    if (h == 0) P.lse[(int64_t)head * P.T + s0 + qrow] = (lt > 0.f) ? (m + log2f(lt)) * kLn2 : -INFINITY;
+  }
+  if (qrow < seqlen && h == 0)
+    P.lse[(int64_t)head * P.T + s0 + qrow] = (lt > 0.f) ? (m + log2f(lt)) * kLn2 : -INFINITY;
+  if (P.stamps != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    fa_stamp(P.stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), 3);
   }
 }
 
@@ -737,9 +802,10 @@ static void check_qkv(const at::Tensor& t, const char* name, int64_t heads, int6
             name, " must be [T, H, D] with contiguous heads and 16-B aligned token stride");
 }
 
-std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k,
-                                                  const at::Tensor& v, const at::Tensor& cu_seqlens,
-                                                  int64_t max_seqlen, double scale, bool causal) {
+static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& q, const at::Tensor& k,
+                                                              const at::Tensor& v, const at::Tensor& cu_seqlens,
+                                                              int64_t max_seqlen, double scale, bool causal,
+                                                              at::Tensor* stamps) {
   const int64_t T = q.size(0), hq = q.size(1), D = q.size(2), hkv = k.size(1);
   check_qkv(q, "q", hq, D);
   check_qkv(k, "k", hkv, D);
@@ -754,20 +820,51 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   auto lse = at::empty({hq, T}, q.options().dtype(at::kFloat));
   const int nseq = cu_seqlens.numel() - 1;
   if (T == 0 || nseq <= 0 || max_seqlen <= 0) return {o, lse};
+  DTG_CHECK(nseq <= 65535, "flash_attn: at most 65535 sequences per call");
+  const int nqb = (int)((max_seqlen + fa::kFwdBQ - 1) / fa::kFwdBQ);
   fa::FwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), q.stride(0), k.stride(0), v.stride(0),
                   bf16_mut(o), lse.data_ptr<float>(), cu_seqlens.data_ptr<int>(), T, (int)hq, (int)hkv,
-                  (float)(scale * fa::kLog2e)};
-  DTG_CHECK(nseq <= 65535, "flash_attn: at most 65535 sequences per call");
-  dim3 grid(hq, nseq, (max_seqlen + fa::kFwdBQ - 1) / fa::kFwdBQ);
+                  (float)(scale * fa::kLog2e), nullptr};
+  dim3 grid(hq, nseq, nqb);
+  if (stamps != nullptr) {
+    *stamps = at::zeros({(int64_t)grid.x * grid.y * grid.z, 6}, q.options().dtype(at::kLong));
+    P.stamps = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
+  }
+  // DTG_FA_FWD=narrow: the round-1 row-per-lane dwordx2 epilogue (read per call: same-process A/B)
+  // DTG_FA_FWD=wide: row-per-lane Q fragment loads instead of the LDS-staged Q
+  const char* variant = std::getenv("DTG_FA_FWD");
+  const bool wide = !(variant != nullptr && variant[0] == 'n');
+  const bool qlds = !(variant != nullptr && (variant[0] == 'n' || variant[0] == 'w'));
   const size_t lds = 4 * fa::kFwdBK * D * 2;
-#define DTG_FWD(DD, C)                                                                    \
-  do { set_lds_limit((const void*)&fa::fwd_kernel<DD, C>, lds);                              \
-       hipLaunchKernelGGL((fa::fwd_kernel<DD, C>), grid, dim3(256), lds, stream(), P); } while (0)
-  if (D == 128) { if (causal) DTG_FWD(128, true); else DTG_FWD(128, false); }
-  else { if (causal) DTG_FWD(64, true); else DTG_FWD(64, false); }
+#define DTG_FWD(DD, C, W, Q)                                                              \
+  do { set_lds_limit((const void*)&fa::fwd_kernel<DD, C, W, Q>, lds);                        \
+       hipLaunchKernelGGL((fa::fwd_kernel<DD, C, W, Q>), grid, dim3(256), lds, stream(), P); } while (0)
+#define DTG_FWD_W(DD, C)                                                                  \
+  do { if (!wide) DTG_FWD(DD, C, false, false); else if (!qlds) DTG_FWD(DD, C, true, false);   \
+       else DTG_FWD(DD, C, true, true); } while (0)
+  if (D == 128) { if (causal) DTG_FWD_W(128, true); else DTG_FWD_W(128, false); }
+  else { if (causal) DTG_FWD_W(64, true); else DTG_FWD_W(64, false); }
+#undef DTG_FWD_W
 #undef DTG_FWD
   DTG_LAUNCH_CHECK();
   return {o, lse};
+}
+
+std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k,
+                                                  const at::Tensor& v, const at::Tensor& cu_seqlens,
+                                                  int64_t max_seqlen, double scale, bool causal) {
+  return flash_attn_fwd_impl(q, k, v, cu_seqlens, max_seqlen, scale, causal, nullptr);
+}
+
+// Diagnostic: the same launch with per-workgroup timeline stamps [start, prologue done, tile
+// loop done, stores complete, HW_ID, XCC_ID] (tools/fa_timeline.py).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_fwd_stamped(const at::Tensor& q, const at::Tensor& k,
+                                                                      const at::Tensor& v,
+                                                                      const at::Tensor& cu_seqlens,
+                                                                      int64_t max_seqlen, double scale, bool causal) {
+  at::Tensor st;
+  auto [o, lse] = flash_attn_fwd_impl(q, k, v, cu_seqlens, max_seqlen, scale, causal, &st);
+  return {o, lse, st};
 }
 
 // Shared backward driver: outputs are [T, H, D] views (contiguous heads, any token stride).
@@ -883,6 +980,7 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& qkv, int
 
 TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
   m.impl("flash_attn_fwd", &flash_attn_fwd);
+  m.impl("flash_attn_fwd_stamped", &flash_attn_fwd_stamped);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("flash_attn_bwd_qkv", &flash_attn_bwd_qkv);
 }

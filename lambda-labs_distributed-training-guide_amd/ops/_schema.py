@@ -31,6 +31,8 @@ _DEFS = [
     "Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> Tensor",
     "transpose2d(Tensor x) -> Tensor",
     "embedding_bwd_(Tensor(a!) out, Tensor ids, Tensor dy) -> ()",
+    "flash_attn_fwd_stamped(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
+    "bool causal) -> (Tensor, Tensor, Tensor)",
 ]
 
 for _d in _DEFS:

@@ -7,13 +7,15 @@ Directory layout under `{save_dir}/{experiment_name}/` follows the reference per
                       crashed on resume)
   * sharded (04-07):  checkpoint/ (.metadata + one file per rank), lr_scheduler.pt, state.json, rng.pt
 
-Sharded format (a DCP-like layout, resharding-capable): every rank writes
-`checkpoint/__{rank}_0.distcp` holding, for each parameter slice it owns, the parameter values
-and both AdamW moments (plain tensors: loadable with `torch.load(weights_only=True)`), and rank 0
-writes `checkpoint/.metadata` (JSON) with every file's slice index.  On load each rank copies
-the overlap of every stored slice with the slices it owns now, so a checkpoint written by W
-ranks loads on W' ranks (FSDP, ZeRO and DDP layouts alike); TP shards are matched by tp rank.
-Barriers bracket every save (reference C2) so no rank reads a half-written directory.
+Sharded format `dtg-sharded-v2` (this framework's own; not torch DCP, whose file names it does
+not borrow): every rank writes `checkpoint/shard_rNNNNN.pt` holding, for each parameter slice it
+owns, the parameter values and both AdamW moments (plain tensors: loadable with
+`torch.load(weights_only=True)`), and rank 0 writes `checkpoint/index.json` with every slice's
+position in GLOBAL parameter coordinates.  On load each rank copies the overlap of every stored
+slice with the slices it owns now, so a checkpoint written on (W data-parallel x a tensor-
+parallel) ranks loads on (W' x b) -- FSDP, ZeRO and DDP layouts alike -- and a load that would
+leave any owned element unwritten fails.  Barriers bracket every save (reference C2) so no rank
+reads a half-written directory.
 """
 from __future__ import annotations
 
@@ -87,26 +89,128 @@ def load_rng(path, local_rank: int = 0):
 
 
 # ------------------------------------------------------------------------------ sharded
-def _tp_rank(engine):
-    tp = getattr(engine.module, "tp", None)
-    return (tp.rank, tp.size) if tp is not None and tp.enabled else (0, 1)
+# Every stored slice is described in GLOBAL (un-tensor-parallel) parameter coordinates: a
+# rank's TP-local flat range is cut into rectangles (global row 0, rows, global col 0, cols,
+# offset in the slice's flat data).  Loading intersects the rectangles a rank owns NOW (its own
+# TP degree and data-parallel sharding) with the stored ones, so one checkpoint loads on any
+# (dp, tp) layout: W -> W' data-parallel ranks and TP a -> TP b, including TP -> no TP
+# (reference: DCP over DTensor modules reshards on load, 06-tensor-parallel/train_llm.py:177-190,
+# 283-295).  Every owned element must be covered exactly, or the load fails.
+FORMAT = "dtg-sharded-v2"
+INDEX = "index.json"
 
 
-def snapshot_sharded(engine):
+def _shard_file(rank: int) -> str:
+    return f"shard_r{rank:05d}.pt"
+
+
+def param_kind(name: str) -> str:
+    """How the tensor-parallel plan (parallel/tensor_parallel.py) splits a Llama parameter."""
+    if name.endswith("self_attn.qkv_proj.weight"):
+        return "qkv"
+    if name.endswith("mlp.gate_up_proj.weight"):
+        return "gate_up"
+    if name.endswith("self_attn.o_proj.weight") or name.endswith("mlp.down_proj.weight"):
+        return "col"
+    if name in ("embed_tokens.weight", "lm_head.weight"):
+        return "row"
+    return "rep"
+
+
+class _TPGeom:
+    def __init__(self, engine):
+        tp = getattr(engine.module, "tp", None)
+        self.rank, self.size = (tp.rank, tp.size) if tp is not None and tp.enabled else (0, 1)
+        cfg = getattr(engine.module, "config", None)
+        self.cfg = cfg
+
+    def blocks(self, kind, rows_local):
+        """[(local row start, rows, global row start)] of the row-sharded blocks of a param."""
+        r, n = self.rank, self.size
+        if kind == "qkv" and n > 1:
+            d, nq, nkv = self.cfg.head_dim, self.cfg.num_attention_heads, self.cfg.num_key_value_heads
+            sizes_l = [nq // n * d, nkv // n * d, nkv // n * d]
+            gstart = [0, nq * d, (nq + nkv) * d]
+        elif kind == "gate_up" and n > 1:
+            sizes_l = [rows_local // 2, rows_local // 2]
+            gstart = [0, rows_local // 2 * n]
+        elif kind in ("row", "qkv", "gate_up") and n > 1:
+            sizes_l, gstart = [rows_local], [0]
+        else:
+            return [(0, rows_local, 0)]
+        out, lo = [], 0
+        for sz, g in zip(sizes_l, gstart):
+            out.append((lo, sz, g + r * sz))
+            lo += sz
+        return out
+
+    def global_shape(self, kind, local_shape):
+        R, C = (local_shape[0], int(np.prod(local_shape[1:]))) if len(local_shape) > 1 else (1, local_shape[0])
+        if self.size == 1 or kind == "rep":
+            return [R, C]
+        if kind == "col":
+            return [R, C * self.size]
+        return [R * self.size, C]
+
+    def rects(self, name, local_shape, start, n):
+        """Global rectangles [r0, nr, c0, nc, off] of the local flat range [start, start + n)."""
+        kind = param_kind(name) if self.size > 1 else "rep"
+        R, C = (local_shape[0], int(np.prod(local_shape[1:]))) if len(local_shape) > 1 else (1, local_shape[0])
+        gc0 = self.rank * C if kind == "col" else 0
+        blocks = self.blocks(kind, R)
+
+        def grow(j):
+            for lo, sz, g in blocks:
+                if lo <= j < lo + sz:
+                    return g + (j - lo), lo + sz
+            raise AssertionError((name, j))
+
+        out, pos, end = [], start, start + n
+        while pos < end:
+            j, c = divmod(pos, C)
+            if c != 0 or end - pos < C:  # partial row
+                nc = min(C - c, end - pos)
+                g, _ = grow(j)
+                out.append([g, 1, gc0 + c, nc, pos - start])
+                pos += nc
+                continue
+            j_end = j + (end - pos) // C
+            while j < j_end:
+                g, blk_end = grow(j)
+                j_stop = min(j_end, blk_end)
+                out.append([g, j_stop - j, gc0, C, pos - start])
+                pos += (j_stop - j) * C
+                j = j_stop
+        return out
+
+
+def _replicated_engine(engine) -> bool:
+    return getattr(engine, "mode", "fsdp") in ("single", "ddp")
+
+
+def snapshot_sharded(engine, global_step=None):
     """Collective: copy this rank's parameter + AdamW-moment slices to host memory and gather
     the slice index of every rank.  Returns (tensors, entry, metadata-or-None) for
-    write_sharded; after it returns the device state may change (async checkpointing)."""
+    write_sharded; after it returns the device state may change (async checkpointing).
+
+    Replicated copies are written once: with a replicated engine (DDP / single) only the first
+    data-parallel rank of each TP group writes, and TP-replicated parameters (norms) only by
+    TP rank 0."""
     rank, world = get_rank(), get_world_size()
+    geo = _TPGeom(engine)
+    shapes_local = {n: list(p.shape) for n, p in engine.module.named_parameters()}
+    write = not (_replicated_engine(engine) and getattr(engine, "rank", 0) != 0)
     pieces = engine.ckpt_pieces()
     tensors, index = {}, []
     for j, (name, start, n, pview, sidx) in enumerate(pieces):
-        tensors[f"p{j}"] = pview.detach().reshape(-1).to("cpu", copy=True)
-        tensors[f"m{j}"] = engine.exp_avg[sidx:sidx + n].to("cpu", copy=True)
-        tensors[f"v{j}"] = engine.exp_avg_sq[sidx:sidx + n].to("cpu", copy=True)
-        index.append([name, int(start), int(n)])
-    tp_rank, tp_size = _tp_rank(engine)
-    fname = f"__{rank}_0.distcp"
-    entry = {"file": fname, "rank": rank, "tp_rank": tp_rank, "index": index}
+        if not write or (geo.size > 1 and geo.rank != 0 and param_kind(name) == "rep"):
+            continue
+        k = len(index)
+        tensors[f"p{k}"] = pview.detach().reshape(-1).to("cpu", copy=True)
+        tensors[f"m{k}"] = engine.exp_avg[sidx:sidx + n].to("cpu", copy=True)
+        tensors[f"v{k}"] = engine.exp_avg_sq[sidx:sidx + n].to("cpu", copy=True)
+        index.append([name, int(n), geo.rects(name, shapes_local[name], int(start), int(n))])
+    entry = {"file": _shard_file(rank), "rank": rank, "tp_rank": geo.rank, "index": index}
     if dist.is_initialized() and world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, entry)
@@ -114,9 +218,10 @@ def snapshot_sharded(engine):
         gathered = [entry]
     meta = None
     if rank == 0:
-        shapes = {n: list(p.shape) for n, p in engine.module.named_parameters()}
-        meta = {"world_size": world, "tp_size": tp_size, "step": int(engine.step_count), "files": gathered,
-                "param_shapes_tp_local": shapes, "format": "dtg-sharded-v1"}
+        gshapes = {n: geo.global_shape(param_kind(n) if geo.size > 1 else "rep", sh) for n, sh in shapes_local.items()}
+        meta = {"format": FORMAT, "world_size": world, "tp_size": geo.size, "step": int(engine.step_count),
+                "global_step": global_step, "param_shapes_global": gshapes,
+                "files": [f for f in gathered if f["index"]]}
     return tensors, entry, meta
 
 
@@ -124,55 +229,84 @@ def write_sharded(ckpt_dir, tensors, entry, meta):
     """Local file writes only (no collectives): safe on a background thread."""
     ckpt_dir = Path(ckpt_dir)
     ckpt_dir.mkdir(parents=True, exist_ok=True)
-    torch.save(tensors, ckpt_dir / entry["file"])
+    if entry["index"]:
+        torch.save(tensors, ckpt_dir / entry["file"])
     if meta is not None:
-        with open(ckpt_dir / ".metadata", "w") as fp:
+        with open(ckpt_dir / INDEX, "w") as fp:
             json.dump(meta, fp)
 
 
-def save_sharded(ckpt_dir, engine):
-    """All ranks: write this rank's parameter + optimizer-state slices; rank 0 writes metadata."""
+def save_sharded(ckpt_dir, engine, global_step=None):
+    """All ranks: write this rank's parameter + optimizer-state slices; rank 0 writes the index."""
     ckpt_dir = Path(ckpt_dir)
     barrier()
     if get_rank() == 0:
         ckpt_dir.mkdir(parents=True, exist_ok=True)
     barrier()
-    write_sharded(ckpt_dir, *snapshot_sharded(engine))
+    write_sharded(ckpt_dir, *snapshot_sharded(engine, global_step))
     barrier()
+
+
+def read_index(ckpt_dir):
+    path = Path(ckpt_dir) / INDEX
+    if not path.exists():
+        raise FileNotFoundError(f"{ckpt_dir}: no {INDEX} (not a {FORMAT} checkpoint)")
+    with open(path) as fp:
+        meta = json.load(fp)
+    if meta.get("format") != FORMAT:
+        raise ValueError(f"{path}: format {meta.get('format')!r}, expected {FORMAT!r}")
+    return meta
 
 
 @torch.no_grad()
 def load_sharded(ckpt_dir, engine, load_optimizer: bool = True):
+    """Fill this rank's owned parameter (and AdamW-moment) slices from a sharded checkpoint
+    written on any data-parallel world size and any tensor-parallel degree.  Raises if a
+    parameter is missing, its global shape differs, or any owned element is not covered."""
     ckpt_dir = Path(ckpt_dir)
-    with open(ckpt_dir / ".metadata") as fp:
-        meta = json.load(fp)
-    tp_rank, tp_size = _tp_rank(engine)
-    assert meta.get("tp_size", 1) == tp_size, "checkpoint tensor-parallel degree differs from the run's"
-    # stored slices by parameter name: (file, key index, start, n)
-    stored = {}
+    meta = read_index(ckpt_dir)
+    geo = _TPGeom(engine)
+    shapes_local = {n: list(p.shape) for n, p in engine.module.named_parameters()}
+    gshapes = meta["param_shapes_global"]
+    for name, sh in shapes_local.items():
+        mine = geo.global_shape(param_kind(name) if geo.size > 1 else "rep", sh)
+        if name not in gshapes:
+            raise KeyError(f"checkpoint {ckpt_dir} has no parameter {name!r}")
+        if list(gshapes[name]) != mine:
+            raise ValueError(f"{name}: checkpoint global shape {gshapes[name]} != model's {mine}")
+    stored = {}  # name -> [(file, key, rect)]
     for f in meta["files"]:
-        if f.get("tp_rank", 0) != tp_rank:
-            continue
-        for j, (name, start, n) in enumerate(f["index"]):
-            stored.setdefault(name, []).append((f["file"], j, start, n))
+        for k, (name, n, rects) in enumerate(f["index"]):
+            for rc in rects:
+                stored.setdefault(name, []).append((f["file"], k, rc))
     cache = {}
 
     def get(fname):
         if fname not in cache:
+            if not (ckpt_dir / fname).exists():
+                raise FileNotFoundError(f"checkpoint shard {ckpt_dir / fname} is missing")
             cache[fname] = torch.load(ckpt_dir / fname, weights_only=True, mmap=True)
         return cache[fname]
 
     for name, start, n, pview, sidx in engine.ckpt_pieces():
-        flat = pview.reshape(-1)
-        for fname, j, s2, n2 in stored.get(name, []):
-            lo, hi = max(start, s2), min(start + n, s2 + n2)
-            if lo >= hi:
-                continue
-            t = get(fname)
-            flat[lo - start:hi - start].copy_(t[f"p{j}"][lo - s2:hi - s2])
-            if load_optimizer:
-                engine.exp_avg[sidx + lo - start:sidx + hi - start].copy_(t[f"m{j}"][lo - s2:hi - s2])
-                engine.exp_avg_sq[sidx + lo - start:sidx + hi - start].copy_(t[f"v{j}"][lo - s2:hi - s2])
+        dsts = [pview.reshape(-1)]
+        if load_optimizer:
+            dsts += [engine.exp_avg[sidx:sidx + n], engine.exp_avg_sq[sidx:sidx + n]]
+        covered = 0
+        for tr0, tnr, tc0, tnc, toff in geo.rects(name, shapes_local[name], int(start), int(n)):
+            for fname, k, (sr0, snr, sc0, snc, soff) in stored.get(name, []):
+                r_lo, r_hi = max(tr0, sr0), min(tr0 + tnr, sr0 + snr)
+                c_lo, c_hi = max(tc0, sc0), min(tc0 + tnc, sc0 + snc)
+                if r_lo >= r_hi or c_lo >= c_hi:
+                    continue
+                t = get(fname)
+                for dst, key in zip(dsts, ("p", "m", "v")):
+                    src = t[f"{key}{k}"][soff:soff + snr * snc].view(snr, snc)[r_lo - sr0:r_hi - sr0, c_lo - sc0:c_hi - sc0]
+                    dst[toff:toff + tnr * tnc].view(tnr, tnc)[r_lo - tr0:r_hi - tr0, c_lo - tc0:c_hi - tc0].copy_(src)
+                covered += (r_hi - r_lo) * (c_hi - c_lo)
+        if covered != n:
+            raise RuntimeError(f"checkpoint {ckpt_dir} covers {covered} of the {n} elements this rank owns "
+                               f"of {name!r} (elements [{start}, {start + n}))")
     if load_optimizer:
         engine.step_count = int(meta["step"])
     # replicated engines must see identical parameters everywhere (ZeRO all-gathers its slices)
@@ -180,6 +314,7 @@ def load_sharded(ckpt_dir, engine, load_optimizer: bool = True):
     if sync is not None:
         sync()
     barrier()
+    return meta
 
 
 # ------------------------------------------------------------------------------ high level
@@ -207,7 +342,7 @@ class CheckpointManager:
         self._error = None
 
     # ------------------------------------------------------------------ async path
-    def _snapshot_host(self):
+    def _snapshot_host(self, global_step=None):
         """Collective part of a save: everything the writer thread needs, on the host."""
         jobs = []  # (relative path, object) for torch.save; sharded handled separately
         shard = None
@@ -220,7 +355,7 @@ class CheckpointManager:
                 sd = self.engine.full_state_dict()
                 if get_rank() == 0:
                     jobs.append(("model.pt", sd))
-            shard = snapshot_sharded(self.engine)
+            shard = snapshot_sharded(self.engine, global_step)
         return jobs, shard
 
     def _write_pending(self, jobs, shard):
@@ -249,6 +384,10 @@ class CheckpointManager:
 
             pend, d = self.exp_dir / self.PENDING, self.exp_dir
             state, sched_sd, rng = self._pending
+            # state.json goes first and comes back last: a crash anywhere in between leaves no
+            # state.json, i.e. no checkpoint, instead of an old state.json beside new weights
+            if (d / "state.json").exists():
+                os.remove(d / "state.json")
             for item in pend.iterdir():
                 dst = d / item.name
                 if dst.is_dir():
@@ -268,7 +407,7 @@ class CheckpointManager:
 
             self.finalize()
             barrier()
-            jobs, shard = self._snapshot_host()
+            jobs, shard = self._snapshot_host(state.get("global_step"))
             if get_rank() == 0:
                 box = _RngBox()
                 save_rng(box)
@@ -281,6 +420,10 @@ class CheckpointManager:
         rank = get_rank()
         d = self.exp_dir
         barrier()
+        if rank == 0 and (d / "state.json").exists():
+            os.remove(d / "state.json")  # re-written last: never an old state beside new weights
+        barrier()
+        gs = state.get("global_step")
         if self.style == "full":
             if rank == 0:
                 torch.save(self.engine.full_state_dict(), d / "model.pt")
@@ -289,9 +432,9 @@ class CheckpointManager:
             sd = self.engine.full_state_dict()
             if rank == 0:
                 torch.save(sd, d / "model.pt")
-            save_sharded(d / "checkpoint", self.engine)
+            save_sharded(d / "checkpoint", self.engine, gs)
         else:
-            save_sharded(d / "checkpoint", self.engine)
+            save_sharded(d / "checkpoint", self.engine, gs)
         if rank == 0:
             torch.save(self.lr_scheduler.state_dict(), d / "lr_scheduler.pt")
             save_rng(d / "rng.pt")
@@ -306,12 +449,16 @@ class CheckpointManager:
             sd = torch.load(d / "model.pt", map_location=dev, weights_only=True)
             self.engine.module.load_state_dict(sd)
             self.optimizer.load_state_dict(torch.load(d / "optimizer.pt", map_location=dev, weights_only=True))
+            meta = None
         else:
-            load_sharded(d / "checkpoint", self.engine)
+            meta = load_sharded(d / "checkpoint", self.engine)
         self.lr_scheduler.load_state_dict(torch.load(d / "lr_scheduler.pt", weights_only=True))
         if (d / "rng.pt").exists():
             load_rng(d / "rng.pt", self.local_rank)
         with open(d / "state.json") as fp:
             state = json.load(fp)
+        if meta is not None and meta.get("global_step") is not None and meta["global_step"] != state.get("global_step"):
+            raise RuntimeError(f"{d}: checkpoint/ holds step {meta['global_step']} but state.json says "
+                               f"{state.get('global_step')} (interrupted save?)")
         barrier()
         return state

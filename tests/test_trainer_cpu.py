@@ -42,7 +42,7 @@ def test_fsdp_chapter_checkpoint_resume(tmp_path):
     r = _torchrun("04-fully-sharded-data-parallel", base + ["--max-steps", "2"])
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     ck = tmp_path / "fs" / "checkpoint"
-    assert (ck / ".metadata").exists() and (ck / "__0_0.distcp").exists() and (ck / "__1_0.distcp").exists()
+    assert (ck / "index.json").exists() and (ck / "shard_r00000.pt").exists() and (ck / "shard_r00001.pt").exists()
     r = _torchrun("04-fully-sharded-data-parallel", base + ["--max-steps", "4"])
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "Resuming" in out, out[-3000:]
@@ -61,7 +61,7 @@ def test_fsdp_async_checkpoint_resume(tmp_path):
     d = tmp_path / "fa"
     assert not (d / ".pending").exists()
     assert json.loads((d / "state.json").read_text())["global_step"] == 4
-    assert (d / "checkpoint" / ".metadata").exists() and (d / "rng.pt").exists() and (d / "lr_scheduler.pt").exists()
+    assert (d / "checkpoint" / "index.json").exists() and (d / "rng.pt").exists() and (d / "lr_scheduler.pt").exists()
     r = _torchrun("04-fully-sharded-data-parallel", base + ["--max-steps", "6"])
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "Resuming" in out, out[-3000:]

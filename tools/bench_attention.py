@@ -32,13 +32,79 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--sweep", action="store_true",
                     help="constant 16k tokens, S = 512..8192, causal and non-causal (Hq32/Hkv8/D128)")
+    ap.add_argument("--ab", default=None,
+                    help="comma list of DTG_FA_FWD variants (e.g. v0,v1): forward timed in interleaved "
+                         "rounds in ONE process (same device, same clocks), medians reported")
     a = ap.parse_args()
+    if a.ab:
+        return ab(a, a.ab.split(","))
     if a.sweep:
         for S in (512, 1024, 2048, 4096, 8192):
             for causal in (True, False):
                 run(a, dict(B=16384 // S, S=S, hq=32, hkv=8, d=128, docs=None), f"sweep_S{S}", causal)
         return
     run(a, SHAPES[a.shape], a.shape, True)
+
+
+def _inputs(c, causal):
+    dev = torch.device("cuda:0")
+    B, S, hq, hkv, d = c["B"], c["S"], c["hq"], c["hkv"], c["d"]
+    T = B * S
+    if c["docs"]:
+        g = torch.Generator().manual_seed(0)
+        lens, left = [], T
+        while left > 0:
+            n = min(left, int(torch.randint(64, 2 * c["docs"], (1,), generator=g)))
+            lens.append(n)
+            left -= n
+        cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32)
+        flops = sum(l * l / (2 if causal else 1) for l in lens) * 4 * d * hq
+    else:
+        cu = torch.arange(0, T + 1, S, dtype=torch.int32)
+        flops = B * S * S / (2 if causal else 1) * 4 * d * hq
+    cu = cu.to(dev)
+    maxlen = int((cu[1:] - cu[:-1]).max())
+    qkv = torch.randn(T, (hq + 2 * hkv) * d, device=dev).bfloat16()
+    q = qkv[:, : hq * d].view(T, hq, d)
+    k = qkv[:, hq * d:(hq + hkv) * d].view(T, hkv, d)
+    v = qkv[:, (hq + hkv) * d:].view(T, hkv, d)
+    return q, k, v, cu, maxlen, flops, 1 / math.sqrt(d)
+
+
+def ab(a, variants, rounds=7):
+    import statistics
+
+    cases = [("S1024c", dict(B=16, S=1024, hq=32, hkv=8, d=128, docs=None), True),
+             ("S512nc", dict(B=32, S=512, hq=32, hkv=8, d=128, docs=None), False),
+             ("S8192nc", dict(B=2, S=8192, hq=32, hkv=8, d=128, docs=None), False),
+             ("S4096c", dict(B=4, S=4096, hq=32, hkv=8, d=128, docs=None), True),
+             ("rime", SHAPES["rime"], True), ("gpt2", SHAPES["gpt2"], True)]
+    ops = torch.ops.dtg
+    for name, c, causal in cases:
+        q, k, v, cu, maxlen, flops, scale = _inputs(c, causal)
+        ref = None
+        times = {vv: [] for vv in variants}
+        for r in range(rounds):
+            for vv in variants:
+                os.environ["DTG_FA_FWD"] = vv
+                for _ in range(5):
+                    o, _ = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal)
+                if ref is None:
+                    ref = o.float()
+                elif r == 0:
+                    assert (o.float() - ref).abs().max().item() < 2e-2, (name, vv)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal)
+                e1.record()
+                torch.cuda.synchronize()
+                times[vv].append(e0.elapsed_time(e1) / a.iters)
+        rec = {"case": name}
+        for vv in variants:
+            med = statistics.median(times[vv])
+            rec[vv] = {"ms": round(med, 4), "min_ms": round(min(times[vv]), 4), "TFLOPs": round(flops / med / 1e9, 1)}
+        print(json.dumps(rec), flush=True)
 
 
 def run(a, c, name, causal):
@@ -70,7 +136,7 @@ def run(a, c, name, causal):
     o, lse = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal)
 
     def timeit(fn):
-        for _ in range(3):
+        for _ in range(max(10, a.iters // 2)):  # settle clocks (DVFS) before timing
             fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
