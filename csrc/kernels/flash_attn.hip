@@ -451,24 +451,6 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   const bool qok = qrow < seqlen;
   const int64_t t_row = s0 + (qok ? qrow : seqlen - 1);
 
-  bf16x8 qf[NC], dof[NC];
-  load_row_frags<NC>(P.q + t_row * P.sq + (int64_t)head * D, qok, h, qf);
-  load_row_frags<NC>(P.dout + (t_row * P.hq + head) * D, qok, h, dof);
-  float delta;
-  {
-    bf16x8 of[NC];
-    load_row_frags<NC>(P.o + (t_row * P.hq + head) * D, qok, h, of);
-    float part = 0.f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) part += static_cast<float>(dof[c][j]) * static_cast<float>(of[c][j]);
-    }
-    delta = part + __shfl_xor(part, 32, 64);
-    if (qok && h == 0) P.delta[(int64_t)head * P.T + s0 + qrow] = delta;
-  }
-  const float lse2 = qok ? P.lse[(int64_t)head * P.T + s0 + qrow] * kLog2e : 0.f;
-
   int koff[NC], toa[ND], tob[ND];
 #pragma unroll
   for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
@@ -480,13 +462,53 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   const uint16_t* kbase = P.k + (int64_t)s0 * P.sk + (int64_t)kvh * D;
   const uint16_t* vbase = P.v + (int64_t)s0 * P.sv + (int64_t)kvh * D;
 
+  // Prologue: Q, dO and O rows arrive as whole lines (coalesced, range-checked buffer loads:
+  // rows past the end read zeros), delta = rowsum(dO * O) is reduced in that layout, and Q / dO
+  // reach their MFMA fragments through LDS (both K/V buffer pairs are free until tile 0 is
+  // staged) -- instead of three sets of fragment-shaped loads (32 rows x 32 B per instruction).
+  constexpr int QIMG = kDqBQ * RB;
+  static_assert(2 * QIMG <= 4 * TILE, "Q + dO images must fit the K/V buffers");
+  float* rowd = reinterpret_cast<float*>(smem + 4 * TILE);  // [kDqBQ] delta per row
+  bf16x8 qf[NC], dof[NC];
+  float delta;
+  Stager<kDqBK, D, 256> sk, sv;
+  {
+    Stager<kDqBQ, D, 256> sq, sdo, so;
+    const int64_t srow = (int64_t)(s0 + q0);
+    sq.load(P.q + srow * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
+    sdo.load(P.dout + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
+    so.load(P.o + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
+    sk.load(kbase, P.sk, seqlen);
+    sv.load(vbase, P.sv, seqlen);
+    constexpr int NCH = D / 8, RSTEP = 256 / NCH, PER = kDqBQ / RSTEP;
+    const int row0 = threadIdx.x / NCH, ch = threadIdx.x % NCH;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += bf2f(sdo.regs[i][j]) * bf2f(so.regs[i][j]);
+#pragma unroll
+      for (int x = 1; x < NCH; x <<= 1) part += __shfl_xor(part, x, 64);  // the row's NCH lanes
+      if (ch == 0) rowd[row0 + i * RSTEP] = part;
+    }
+    sq.store(smem);
+    sdo.store(smem + QIMG);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      qf[c] = lds_frag(smem + 32 * w * RB + koff[c]);
+      dof[c] = lds_frag(smem + QIMG + 32 * w * RB + koff[c]);
+    }
+    delta = rowd[32 * w + r];
+    __syncthreads();  // every wave holds its fragments before tile 0 overwrites the images
+  }
+  if (qok && h == 0) P.delta[(int64_t)head * P.T + s0 + qrow] = delta;
+  const float lse2 = qok ? P.lse[(int64_t)head * P.T + s0 + qrow] * kLog2e : 0.f;
+
   f32x16 acc[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) acc[i] = f32x16{};
 
-  Stager<kDqBK, D, 256> sk, sv;
-  sk.load(kbase, P.sk, seqlen);
-  sv.load(vbase, P.sv, seqlen);
   sk.store(smem);
   sv.store(smem + TILE);
   __syncthreads();
@@ -561,21 +583,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   }
   if (t < ntiles) tile_step(t, std::integral_constant<int, 0>{});
 
-  if (qok) {
-    uint16_t* op = P.dq + (int64_t)(s0 + qrow) * P.sdq + (int64_t)head * D;
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        ushort4 v;
-        v.x = f2bf(acc[d][4 * g4 + 0] * P.scale);
-        v.y = f2bf(acc[d][4 * g4 + 1] * P.scale);
-        v.z = f2bf(acc[d][4 * g4 + 2] * P.scale);
-        v.w = f2bf(acc[d][4 * g4 + 3] * P.scale);
-        *reinterpret_cast<ushort4*>(op + 32 * d + 8 * g4 + 4 * h) = v;
-      }
-    }
-  }
+  store_rows_wide<ND>(acc, P.scale, P.dq + (int64_t)(s0 + min(qrow, seqlen - 1)) * P.sdq + (int64_t)head * D, qok);
 }
 
 // dK, dV, key-stationary: 4 waves x 32 keys, one wave per SIMD with the dK/dV accumulators in
@@ -769,23 +777,9 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     }
   }
 
-  if (key < seqlen) {
-    uint16_t* dkp = P.dk + (int64_t)(s0 + key) * P.sdk + (int64_t)kvh * D;
-    uint16_t* dvp = P.dv + (int64_t)(s0 + key) * P.sdv + (int64_t)kvh * D;
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        ushort4 a, b;
-        a.x = f2bf(dk[d][4 * g4 + 0] * P.scale); a.y = f2bf(dk[d][4 * g4 + 1] * P.scale);
-        a.z = f2bf(dk[d][4 * g4 + 2] * P.scale); a.w = f2bf(dk[d][4 * g4 + 3] * P.scale);
-        b.x = f2bf(dv[d][4 * g4 + 0]); b.y = f2bf(dv[d][4 * g4 + 1]);
-        b.z = f2bf(dv[d][4 * g4 + 2]); b.w = f2bf(dv[d][4 * g4 + 3]);
-        *reinterpret_cast<ushort4*>(dkp + 32 * d + 8 * g4 + 4 * h) = a;
-        *reinterpret_cast<ushort4*>(dvp + 32 * d + 8 * g4 + 4 * h) = b;
-      }
-    }
-  }
+  const int64_t krow = s0 + min(key, seqlen - 1);
+  store_rows_wide<ND>(dk, P.scale, P.dk + krow * P.sdk + (int64_t)kvh * D, key < seqlen);
+  store_rows_wide<ND>(dv, 1.f, P.dv + krow * P.sdv + (int64_t)kvh * D, key < seqlen);
 }
 
 }  // namespace fa
@@ -919,7 +913,7 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   }();
   {
     dim3 grid(hq, nseq, (max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ);
-    const size_t lds = 4 * fa::kDqBK * D * 2;
+    const size_t lds = 4 * fa::kDqBK * D * 2 + fa::kDqBQ * 4;  // + the per-row delta
 #define DTG_BWD_DQ(DD, C, O)                                                              \
   do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O>, lds);                        \
        hipLaunchKernelGGL((fa::bwd_dq_kernel<DD, C, O>), grid, dim3(256), lds, stream(), P); } while (0)
