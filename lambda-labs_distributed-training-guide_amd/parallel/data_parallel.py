@@ -58,8 +58,12 @@ class DataParallel:
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         for n, p in named:
             p._dtg_name = n
+        tp_on = tp_group is not None and comm.world(tp_group) > 1
         self.space = FlatSpace(named, dev, world=self.world if self.mode == "zero" else 1,
-                               bucket_bytes=bucket_mb << 20, dtype=named[0][1].dtype)
+                               bucket_bytes=bucket_mb << 20, dtype=named[0][1].dtype,
+                               trailing=(lambda p: getattr(p, "_dtg_sequence_parallel", False)) if tp_on else None)
+        self._sp_bucket = next((b for b in self.space.buckets if b.trailing), None)
+        self._sp_reduced = False
         self.params = rebind_parameters(model, self.space, copy_data=True, notify=self._on_grad)
         self._sync_enabled = True
         self._inflight = []
@@ -119,9 +123,17 @@ class DataParallel:
         finally:
             self._sync_enabled = prev
 
+    def _reduce_sp(self):
+        """Sequence-parallel (TP-replicated) norm weights: every TP rank holds a partial gradient;
+        ONE all-reduce over the trailing bucket sums them (was one per parameter: 65
+        latency-bound collectives per step at 8B).  Linear, so it may run once after several
+        accumulated micro-batches."""
+        b = self._sp_bucket
+        if b is not None and not self._sp_reduced:
+            comm.all_reduce_(self.space.grad_buf[b.start:b.end], self.tp_group)
+            self._sp_reduced = True
+
     def _on_grad(self, p):
-        if getattr(p, "_dtg_sequence_parallel", False) and self.tp_group is not None:
-            comm.all_reduce_(p.main_grad, self.tp_group)
         if not self._sync_enabled or (self.mode == "single" and not self.overlap_optimizer):
             return
         b = p._dtg_bucket
@@ -133,6 +145,8 @@ class DataParallel:
         if b.launched:
             return
         b.launched = True
+        if b.trailing:
+            self._reduce_sp()
         view = self.space.grad_buf[b.start:b.end]
         if self.mode == "ddp":
             b.work = dist.all_reduce(view, group=self.group, async_op=True)
@@ -181,6 +195,8 @@ class DataParallel:
 
     def finish_grad_sync(self):
         """Call after backward (the last micro-batch): flush unlaunched buckets, wait for all."""
+        if self.mode == "single" and not self.overlap_optimizer and self._sync_enabled:
+            self._reduce_sp()
         if (self.mode != "single" or self.overlap_optimizer) and self._sync_enabled:
             for p in self.params:
                 if not getattr(p, "_dtg_grad_written", False):
@@ -202,6 +218,7 @@ class DataParallel:
 
     def zero_grad(self):
         reset_grad_state(self.params)
+        self._sp_reduced = False
         for b in self.space.buckets:
             b.pending = b.expected
             b.launched = False

@@ -27,10 +27,11 @@ def _round_up(x, m):
 
 
 class Bucket:
-    __slots__ = ("index", "start", "end", "params", "pending", "expected", "work", "launched", "stepped")
+    __slots__ = ("index", "start", "end", "params", "pending", "expected", "work", "launched", "stepped", "trailing")
 
-    def __init__(self, index, start, end, params):
+    def __init__(self, index, start, end, params, trailing=False):
         self.index, self.start, self.end, self.params = index, start, end, params
+        self.trailing = trailing  # the separate last bucket of `trailing`-predicate params
         self.expected = sum(getattr(p, "_dtg_uses", 1) for p in params)
         self.pending = self.expected
         self.work = None
@@ -47,7 +48,10 @@ class FlatSpace:
 
     def __init__(self, named_params: Sequence[Tuple[str, nn.Parameter]], device, world: int = 1,
                  bucket_bytes: int = 256 << 20, dtype=torch.bfloat16, grad_dtype=None, reverse=True,
-                 alloc_params=True):
+                 alloc_params=True, trailing: Optional[Callable] = None):
+        """`trailing(p)`: parameters moved into one extra bucket after all others (tensor-
+        parallel replicated norm weights: their gradients are summed over TP with ONE
+        all-reduce of that bucket instead of one per parameter)."""
         self.world = world
         self.device = torch.device(device)
         self.dtype = dtype
@@ -55,6 +59,9 @@ class FlatSpace:
         items = list(named_params)
         if reverse:
             items = items[::-1]
+        tail = [(n, p) for n, p in items if trailing is not None and trailing(p)]
+        items = [(n, p) for n, p in items if not (trailing is not None and trailing(p))] + tail
+        n_main = len(items) - len(tail)
         self.names = [n for n, _ in items]
         esz = torch.tensor([], dtype=dtype).element_size()
         cap = max(1, bucket_bytes // esz)
@@ -63,9 +70,9 @@ class FlatSpace:
         self.offsets: List[int] = []
         buckets_spec = []
         cur_start, cur, cur_params = 0, 0, []
-        for n, p in items:
+        for k, (n, p) in enumerate(items):
             sz = _round_up(p.numel(), ALIGN)
-            if cur_params and (cur - cur_start) + sz > cap:
+            if cur_params and ((cur - cur_start) + sz > cap or k == n_main):
                 end = cur_start + _round_up(cur - cur_start, unit)
                 buckets_spec.append((cur_start, end, cur_params))
                 cur_start = cur = end
@@ -82,7 +89,8 @@ class FlatSpace:
         self.params_src = [p for _, p in items]
         self.param_buf = torch.zeros(self.numel, dtype=dtype, device=self.device) if alloc_params else None
         self.grad_buf = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
-        self.buckets = [Bucket(i, s, e, ps) for i, (s, e, ps) in enumerate(buckets_spec)]
+        self.buckets = [Bucket(i, s, e, ps, trailing=bool(tail) and i == len(buckets_spec) - 1)
+                        for i, (s, e, ps) in enumerate(buckets_spec)]
         self.param_bucket = []
         for b in self.buckets:
             self.param_bucket.extend([b] * len(b.params))

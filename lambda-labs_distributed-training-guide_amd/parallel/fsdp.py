@@ -88,6 +88,11 @@ def size_based_units(model: nn.Module, min_num_params: int) -> List[nn.Module]:
 class _Unit:
     def __init__(self, engine: "FullyShard", idx: int, module: nn.Module, named: Sequence, is_root: bool):
         self.engine, self.idx, self.module, self.is_root = engine, idx, module, is_root
+        # TP-replicated (sequence-parallel) parameters last and contiguous: one TP all-reduce
+        # of that slice per unit before its reduce-scatter, instead of one per parameter
+        named = [x for x in named if not getattr(x[1], "_dtg_sequence_parallel", False)] + \
+                [x for x in named if getattr(x[1], "_dtg_sequence_parallel", False)]
+        self.n_sp = sum(1 for _, p in named if getattr(p, "_dtg_sequence_parallel", False))
         self.names = [n for n, _ in named]
         self.params_src = [p for _, p in named]
         self.shapes = [tuple(p.shape) for p in self.params_src]
@@ -364,8 +369,6 @@ class FullyShard:
 
     def _on_grad(self, p):
         u = p._dtg_unit
-        if getattr(p, "_dtg_sequence_parallel", False) and self.tp_group is not None:
-            dist.all_reduce(p.main_grad, group=self.tp_group)
         u.pending -= 1
         if u.pending == 0:
             self._launch_rs(u)
@@ -381,6 +384,9 @@ class FullyShard:
         end = u.offsets[-1] + math.prod(u.shapes[-1]) if u.params else 0
         if end < u.numel:
             u.full_grad[end:].zero_()
+        if u.n_sp and self.tp_group is not None and comm.world(self.tp_group) > 1:
+            lo = u.offsets[len(u.params) - u.n_sp]
+            comm.all_reduce_(u.full_grad[lo:end], self.tp_group)
         gs = self._shard_view(u, self.shard_grads)
         first = self._first_micro
         direct = not (self.cpu_offload or not first)  # reduce-scatter straight into the grad shard
