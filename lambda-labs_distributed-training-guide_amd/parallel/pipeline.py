@@ -91,6 +91,8 @@ class PipelineStage:
         self.tie_group = None
         if self.size > 1 and self.tied and model.embed_tokens is not None:
             model.embed_tokens.weight._dtg_uses = 1  # one use per stage (embedding, or lm_head)
+            if not self.first:  # the last stage's copy of the tied matrix: checkpointed by stage 0
+                model._dtg_ckpt_skip = {"embed_tokens.weight"}
         if self.size > 1 and self.tied:
             # first + last stage of every pipeline (new_group is collective over the world)
             W, P = dist.get_world_size(), self.size

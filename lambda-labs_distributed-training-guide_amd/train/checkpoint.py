@@ -184,6 +184,22 @@ class _TPGeom:
         return out
 
 
+def _name_map(engine):
+    """Parameter name -> checkpoint (global) name: a pipeline stage's decoder layers are
+    renumbered from 0 locally (`_dtg_layer_offset` = its first global layer)."""
+    off = getattr(engine.module, "_dtg_layer_offset", 0)
+    if not off:
+        return lambda n: n
+
+    def g(n):
+        if n.startswith("layers."):
+            i, rest = n[len("layers."):].split(".", 1)
+            return f"layers.{int(i) + off}.{rest}"
+        return n
+
+    return g
+
+
 def _replicated_engine(engine) -> bool:
     return getattr(engine, "mode", "fsdp") in ("single", "ddp")
 
@@ -198,18 +214,20 @@ def snapshot_sharded(engine, global_step=None):
     TP rank 0."""
     rank, world = get_rank(), get_world_size()
     geo = _TPGeom(engine)
+    gname = _name_map(engine)
     shapes_local = {n: list(p.shape) for n, p in engine.module.named_parameters()}
     write = not (_replicated_engine(engine) and getattr(engine, "rank", 0) != 0)
+    skip = getattr(engine.module, "_dtg_ckpt_skip", set())  # e.g. a pipeline's second tied-embedding copy
     pieces = engine.ckpt_pieces()
     tensors, index = {}, []
     for j, (name, start, n, pview, sidx) in enumerate(pieces):
-        if not write or (geo.size > 1 and geo.rank != 0 and param_kind(name) == "rep"):
+        if not write or name in skip or (geo.size > 1 and geo.rank != 0 and param_kind(name) == "rep"):
             continue
         k = len(index)
         tensors[f"p{k}"] = pview.detach().reshape(-1).to("cpu", copy=True)
         tensors[f"m{k}"] = engine.exp_avg[sidx:sidx + n].to("cpu", copy=True)
         tensors[f"v{k}"] = engine.exp_avg_sq[sidx:sidx + n].to("cpu", copy=True)
-        index.append([name, int(n), geo.rects(name, shapes_local[name], int(start), int(n))])
+        index.append([gname(name), int(n), geo.rects(name, shapes_local[name], int(start), int(n))])
     entry = {"file": _shard_file(rank), "rank": rank, "tp_rank": geo.rank, "index": index}
     if dist.is_initialized() and world > 1:
         gathered = [None] * world
@@ -218,10 +236,23 @@ def snapshot_sharded(engine, global_step=None):
         gathered = [entry]
     meta = None
     if rank == 0:
-        gshapes = {n: geo.global_shape(param_kind(n) if geo.size > 1 else "rep", sh) for n, sh in shapes_local.items()}
+        files = [f for f in gathered if f["index"]]
+        gshapes = {}  # from every rank: a pipeline stage knows only its own layers
+        if dist.is_initialized() and world > 1:
+            mine = {gname(n): geo.global_shape(param_kind(n) if geo.size > 1 else "rep", sh)
+                    for n, sh in shapes_local.items()}
+            allshapes = [None] * world
+            dist.gather_object(mine, allshapes, dst=0)
+            for d in allshapes:
+                gshapes.update(d)
+        else:
+            gshapes = {gname(n): geo.global_shape(param_kind(n) if geo.size > 1 else "rep", sh)
+                       for n, sh in shapes_local.items()}
         meta = {"format": FORMAT, "world_size": world, "tp_size": geo.size, "step": int(engine.step_count),
-                "global_step": global_step, "param_shapes_global": gshapes,
-                "files": [f for f in gathered if f["index"]]}
+                "global_step": global_step, "param_shapes_global": gshapes, "files": files}
+    elif dist.is_initialized() and world > 1:
+        dist.gather_object({gname(n): geo.global_shape(param_kind(n) if geo.size > 1 else "rep", sh)
+                            for n, sh in shapes_local.items()}, None, dst=0)
     return tensors, entry, meta
 
 
@@ -266,14 +297,15 @@ def load_sharded(ckpt_dir, engine, load_optimizer: bool = True):
     ckpt_dir = Path(ckpt_dir)
     meta = read_index(ckpt_dir)
     geo = _TPGeom(engine)
+    gname = _name_map(engine)
     shapes_local = {n: list(p.shape) for n, p in engine.module.named_parameters()}
     gshapes = meta["param_shapes_global"]
     for name, sh in shapes_local.items():
         mine = geo.global_shape(param_kind(name) if geo.size > 1 else "rep", sh)
-        if name not in gshapes:
-            raise KeyError(f"checkpoint {ckpt_dir} has no parameter {name!r}")
-        if list(gshapes[name]) != mine:
-            raise ValueError(f"{name}: checkpoint global shape {gshapes[name]} != model's {mine}")
+        if gname(name) not in gshapes:
+            raise KeyError(f"checkpoint {ckpt_dir} has no parameter {gname(name)!r}")
+        if list(gshapes[gname(name)]) != mine:
+            raise ValueError(f"{gname(name)}: checkpoint global shape {gshapes[gname(name)]} != model's {mine}")
     stored = {}  # name -> [(file, key, rect)]
     for f in meta["files"]:
         for k, (name, n, rects) in enumerate(f["index"]):
@@ -294,7 +326,7 @@ def load_sharded(ckpt_dir, engine, load_optimizer: bool = True):
             dsts += [engine.exp_avg[sidx:sidx + n], engine.exp_avg_sq[sidx:sidx + n]]
         covered = 0
         for tr0, tnr, tc0, tnc, toff in geo.rects(name, shapes_local[name], int(start), int(n)):
-            for fname, k, (sr0, snr, sc0, snc, soff) in stored.get(name, []):
+            for fname, k, (sr0, snr, sc0, snc, soff) in stored.get(gname(name), []):
                 r_lo, r_hi = max(tr0, sr0), min(tr0 + tnr, sr0 + snr)
                 c_lo, c_hi = max(tc0, sc0), min(tc0 + tnc, sc0 + snc)
                 if r_lo >= r_hi or c_lo >= c_hi:

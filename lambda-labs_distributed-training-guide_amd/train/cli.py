@@ -67,6 +67,11 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                             "all-to-all seq<->heads around attention (packed rows supported)")
         g.add_argument("--cp", default=1, type=int,
                        help="context parallel degree: zig-zag row shards, all-gathered K/V (dense rows)")
+        g.add_argument("--pp", default=1, type=int,
+                       help="pipeline parallel degree: contiguous ranks form a pipeline of decoder-layer stages "
+                            "(1F1B schedule, point-to-point activations); the rest is data parallel")
+        g.add_argument("--pp-microbatches", default=4, type=int,
+                       help="1F1B micro-batches per step (must divide --batch-size)")
     g.add_argument("--grad-accum", default=1, type=int, help="micro-batches per optimizer step (no_sync)")
     g.add_argument("--bucket-mb", default=256, type=int, help="gradient bucket size for DDP/ZeRO")
     if chapter == "02":

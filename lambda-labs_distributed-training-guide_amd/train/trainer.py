@@ -110,6 +110,16 @@ def _build(args, chapter, device, world):
         dp_group, seq_group, dp_rank, seq_rank, dp_size = make_mesh(nseq)
         seq = ("sp" if args.sp > 1 else "cp", seq_group, seq_rank, nseq)
         LOGGER.info(f"mesh: dp={dp_size} x {seq[0]}={nseq} (dp_rank={dp_rank}, {seq[0]}_rank={seq_rank})")
+    pp = max(1, getattr(args, "pp", 1))
+    pp_group = None
+    if pp > 1:
+        assert nseq == 1, "--pp is not combined with --sp / --cp"
+        from ..parallel.tensor_parallel import make_mesh
+
+        # contiguous ranks form one pipeline (its P-1 boundaries on distinct xGMI links);
+        # strided groups are the data-parallel replicas of each stage
+        dp_group, pp_group, dp_rank, pp_rank, dp_size = make_mesh(pp)
+        LOGGER.info(f"mesh: dp={dp_size} x pp={pp} (dp_rank={dp_rank}, stage={pp_rank})")
     replicate_group = None
     if getattr(args, "sharding", "full") == "hybrid" and world > 1:
         from ..parallel.tensor_parallel import make_mesh
@@ -128,6 +138,14 @@ def _build(args, chapter, device, world):
     else:
         model = build_model(cfg, device=device, tp_group=tp_group)
     model._dtg_seq = seq
+    model._dtg_pp = None
+    if pp > 1:
+        from ..parallel.pipeline import PipelineStage
+
+        stage = PipelineStage(model, pp_group)
+        model._dtg_layer_offset = stage.layer_range[0]  # checkpoints use global layer names
+        model._dtg_pp = stage
+        LOGGER.info(f"pipeline stage {stage.stage}/{pp}: layers [{stage.layer_range[0]}, {stage.layer_range[1]})")
     if args.activation_checkpointing == "on":
         apply_activation_checkpointing(model)
     LOGGER.info(f"{sum(p.numel() for p in model.parameters()) / 1e9:.3f}B parameters (this rank's shard of TP)")
@@ -143,8 +161,10 @@ def _build(args, chapter, device, world):
                             replicate_group=replicate_group)
         style = "sharded"
     else:
-        if world == 1:
+        if world == 1 or (pp > 1 and dp_size == 1):
             mode = "single"
+        elif pp > 1:
+            mode = args.dp_mode if chapter == "02" else "ddp"
         elif seq is not None:  # parameters replicated on every rank; the row's loss is split over seq ranks
             mode = args.dp_mode if chapter == "02" else "ddp"
         elif chapter in ("01", "rime"):
@@ -155,10 +175,18 @@ def _build(args, chapter, device, world):
             mode = "ddp" if args.zero_stage == 0 else "zero"
         else:  # 06: data parallel across TP groups
             mode = "ddp"
-        engine = DataParallel(model, mode=mode, group=None if seq is not None else dp_group, tp_group=tp_group,
+        engine = DataParallel(model, mode=mode, group=dp_group if pp > 1 else (None if seq is not None else dp_group),
+                              tp_group=tp_group,
                               bucket_mb=args.bucket_mb, broadcast_from_rank0=tp_group is None,
                               grad_divisor=dp_size if seq is not None else None)
         style = "full" if mode == "single" and chapter in ("01", "rime") else ("dp" if chapter == "02" else "sharded")
+        if pp > 1:
+            style = "sharded"  # no rank holds the whole model: no model.pt
+    if model._dtg_pp is not None:
+        from ..parallel.pipeline import OneFOneB
+
+        assert max(1, args.grad_accum) == 1, "--pp: the pipeline's micro-batches are the accumulation (--pp-microbatches)"
+        model._dtg_pp = OneFOneB(model._dtg_pp, engine, num_microbatches=args.pp_microbatches)
     LOGGER.info(f"After engine ({engine.mode}): {get_mem_stats(device)}")
     if args.init_from:
         from ..models.loading import load_pretrained
@@ -294,6 +322,13 @@ def run(chapter: str, argv=None):
             else:
                 opt.zero_grad(set_to_none=True)
                 loss_sum = None
+            if model._dtg_pp is not None and micro:  # 1F1B: forward and backward interleaved
+                b = micro[0]
+                wait_for_peers()
+                with timers["forward"]:
+                    loss_sum = model._dtg_pp.step(b["input_ids"], labels=b["labels"], num_valid=b["num_valid"],
+                                                  position_ids=b.get("position_ids")).detach()
+                micro_pp, micro = micro, []
             for j, b in enumerate(micro):
                 ctx = engine.no_sync() if j < accum - 1 else _null()
                 with ctx:
@@ -304,6 +339,8 @@ def run(chapter: str, argv=None):
                     with timers["backward"]:
                         engine.backward(out.loss)
                 loss_sum = out.loss.detach() if loss_sum is None else loss_sum + out.loss.detach()
+            if model._dtg_pp is not None:
+                micro = micro_pp
             if micro:
                 wait_for_peers()
                 with timers["update"]:

@@ -132,3 +132,22 @@ def test_running_loss_window_means_match_per_step_losses(tmp_path):
     assert len(per_step) == 6 and len(windows) == 3
     for k in range(3):
         assert windows[k] == pytest.approx((per_step[2 * k] + per_step[2 * k + 1]) / 2, rel=1e-5)
+
+
+@pytest.mark.slow
+def test_pp_chapter_runs_and_checkpoint_reshards_to_no_pp(tmp_path):
+    """Chapter 02 with --pp 2 (1F1B, gloo): trains, checkpoints with global layer names, and
+    the checkpoint resumes under --pp 1 on 2 data-parallel ranks (stage layout -> DP layout)."""
+    base = ["-e", "pp", "-d", "synthetic", "-m", "llama-tiny", "-s", "32", "--num-samples", "64", "-b", "4",
+            "--save-dir", str(tmp_path), "--log-freq", "1", "--ckpt-freq", "2", "--num-workers", "0"]
+    r = _torchrun("02-distributed-data-parallel", base + ["--max-steps", "2", "--pp", "2", "--pp-microbatches", "2"])
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "pipeline stage 1/2" in out
+    meta = json.loads((tmp_path / "pp" / "checkpoint" / "index.json").read_text())
+    names = {e[0] for f in meta["files"] for e in f["index"]}
+    assert "layers.1.mlp.gate_up_proj.weight" in names and "layers.0.mlp.gate_up_proj.weight" in names
+    r = _torchrun("02-distributed-data-parallel", base + ["--max-steps", "4"])
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "Resuming" in out, out[-3000:]
+    assert json.loads((tmp_path / "pp" / "state.json").read_text())["global_step"] == 4
