@@ -204,6 +204,20 @@ __device__ __forceinline__ void store_rows_wide(const f32x16* acc, float scale, 
   }
 }
 
+// Keys of query sequence `seq`: by default the sequence's own tokens (self-attention over
+// cu_seqlens).  With explicit per-sequence key ranges (kstart/klen: context parallelism, where a
+// local query chunk attends to a prefix of the gathered full row) the causal mask is
+// bottom-right aligned as in FlashAttention-2 varlen: query i of a sequence of len_q queries
+// attends to keys <= i + (len_k - len_q).
+struct KeyRange {
+  int start, len, off;
+};
+__device__ __forceinline__ KeyRange key_range(const int* kstart, const int* klen, int seq, int s0, int seqlen) {
+  if (kstart == nullptr) return KeyRange{s0, seqlen, 0};
+  const int n = klen[seq];
+  return KeyRange{kstart[seq], n, n - seqlen};
+}
+
 struct FwdParams {
   const uint16_t *q, *k, *v;
   int64_t sq, sk, sv;  // token strides (elements)
@@ -214,6 +228,7 @@ struct FwdParams {
   int hq, hkv;
   float c2;  // softmax scale * log2(e)
   long long* stamps;  // diagnostic path only (flash_attn_fwd_stamped): 6 words per workgroup
+  const int *kstart, *klen;  // optional per-sequence key ranges (see KeyRange)
 };
 
 // In-kernel timeline stamps (CDNA guide §7 'In-kernel stamps'): constant-rate 100 MHz clock,
@@ -246,6 +261,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   const int qb = CAUSAL ? (gridDim.z - 1 - blockIdx.z) : blockIdx.z;  // heavy blocks first
   const int q0 = qb * kFwdBQ;
   if (q0 >= seqlen) return;
+  const KeyRange kr = key_range(P.kstart, P.klen, seq, s0, seqlen);
+  const int klen = kr.len, koff_c = kr.off;  // causal: query i attends keys <= i + koff_c
   const int kvh = head / (P.hq / P.hkv);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -264,10 +281,10 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
 #pragma unroll
   for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
 
-  const int kv_end = CAUSAL ? min(seqlen, q0 + kFwdBQ) : seqlen;
+  const int kv_end = CAUSAL ? min(klen, q0 + kFwdBQ + koff_c) : klen;
   const int ntiles = (kv_end + kFwdBK - 1) / kFwdBK;
-  const uint16_t* kbase = P.k + (int64_t)s0 * P.sk + (int64_t)kvh * D;
-  const uint16_t* vbase = P.v + (int64_t)s0 * P.sv + (int64_t)kvh * D;
+  const uint16_t* kbase = P.k + (int64_t)kr.start * P.sk + (int64_t)kvh * D;
+  const uint16_t* vbase = P.v + (int64_t)kr.start * P.sv + (int64_t)kvh * D;
 
   f32x16 acc[ND];
 #pragma unroll
@@ -275,8 +292,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   float m = -INFINITY, l = 0.f;
 
   Stager<kFwdBK, D, 256> sk, sv;
-  sk.load(kbase, P.sk, seqlen);
-  sv.load(vbase, P.sv, seqlen);
+  sk.load(kbase, P.sk, klen);
+  sv.load(vbase, P.sv, klen);
   if constexpr (QLDS) sq.store(smem + 2 * TILE);  // the second K/V buffer is free until tile 0 ends
   sk.store(smem);
   sv.store(smem + TILE);
@@ -296,12 +313,12 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
     const bool more = t + 1 < ntiles;
     if (more) {
       const int nk = kt0 + kFwdBK;
-      sk.load(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk);
-      sv.load(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk);
+      sk.load(kbase + (int64_t)nk * P.sk, P.sk, klen - nk);
+      sv.load(vbase + (int64_t)nk * P.sv, P.sv, klen - nk);
     }
     const char* K = smem + B * 2 * TILE;
     const char* V = K + TILE;
-    if (!CAUSAL || kt0 <= wave_qmax) {  // wave-uniform skip of tiles above the diagonal
+    if (!CAUSAL || kt0 <= wave_qmax + koff_c) {  // wave-uniform skip of tiles above the diagonal
       f32x16 s[2];
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -315,11 +332,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       }
       pipeline_reads<2 * NC, 1, 4>();
       __builtin_amdgcn_sched_barrier(0);
-      if ((CAUSAL && kt0 + kFwdBK - 1 > wave_q0) || kt0 + kFwdBK > seqlen) {
+      if ((CAUSAL && kt0 + kFwdBK - 1 > wave_q0 + koff_c) || kt0 + kFwdBK > klen) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-          // key = kt0 + 32 kt + acc_row is masked when key > min(qrow, seqlen - 1)
-          const int lim = (CAUSAL ? min(qrow, seqlen - 1) : seqlen - 1) - (kt0 + 32 * kt + 4 * h);
+          // key = kt0 + 32 kt + acc_row is masked when key > min(qrow + koff_c, klen - 1)
+          const int lim = (CAUSAL ? min(qrow + koff_c, klen - 1) : klen - 1) - (kt0 + 32 * kt + 4 * h);
 #pragma unroll
           for (int i = 0; i < 16; ++i) s[kt][i] = acc_row0(i) > lim ? -INFINITY : s[kt][i];
         }
@@ -421,6 +438,7 @@ struct BwdParams {
   int64_t T;
   int hq, hkv;
   float scale, c2;
+  const int *kstart, *klen;  // optional per-sequence key ranges (see KeyRange)
 };
 
 constexpr int kDqBQ = 128;  // query rows per workgroup (4 waves x 32)
@@ -444,6 +462,8 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   const int qb = CAUSAL ? (gridDim.z - 1 - blockIdx.z) : blockIdx.z;  // heavy blocks first
   const int q0 = qb * kDqBQ;
   if (q0 >= seqlen) return;
+  const KeyRange kr = key_range(P.kstart, P.klen, seq, s0, seqlen);
+  const int klen = kr.len, koff_c = kr.off;
   const int kvh = head / (P.hq / P.hkv);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -457,10 +477,10 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 #pragma unroll
   for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
 
-  const int kv_end = CAUSAL ? min(seqlen, q0 + kDqBQ) : seqlen;
+  const int kv_end = CAUSAL ? min(klen, q0 + kDqBQ + koff_c) : klen;
   const int ntiles = (kv_end + kDqBK - 1) / kDqBK;
-  const uint16_t* kbase = P.k + (int64_t)s0 * P.sk + (int64_t)kvh * D;
-  const uint16_t* vbase = P.v + (int64_t)s0 * P.sv + (int64_t)kvh * D;
+  const uint16_t* kbase = P.k + (int64_t)kr.start * P.sk + (int64_t)kvh * D;
+  const uint16_t* vbase = P.v + (int64_t)kr.start * P.sv + (int64_t)kvh * D;
 
   // Prologue: Q, dO and O rows arrive as whole lines (coalesced, range-checked buffer loads:
   // rows past the end read zeros), delta = rowsum(dO * O) is reduced in that layout, and Q / dO
@@ -478,8 +498,8 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     sq.load(P.q + srow * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
     sdo.load(P.dout + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
     so.load(P.o + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
-    sk.load(kbase, P.sk, seqlen);
-    sv.load(vbase, P.sv, seqlen);
+    sk.load(kbase, P.sk, klen);
+    sv.load(vbase, P.sv, klen);
     constexpr int NCH = D / 8, RSTEP = 256 / NCH, PER = kDqBQ / RSTEP;
     const int row0 = threadIdx.x / NCH, ch = threadIdx.x % NCH;
 #pragma unroll
@@ -521,8 +541,8 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     const bool more = t + 1 < ntiles;
     if (more) {
       const int nk = kt0 + kDqBK;
-      sk.load(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk);
-      sv.load(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk);
+      sk.load(kbase + (int64_t)nk * P.sk, P.sk, klen - nk);
+      sv.load(vbase + (int64_t)nk * P.sv, P.sv, klen - nk);
     }
     const char* K = smem + B * 2 * TILE;
     const char* V = K + TILE;
@@ -530,7 +550,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     for (int kt = 0; kt < 2; ++kt) {
       const int key0 = kt0 + 32 * kt;
       // Wave-uniform skip of 32-key halves entirely above the diagonal or past the end.
-      if ((CAUSAL && key0 > wave_qmax) || key0 >= seqlen) continue;
+      if ((CAUSAL && key0 > wave_qmax + koff_c) || key0 >= klen) continue;
       f32x16 s = f32x16{}, dp = f32x16{};
       __builtin_amdgcn_sched_barrier(0);
       {
@@ -548,8 +568,8 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = fexp2(__builtin_fmaf(s[i], P.c2, -lse2));
-      if ((CAUSAL && key0 + 31 > wave_q0) || key0 + 32 > seqlen) {
-        const int lim = (CAUSAL ? min(qrow, seqlen - 1) : seqlen - 1) - (key0 + 4 * h);
+      if ((CAUSAL && key0 + 31 > wave_q0 + koff_c) || key0 + 32 > klen) {
+        const int lim = (CAUSAL ? min(qrow + koff_c, klen - 1) : klen - 1) - (key0 + 4 * h);
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[i] = acc_row0(i) > lim ? 0.f : s[i];
       }
@@ -605,8 +625,10 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
   const int seq = blockIdx.y, kvh = blockIdx.x;
   const int s0 = P.cu[seq];
   const int seqlen = P.cu[seq + 1] - s0;
+  const KeyRange kr = key_range(P.kstart, P.klen, seq, s0, seqlen);
+  const int klen = kr.len, koff_c = kr.off;  // query q attends key k iff k <= q + koff_c
   const int kb = blockIdx.z * kKvBK;  // z = 0 first: the heaviest causal key blocks
-  if (kb >= seqlen) return;
+  if (kb >= klen) return;
   const int group = P.hq / P.hkv;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -615,8 +637,8 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
 
   bf16x8 kf[NC], vf[NC];
   {
-    const bool ok = key < seqlen;
-    const int64_t t = s0 + (ok ? key : seqlen - 1);
+    const bool ok = key < klen;
+    const int64_t t = kr.start + (ok ? key : klen - 1);
     load_row_frags<NC>(P.k + t * P.sk + (int64_t)kvh * D, ok, h, kf);
     load_row_frags<NC>(P.v + t * P.sv + (int64_t)kvh * D, ok, h, vf);
   }
@@ -633,7 +655,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     dv[i] = f32x16{};
   }
 
-  const int first_slice = CAUSAL ? (kb / kKvBQ) : 0;
+  const int first_slice = CAUSAL ? (max(0, kb - koff_c) / kKvBQ) : 0;
   const int per_head = (seqlen + kKvBQ - 1) / kKvBQ - first_slice;
   const int nitems = per_head * group;
   const float inv_scale = 1.f / P.scale;
@@ -702,8 +724,8 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
-      if (CAUSAL && wkey0 + 31 > qs) {
-        const int lim = key - qs - 4 * h;  // query row qs + acc_row < key is masked
+      if (CAUSAL && wkey0 + 31 > qs + koff_c) {
+        const int lim = key - koff_c - qs - 4 * h;  // query row qs + acc_row < key - koff_c is masked
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) < lim) ? 0.f : s[i];
       }
@@ -777,9 +799,9 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     }
   }
 
-  const int64_t krow = s0 + min(key, seqlen - 1);
-  store_rows_wide<ND>(dk, P.scale, P.dk + krow * P.sdk + (int64_t)kvh * D, key < seqlen);
-  store_rows_wide<ND>(dv, 1.f, P.dv + krow * P.sdv + (int64_t)kvh * D, key < seqlen);
+  const int64_t krow = kr.start + min(key, klen - 1);
+  store_rows_wide<ND>(dk, P.scale, P.dk + krow * P.sdk + (int64_t)kvh * D, key < klen);
+  store_rows_wide<ND>(dv, 1.f, P.dv + krow * P.sdv + (int64_t)kvh * D, key < klen);
 }
 
 }  // namespace fa
@@ -796,15 +818,28 @@ static void check_qkv(const at::Tensor& t, const char* name, int64_t heads, int6
             name, " must be [T, H, D] with contiguous heads and 16-B aligned token stride");
 }
 
+// Optional per-sequence key ranges (k_start / k_len int32 [nseq]): checked, or nullptr pointers.
+static void key_range_ptrs(const at::Tensor* k_start, const at::Tensor* k_len, int nseq, const int** ks,
+                           const int** kl) {
+  *ks = *kl = nullptr;
+  if (k_start == nullptr) return;
+  for (const at::Tensor* t : {k_start, k_len})
+    DTG_CHECK(t->scalar_type() == at::kInt && t->is_cuda() && t->is_contiguous() && t->numel() == nseq,
+              "flash_attn: k_start / k_len must be int32 [nseq] on the GPU");
+  *ks = k_start->data_ptr<int>();
+  *kl = k_len->data_ptr<int>();
+}
+
 static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& q, const at::Tensor& k,
                                                               const at::Tensor& v, const at::Tensor& cu_seqlens,
                                                               int64_t max_seqlen, double scale, bool causal,
-                                                              at::Tensor* stamps) {
+                                                              at::Tensor* stamps, const at::Tensor* k_start = nullptr,
+                                                              const at::Tensor* k_len = nullptr) {
   const int64_t T = q.size(0), hq = q.size(1), D = q.size(2), hkv = k.size(1);
   check_qkv(q, "q", hq, D);
   check_qkv(k, "k", hkv, D);
   check_qkv(v, "v", hkv, D);
-  DTG_CHECK(k.size(0) == T && v.size(0) == T, "flash_attn: q/k/v token counts differ");
+  DTG_CHECK(v.size(0) == k.size(0) && (k_start != nullptr || k.size(0) == T), "flash_attn: q/k/v token counts differ");
   DTG_CHECK(hq % hkv == 0, "flash_attn: Hq must be a multiple of Hkv");
   DTG_CHECK(D == 64 || D == 128, "flash_attn: head_dim must be 64 or 128");
   DTG_CHECK(cu_seqlens.scalar_type() == at::kInt && cu_seqlens.is_cuda() && cu_seqlens.is_contiguous(),
@@ -818,7 +853,8 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
   const int nqb = (int)((max_seqlen + fa::kFwdBQ - 1) / fa::kFwdBQ);
   fa::FwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), q.stride(0), k.stride(0), v.stride(0),
                   bf16_mut(o), lse.data_ptr<float>(), cu_seqlens.data_ptr<int>(), T, (int)hq, (int)hkv,
-                  (float)(scale * fa::kLog2e), nullptr};
+                  (float)(scale * fa::kLog2e), nullptr, nullptr, nullptr};
+  key_range_ptrs(k_start, k_len, nseq, &P.kstart, &P.klen);
   dim3 grid(hq, nseq, nqb);
   if (stamps != nullptr) {
     *stamps = at::zeros({(int64_t)grid.x * grid.y * grid.z, 6}, q.options().dtype(at::kLong));
@@ -866,7 +902,8 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
                                 const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
                                 const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale,
                                 bool causal, const at::Tensor& dq, const at::Tensor& dk,
-                                const at::Tensor& dv) {
+                                const at::Tensor& dv, const at::Tensor* k_start = nullptr,
+                                const at::Tensor* k_len = nullptr, int64_t max_seqlen_k = -1) {
   auto dout = dout_.contiguous();
   const int64_t T = q.size(0), hq = q.size(1), D = q.size(2), hkv = k.size(1);
   check_qkv(q, "q", hq, D);
@@ -898,7 +935,9 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   fa::BwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), bf16_ptr(dout), bf16_ptr(o), q.stride(0), k.stride(0),
                   v.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), bf16_mut(dq), bf16_mut(dk),
                   bf16_mut(dv), dq.stride(0), dk.stride(0), dv.stride(0), cu_seqlens.data_ptr<int>(), T, (int)hq,
-                  (int)hkv, (float)scale, (float)(scale * fa::kLog2e)};
+                  (int)hkv, (float)scale, (float)(scale * fa::kLog2e), nullptr, nullptr};
+  key_range_ptrs(k_start, k_len, nseq, &P.kstart, &P.klen);
+  if (max_seqlen_k < 0) max_seqlen_k = max_seqlen;
   // Waves per SIMD of the dq kernel at head_dim 128 (DTG_FA_OCC=1|2; measured in profiles/).
   static const int occ = [] {
     const char* e = std::getenv("DTG_FA_OCC");
@@ -925,7 +964,7 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
     DTG_LAUNCH_CHECK();
   }
   {
-    dim3 grid(hkv, nseq, (max_seqlen + fa::kKvBK - 1) / fa::kKvBK);
+    dim3 grid(hkv, nseq, (max_seqlen_k + fa::kKvBK - 1) / fa::kKvBK);
     const size_t lds = 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
 #define DTG_BWD_KV(DD, C, PF)                                                             \
   do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF>, lds);                     \
@@ -972,7 +1011,31 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& qkv, int
   return dqkv;
 }
 
+// FlashAttention-2-style varlen over explicit per-sequence key ranges (context parallelism).
+std::tuple<at::Tensor, at::Tensor> flash_attn_varlen_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                         const at::Tensor& cu_seqlens_q, const at::Tensor& k_start,
+                                                         const at::Tensor& k_len, int64_t max_seqlen_q,
+                                                         int64_t max_seqlen_k, double scale, bool causal) {
+  (void)max_seqlen_k;  // the forward grid spans query blocks only
+  return flash_attn_fwd_impl(q, k, v, cu_seqlens_q, max_seqlen_q, scale, causal, nullptr, &k_start, &k_len);
+}
+
+// Key ranges must be disjoint; keys outside every range get zero dK / dV.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_varlen_bwd(
+    const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+    const at::Tensor& lse, const at::Tensor& cu_seqlens_q, const at::Tensor& k_start, const at::Tensor& k_len,
+    int64_t max_seqlen_q, int64_t max_seqlen_k, double scale, bool causal) {
+  auto dq = at::empty(q.sizes(), q.options());
+  auto dk = at::zeros(k.sizes(), k.options());
+  auto dv = at::zeros(v.sizes(), v.options());
+  flash_attn_bwd_impl(dout, q, k, v, o, lse, cu_seqlens_q, max_seqlen_q, scale, causal, dq, dk, dv, &k_start, &k_len,
+                      max_seqlen_k);
+  return {dq, dk, dv};
+}
+
 TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
+  m.impl("flash_attn_varlen_fwd", &flash_attn_varlen_fwd);
+  m.impl("flash_attn_varlen_bwd", &flash_attn_varlen_bwd);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("flash_attn_fwd_stamped", &flash_attn_fwd_stamped);
   m.impl("flash_attn_bwd", &flash_attn_bwd);

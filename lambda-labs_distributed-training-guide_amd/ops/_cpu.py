@@ -128,26 +128,44 @@ def adamw_(p, master, g, m, v, lr, beta1, beta2, eps, wd, step, grad_scale, hype
     p.copy_(pf)
 
 
-def _attn_ref(q, k, v, cu_seqlens, scale, causal):
+def _key_ranges(cu_seqlens, k_start=None, k_len=None):
+    """[(q0, q1, k0, k1)] per sequence: self-attention by default, else explicit key ranges with
+    the bottom-right-aligned causal mask (query i of n_q attends keys <= i + n_k - n_q)."""
+    cu = cu_seqlens.tolist()
+    out = []
+    for i in range(len(cu) - 1):
+        a, b = cu[i], cu[i + 1]
+        if k_start is None:
+            out.append((a, b, a, b))
+        else:
+            ks, kl = int(k_start[i]), int(k_len[i])
+            out.append((a, b, ks, ks + kl))
+    return out
+
+
+def _mask(nq, nk):
+    # True = masked: key j > query i + (nk - nq)
+    i = torch.arange(nq)[:, None]
+    j = torch.arange(nk)[None, :]
+    return j > i + (nk - nq)
+
+
+def _attn_ref(q, k, v, cu_seqlens, scale, causal, k_start=None, k_len=None):
     """Per-sequence f32 attention; returns o (bf16/in dtype) and lse [Hq, T] (natural log)."""
     T, hq, d = q.shape
     hkv = k.shape[1]
     rep = hq // hkv
     o = torch.zeros(T, hq, d, dtype=torch.float32)
     lse = torch.full((hq, T), float("-inf"), dtype=torch.float32)
-    cu = cu_seqlens.tolist()
-    for i in range(len(cu) - 1):
-        a, b = cu[i], cu[i + 1]
+    for a, b, ka, kb in _key_ranges(cu_seqlens, k_start, k_len):
         if b <= a:
             continue
         qs = q[a:b].float().transpose(0, 1)  # [hq, s, d]
-        ks = k[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
-        vs = v[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        ks = k[ka:kb].float().transpose(0, 1).repeat_interleave(rep, 0)
+        vs = v[ka:kb].float().transpose(0, 1).repeat_interleave(rep, 0)
         sc = qs @ ks.transpose(1, 2) * scale
         if causal:
-            n = b - a
-            mask = torch.ones(n, n, dtype=torch.bool).triu(1)
-            sc = sc.masked_fill(mask, float("-inf"))
+            sc = sc.masked_fill(_mask(b - a, kb - ka), float("-inf"))
         l_ = torch.logsumexp(sc, -1)
         p = torch.exp(sc - l_[..., None])
         o[a:b] = (p @ vs).transpose(0, 1)
@@ -160,7 +178,12 @@ def flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal):
     return o.to(q.dtype), lse
 
 
-def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal):
+def flash_attn_varlen_fwd(q, k, v, cu_seqlens_q, k_start, k_len, max_seqlen_q, max_seqlen_k, scale, causal):
+    o, lse = _attn_ref(q, k, v, cu_seqlens_q, scale, causal, k_start, k_len)
+    return o.to(q.dtype), lse
+
+
+def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, k_start=None, k_len=None):
     """The kernel's semantics: P = exp(S*scale - lse) with the GIVEN lse, delta = rowsum(dO*O)
     with the GIVEN o (so a block of a larger softmax -- context parallelism -- gets the
     gradient of the full softmax)."""
@@ -168,22 +191,19 @@ def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal)
     hkv = k.shape[1]
     rep = hq // hkv
     dq = torch.zeros(T, hq, d, dtype=torch.float32)
-    dk = torch.zeros(T, hkv, d, dtype=torch.float32)
-    dv = torch.zeros(T, hkv, d, dtype=torch.float32)
-    cu = cu_seqlens.tolist()
-    for i in range(len(cu) - 1):
-        a, b = cu[i], cu[i + 1]
+    dk = torch.zeros(k.shape[0], hkv, d, dtype=torch.float32)
+    dv = torch.zeros(k.shape[0], hkv, d, dtype=torch.float32)
+    for a, b, ka, kb in _key_ranges(cu_seqlens, k_start, k_len):
         if b <= a:
             continue
         qs = q[a:b].float().transpose(0, 1)                               # [hq, s, d]
-        ks = k[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
-        vs = v[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        ks = k[ka:kb].float().transpose(0, 1).repeat_interleave(rep, 0)
+        vs = v[ka:kb].float().transpose(0, 1).repeat_interleave(rep, 0)
         dos = dout[a:b].float().transpose(0, 1)
         os_ = o[a:b].float().transpose(0, 1)
         sc = qs @ ks.transpose(1, 2) * scale
         if causal:
-            n = b - a
-            sc = sc.masked_fill(torch.ones(n, n, dtype=torch.bool).triu(1), float("-inf"))
+            sc = sc.masked_fill(_mask(b - a, kb - ka), float("-inf"))
         p = torch.exp(sc - lse[:, a:b].float()[..., None])
         dvh = p.transpose(1, 2) @ dos
         dp = dos @ vs.transpose(1, 2)
@@ -192,9 +212,14 @@ def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal)
         dqh = ds @ ks * scale
         dkh = ds.transpose(1, 2) @ qs * scale
         dq[a:b] = dqh.transpose(0, 1)
-        dk[a:b] = dkh.view(hkv, rep, b - a, d).sum(1).transpose(0, 1)
-        dv[a:b] = dvh.view(hkv, rep, b - a, d).sum(1).transpose(0, 1)
+        dk[ka:kb] += dkh.view(hkv, rep, kb - ka, d).sum(1).transpose(0, 1)
+        dv[ka:kb] += dvh.view(hkv, rep, kb - ka, d).sum(1).transpose(0, 1)
     return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
+
+
+def flash_attn_varlen_bwd(dout, q, k, v, o, lse, cu_seqlens_q, k_start, k_len, max_seqlen_q, max_seqlen_k, scale,
+                          causal):
+    return flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens_q, max_seqlen_q, scale, causal, k_start, k_len)
 
 
 def flash_attn_bwd_qkv(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal):
@@ -226,6 +251,7 @@ for _name, _fn in list(globals().items()):
     if _name in (
         "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "flash_attn_fwd", "flash_attn_bwd",
-        "flash_attn_bwd_qkv", "transpose2d", "swiglu_bwd_t", "embedding_bwd_",
+        "flash_attn_bwd_qkv", "transpose2d", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
+        "flash_attn_varlen_bwd",
     ):
         LIB.impl(_name, _fn, "CPU")

@@ -31,6 +31,13 @@ _DEFS = [
     "Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> Tensor",
     "transpose2d(Tensor x) -> Tensor",
     "embedding_bwd_(Tensor(a!) out, Tensor ids, Tensor dy) -> ()",
+    # FlashAttention-2-style varlen with explicit per-sequence key ranges (disjoint), causal mask
+    # bottom-right aligned: context parallelism's local query chunks over gathered key prefixes
+    "flash_attn_varlen_fwd(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens_q, Tensor k_start, Tensor k_len, "
+    "int max_seqlen_q, int max_seqlen_k, float scale, bool causal) -> (Tensor, Tensor)",
+    "flash_attn_varlen_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor cu_seqlens_q, "
+    "Tensor k_start, Tensor k_len, int max_seqlen_q, int max_seqlen_k, float scale, bool causal) "
+    "-> (Tensor, Tensor, Tensor)",
     "flash_attn_fwd_stamped(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
     "bool causal) -> (Tensor, Tensor, Tensor)",
 ]

@@ -8,17 +8,16 @@ other ranks' keys and values:
 
   forward   all-gather K|V over the group (one RCCL all-gather per layer -- the 8 GPUs of an
             MI355X node are fully connected, so the gather needs no ring of point-to-point
-            steps), then every local query chunk g attends to key chunks 0..g: the diagonal
-            chunk causally, the earlier ones fully.  All (query chunk, key chunk) blocks are
-            c x c, so they batch into two varlen flash-attention launches (one causal, one
-            not) and the partial outputs merge exactly through their log-sum-exps.
-  backward  the same blocks through the flash backward with the MERGED lse and output (so
-            every block's softmax and delta = rowsum(dO * O) are the global ones): dQ sums
-            over a query's blocks locally; dK / dV blocks accumulate into the full-sequence
-            buffers and are reduce-scattered back to their owners.
+            steps) and put the rows in global order (one index_select); then ONE varlen flash
+            call in which every local query chunk g is a sequence whose keys are its row's
+            prefix 0 .. (g+1)c, causal mask bottom-right aligned (the kernels' per-sequence key
+            ranges).  No per-block launches and no log-sum-exp merge.
+  backward  one varlen backward per local chunk slot (the two slots' key prefixes overlap),
+            dK / dV of the two added, one index_select back to rank order and one
+            reduce-scatter to the owners: O(1) launches per layer in both passes.
 
-Work per rank: 2*cp + 1 blocks of c x c, equal on every rank.  Dense rows only (packed
-documents would need block masks per document).
+Work per rank: the causal work of chunks r and 2cp-1-r, equal on every rank.  Dense rows only
+(packed documents would need block masks per document).
 """
 from __future__ import annotations
 
@@ -71,43 +70,49 @@ def cp_batch(input_ids: torch.Tensor, rank: int, cp: int, ignore_index: int = -1
 
 
 # ------------------------------------------------------------------------------ attention
-def _blocks(rank: int, cp: int, B: int):
-    """(row, local slot, global query chunk, key chunk) of every c x c block this rank computes."""
-    diag, off = [], []
-    for b in range(B):
-        for slot, gq in enumerate(zigzag_chunks(rank, cp)):
-            diag.append((b, slot, gq, gq))
-            off.extend((b, slot, gq, j) for j in range(gq))
-    return diag, off
+def _chunk_perm(cp: int, device) -> torch.Tensor:
+    """perm[g] = position of global chunk g in the gathered (rank, slot) order."""
+    idx = []
+    for g in range(2 * cp):
+        idx.append(2 * g if g < cp else 2 * (2 * cp - 1 - g) + 1)
+    return torch.tensor(idx, dtype=torch.long, device=device)
 
 
 def _gather_kv(k, v, group, cp, B, c):
-    """Local K|V [B*2c, H, D] -> full-sequence K, V [B, 2cp, c, H, D] in global chunk order."""
+    """Local K|V [B*2c, H, D] -> full rows [B*S, H, D] (K and V) in global token order: one
+    all-gather and one index_select, no per-chunk copies."""
     kv = torch.cat([k, v], dim=1).contiguous()                      # [B*2c, 2H, D]
     out = comm.all_gather_dim0(kv, group) if cp > 1 else kv          # [cp*B*2c, 2H, D]
     H2, D = kv.shape[1], kv.shape[2]
-    out = out.view(cp, B, 2, c, H2, D)
-    full = out.new_empty(B, 2 * cp, c, H2, D)
-    for r in range(cp):
-        a, bb = zigzag_chunks(r, cp)
-        full[:, a] = out[r, :, 0]
-        full[:, bb] = out[r, :, 1]
+    rs = out.view(cp, B, 2, c, H2, D).transpose(0, 1).reshape(B, 2 * cp, c, H2, D)  # (rank, slot) order
+    full = rs.index_select(1, _chunk_perm(cp, kv.device)).reshape(B * 2 * cp * c, H2, D)
     H = H2 // 2
-    return full[..., :H, :], full[..., H:, :]
+    return full[:, :H].contiguous(), full[:, H:].contiguous()
 
 
-def _stack(blocks, q, kf, vf):
-    """Concatenate the blocks' q / k / v as varlen sequences of c tokens each."""
-    qs = torch.stack([q[b, s] for b, s, _, _ in blocks])            # [n, c, Hq, D]
-    ks = torch.stack([kf[b, j] for b, _, _, j in blocks])
-    vs = torch.stack([vf[b, j] for b, _, _, j in blocks])
-    n, c = qs.shape[:2]
-    flat = lambda t: t.reshape(n * c, *t.shape[2:])
-    cu = torch.arange(0, (n + 1) * c, c, dtype=torch.int32, device=q.device)
-    return flat(qs), flat(ks), flat(vs), cu
+def _ranges(rank, cp, B, c, device, slots=(0, 1)):
+    """cu_seqlens over the local query chunks of `slots` (one sequence per (row, slot)) and
+    each chunk's key range: the prefix of its row up to and including its own chunk."""
+    S = 2 * cp * c
+    g = zigzag_chunks(rank, cp)
+    starts, lens = [], []
+    for b in range(B):
+        for s in slots:
+            starts.append(b * S)
+            lens.append((g[s] + 1) * c)
+    n = len(starts)
+    cu = torch.arange(0, (n + 1) * c, c, dtype=torch.int32, device=device)
+    mk = lambda xs: torch.tensor(xs, dtype=torch.int32, device=device)
+    return cu, mk(starts), mk(lens), max(lens)
 
 
 class _CPAttention(torch.autograd.Function):
+    """Each local query chunk attends to the causal prefix of its row in ONE varlen flash call
+    (per-sequence key ranges, bottom-right causal alignment): no per-block launches, no
+    log-sum-exp merge.  Backward: one varlen call per local chunk slot (their key prefixes
+    overlap, so dK / dV of the two slots are computed separately and added), then one
+    reduce-scatter of the full-row dK|dV to the owners."""
+
     @staticmethod
     def forward(ctx, q, k, v, group, cp, rank, B, scale):
         # q [B*2c, Hq, D], k / v [B*2c, Hkv, D] (local zig-zag shard, row-major over rows)
@@ -115,70 +120,38 @@ class _CPAttention(torch.autograd.Function):
         c = T // (2 * B)
         kf, vf = _gather_kv(k, v, group, cp, B, c)
         q = q.contiguous()
-        q5 = q.view(B, 2, c, Hq, D)
-        diag, off = _blocks(rank, cp, B)
-        ops = torch.ops.dtg
-        parts = []  # per block list: (o [c,Hq,D], lse [Hq,c])
-        for blocks, causal in ((diag, True), (off, False)):
-            if not blocks:
-                continue
-            qs, ks, vs, cu = _stack(blocks, q5, kf, vf)
-            o, lse = ops.flash_attn_fwd(qs, ks, vs, cu, c, scale, causal)
-            n = len(blocks)
-            parts.append((blocks, o.view(n, c, Hq, D), lse.view(Hq, n, c)))
-        # merge the blocks of each (row, slot) through their log-sum-exps
-        lse_all = q.new_full((B, 2, Hq, c), -math.inf, dtype=torch.float32)
-        for blocks, o, lse in parts:
-            for i, (b, s, _, _) in enumerate(blocks):
-                lse_all[b, s] = torch.logaddexp(lse_all[b, s], lse[:, i])
-        out = torch.zeros(B, 2, c, Hq, D, dtype=torch.float32, device=q.device)
-        for blocks, o, lse in parts:
-            for i, (b, s, _, _) in enumerate(blocks):
-                w = torch.exp(lse[:, i] - lse_all[b, s]).transpose(0, 1).unsqueeze(-1)  # [c, Hq, 1]
-                out[b, s] += w * o[i].float()
-        out = out.to(q.dtype).view(T, Hq, D)
-        ctx.save_for_backward(q, kf, vf, out, lse_all)
+        cu, ks, kl, maxk = _ranges(rank, cp, B, c, q.device)
+        out, lse = torch.ops.dtg.flash_attn_varlen_fwd(q, kf, vf, cu, ks, kl, c, maxk, scale, True)
+        ctx.save_for_backward(q, kf, vf, out, lse)
         ctx.meta = (group, cp, rank, B, c, scale, k.shape[1])
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, kf, vf, out, lse_all = ctx.saved_tensors
+        q, kf, vf, out, lse = ctx.saved_tensors
         group, cp, rank, B, c, scale, Hkv = ctx.meta
         T, Hq, D = q.shape
-        q5 = q.view(B, 2, c, Hq, D)
-        o5 = out.view(B, 2, c, Hq, D)
-        do5 = dout.contiguous().view(B, 2, c, Hq, D)
-        diag, off = _blocks(rank, cp, B)
-        ops = torch.ops.dtg
-        dq = torch.zeros(B, 2, c, Hq, D, dtype=torch.float32, device=q.device)
-        dkf = torch.zeros(kf.shape, dtype=torch.float32, device=q.device)
-        dvf = torch.zeros(vf.shape, dtype=torch.float32, device=q.device)
-        for blocks, causal in ((diag, True), (off, False)):
-            if not blocks:
-                continue
-            qs, ks, vs, cu = _stack(blocks, q5, kf, vf)
-            n = len(blocks)
-            os_ = torch.stack([o5[b, s] for b, s, _, _ in blocks]).reshape(n * c, Hq, D)
-            dos = torch.stack([do5[b, s] for b, s, _, _ in blocks]).reshape(n * c, Hq, D)
-            lse = torch.stack([lse_all[b, s] for b, s, _, _ in blocks], 1).reshape(Hq, n * c).contiguous()
-            dqs, dks, dvs = ops.flash_attn_bwd(dos, qs, ks, vs, os_, lse, cu, c, scale, causal)
-            dqs, dks, dvs = (t.view(n, c, *t.shape[1:]) for t in (dqs, dks, dvs))
-            for i, (b, s, _, j) in enumerate(blocks):
-                dq[b, s] += dqs[i].float()
-                dkf[b, j] += dks[i].float()
-                dvf[b, j] += dvs[i].float()
-        # full-sequence dK / dV -> owners: back to [cp, B, 2, c, ...] rank order, reduce-scatter
-        dkv = torch.cat([dkf, dvf], dim=3)                                 # [B, 2cp, c, 2Hkv, D]
-        send = dkv.new_empty(cp, B, 2, c, 2 * Hkv, D)
-        for r in range(cp):
-            a, bb = zigzag_chunks(r, cp)
-            send[r, :, 0] = dkv[:, a]
-            send[r, :, 1] = dkv[:, bb]
-        send = send.view(cp * B * 2 * c, 2 * Hkv, D)
-        mine = comm.reduce_scatter_dim0(send, group) if cp > 1 else send  # [B*2c, 2Hkv, D]
-        dk, dv = mine[:, :Hkv], mine[:, Hkv:]
-        return (dq.to(q.dtype).view(T, Hq, D), dk.to(q.dtype).contiguous(), dv.to(q.dtype).contiguous(),
+        sl = lambda t: t.view(B, 2, c, *t.shape[1:])
+        q5, o5, do5 = sl(q), sl(out), sl(dout.contiguous())
+        lse4 = lse.view(Hq, B, 2, c)
+        dq = torch.empty_like(q5)
+        dk = dv = None
+        for s in (0, 1):
+            cu, ks, kl, maxk = _ranges(rank, cp, B, c, q.device, slots=(s,))
+            flat = lambda t: t[:, s].reshape(B * c, *t.shape[3:])
+            dqs, dks, dvs = torch.ops.dtg.flash_attn_varlen_bwd(
+                flat(do5), flat(q5), kf, vf, flat(o5), lse4[:, :, s].reshape(Hq, B * c), cu, ks, kl, c, maxk,
+                scale, True)
+            dq[:, s] = dqs.view(B, c, Hq, D)
+            dk = dks.float() if dk is None else dk + dks.float()
+            dv = dvs.float() if dv is None else dv + dvs.float()
+        # full-row dK|dV -> (rank, slot) order -> reduce-scatter to the owners
+        S = 2 * cp * c
+        dkv = torch.cat([dk, dv], dim=1).to(q.dtype).view(B, 2 * cp, c, 2 * Hkv, D)
+        inv = torch.argsort(_chunk_perm(cp, q.device))
+        send = dkv.index_select(1, inv).view(B, cp, 2, c, 2 * Hkv, D).transpose(0, 1).reshape(cp * B * 2 * c, 2 * Hkv, D)
+        mine = comm.reduce_scatter_dim0(send.contiguous(), group) if cp > 1 else send  # [B*2c, 2Hkv, D]
+        return (dq.view(T, Hq, D), mine[:, :Hkv].contiguous(), mine[:, Hkv:].contiguous(),
                 None, None, None, None, None)
 
 
