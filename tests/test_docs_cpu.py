@@ -1,6 +1,7 @@
 """Reference doc/code drift that must not be replicated: every relative
 markdown link in the guide resolves, no chapter README points at the reference's stale
 directory names, and the SLURM script uses real `#SBATCH` directives and an existing entry point."""
+import glob
 import os
 import re
 
@@ -61,3 +62,18 @@ def test_sbatch_directives_and_entry_point():
 def test_chapter_entry_points_exist(chapter):
     d = os.path.join(ROOT, chapter)
     assert any(f.startswith("train_llm") and f.endswith(".py") for f in os.listdir(d))
+
+
+def test_cited_profile_files_exist():
+    """Every `profiles/<file>` a guide page, PARITY.md or a profile note cites must exist: the
+    numbers in the chapters are only as good as the evidence they point at."""
+    pages = list(_guide_pages()) + [os.path.join(ROOT, "PARITY.md")]
+    bad = []
+    for p in pages:
+        for m in re.finditer(r"profiles/([\w.\-/*]+[\w*])", open(p).read()):
+            t = m.group(1)
+            if t.endswith("NN.sh"):
+                continue
+            if not glob.glob(os.path.join(ROOT, "profiles", t)):
+                bad.append((os.path.relpath(p, ROOT), t))
+    assert not bad, bad
