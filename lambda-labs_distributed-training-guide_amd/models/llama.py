@@ -24,7 +24,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .. import ops
-from ..parallel import tp_comm
+from ..parallel import async_tp, tp_comm
 from .config import LlamaConfig
 
 
@@ -49,6 +49,9 @@ class TPInfo:
         self.group = group
         self.size = dist.get_world_size(group) if group is not None else 1
         self.rank = dist.get_rank(group) if group is not None else 0
+        # chunks of the overlapped sequence-parallel regions (parallel/async_tp.py; 1 = the
+        # synchronous gather -> block -> scatter path)
+        self.overlap_chunks = async_tp.DEFAULT_CHUNKS
 
     @property
     def enabled(self):
@@ -130,18 +133,45 @@ class LlamaDecoderLayer(nn.Module):
             n, res = ops.rms_norm(x, self.input_layernorm.weight, self.eps), x
         else:
             n, res = ops.add_rms_norm(x, res, self.input_layernorm.weight, self.eps)
-        if g is not None:
-            n = tp_comm.gather_seq(n, g)
-        a = self.self_attn(n, rc)
-        if g is not None:
-            a = tp_comm.scatter_seq(a, g)
+        ka, km = self._overlap_chunks(n.shape[0], rc) if g is not None else (1, 1)
+        if ka > 1:
+            a = async_tp.sp_region(n, lambda xg, j: self.self_attn(xg, _chunk_ctx(rc, xg.shape[0])), g, ka,
+                                   (self.self_attn.qkv_proj.weight, self.self_attn.o_proj.weight))
+        else:
+            if g is not None:
+                n = tp_comm.gather_seq(n, g)
+            a = self.self_attn(n, rc)
+            if g is not None:
+                a = tp_comm.scatter_seq(a, g)
         n2, res = ops.add_rms_norm(a, res, self.post_attention_layernorm.weight, self.eps)
-        if g is not None:
-            n2 = tp_comm.gather_seq(n2, g)
-        m = self.mlp(n2)
-        if g is not None:
-            m = tp_comm.scatter_seq(m, g)
+        if km > 1:
+            m = async_tp.sp_region(n2, lambda xg, j: self.mlp(xg), g, km,
+                                   (self.mlp.gate_up_proj.weight, self.mlp.down_proj.weight))
+        else:
+            if g is not None:
+                n2 = tp_comm.gather_seq(n2, g)
+            m = self.mlp(n2)
+            if g is not None:
+                m = tp_comm.scatter_seq(m, g)
         return m, res
+
+    def _overlap_chunks(self, rows_local, rc: RunCtx):
+        """(attention, MLP) chunk counts of the overlapped SP regions for this forward."""
+        k = self.tp.overlap_chunks
+        if k <= 1 or getattr(self, "_dtg_checkpointed", False) or not torch.is_grad_enabled():
+            return 1, 1
+        km = async_tp.region_chunks(rows_local, k)
+        dense = (rc.cp_group is None and rc.sp_group is None and rc.cu_seqlens is not None
+                 and rc.cu_seqlens.numel() == rc.rows + 1 and rc.max_seqlen > 0)
+        ka = async_tp.region_chunks(rows_local, k, rc.max_seqlen) if dense else 1
+        return ka, km
+
+
+def _chunk_ctx(rc: RunCtx, rows: int) -> RunCtx:
+    """RunCtx of a gathered chunk of whole dense rows (`rows` tokens = rows // S sequences)."""
+    S = rc.max_seqlen
+    b = rows // S
+    return RunCtx(rc.cos, rc.sin, rc.pos[:rows], rc.cu_seqlens[:b + 1], S, None, b, None)
 
 
 class _VocabParallelEmbedding(torch.autograd.Function):

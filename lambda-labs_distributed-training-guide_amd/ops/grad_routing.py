@@ -29,8 +29,33 @@ def _fresh(param) -> bool:
     return not getattr(param, "_dtg_grad_written", False)
 
 
+# While a chunked region back-propagates (parallel/async_tp.py), one weight receives one
+# gradient contribution per chunk; the engine must hear "final" once, after the last.
+_DEFERRED = None
+
+
+class deferred_notifications:
+    """Collect engine notifications inside the block; fire each parameter's once at exit."""
+
+    def __enter__(self):
+        global _DEFERRED
+        self.outer, _DEFERRED = _DEFERRED, {}
+        return self
+
+    def __exit__(self, *exc):
+        global _DEFERRED
+        pending, _DEFERRED = _DEFERRED, self.outer
+        if exc[0] is None:
+            for p in pending.values():
+                _mark(p)
+        return False
+
+
 def _mark(param):
     param._dtg_grad_written = True
+    if _DEFERRED is not None:
+        _DEFERRED[id(param)] = param
+        return
     cb = getattr(param, "_dtg_notify", None)
     if cb is not None:
         cb(param)

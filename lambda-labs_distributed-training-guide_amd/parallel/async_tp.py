@@ -1,0 +1,121 @@
+"""Tensor/sequence-parallel regions with their collectives overlapped by compute (async TP).
+
+A Megatron sequence-parallel sub-block is
+
+    x_local [T/n, H] --all-gather--> x [T, H] --f--> y partial [T, H] --reduce-scatter--> [T/n, H]
+
+where f is the column-parallel -> row-parallel pair (QKV -> attention -> o_proj, or
+gate_up -> SwiGLU -> down).  Run as written (`tp_comm.gather_seq` / `scatter_seq`), the
+all-gather and the reduce-scatter sit on the critical path, with every GEMM waiting for the
+whole gather and the scatter waiting for the last GEMM.
+
+`sp_region` cuts this rank's T/n rows into k chunks and pipelines them:
+
+    forward   AG(0) | AG(1) f(0) | RS(0) AG(2) f(1) | RS(1) AG(3) f(2) | ... | RS(k-1)
+    backward  the same shape: AG(dY chunk) -> f's backward -> RS(dX chunk)
+
+Chunk j of the gathered tensor is the j-th chunk of every rank ([n * T/(n k), H], rank-major),
+and f is row-local, so y's chunk j reduce-scatters straight into this rank's j-th output chunk:
+no reordering copies.  Collectives are issued with async_op on RCCL (its own stream) or on a
+side stream for the direct-peer xGMI library (utils/comm.py), and waited for only right
+before the GEMM that consumes them.  Only the first gather and the last scatter of a region
+stay exposed (2/k of the traffic instead of all of it).
+
+Each chunk's f is recorded as its own small autograd graph inside the region's forward;
+the region's backward replays them chunk by chunk between the collectives.  Weight gradients
+from the k chunks accumulate in `main_grad` (first chunk writes, later chunks add), and the
+engines' "gradient final" notifications are deferred to the end of the region, so DDP / ZeRO /
+FSDP buckets fire once per weight as before.
+
+Attention chunks must hold whole sequences (dense rows, T/n a multiple of k x S); the MLP
+region accepts any chunking.  Layers under activation checkpointing keep the synchronous
+path (a recompute must not stop half-way through a pipelined region).
+
+Reference behaviour: the reference's TP chapter runs DTensor's synchronous redistributes
+(/root/reference/06-tensor-parallel/train_llm.py:84-128); this is the MI355X design that hides
+them, not a translation.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..ops.grad_routing import deferred_notifications
+from ..utils import comm
+
+DEFAULT_CHUNKS = int(os.environ.get("DTG_TP_OVERLAP_CHUNKS", "2"))
+
+
+class _Region(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, fn, group, k, *params):
+        n = comm.world(group)
+        Tl, H = x.shape
+        Tc = Tl // k
+        xs = x.contiguous().view(k, Tc, H)
+        out = torch.empty_like(xs)
+        g = torch.empty((n * Tc, H), dtype=x.dtype, device=x.device)
+        work = comm.all_gather_dim0_into_async(g, xs[0], group)
+        leaves, ys, rs = [], [], []
+        for j in range(k):
+            work.wait()
+            cur = g
+            if j + 1 < k:  # prefetch the next chunk while this one computes
+                g = torch.empty((n * Tc, H), dtype=x.dtype, device=x.device)
+                work = comm.all_gather_dim0_into_async(g, xs[j + 1], group)
+            with torch.enable_grad():
+                leaf = cur.detach().requires_grad_(True)
+                y = fn(leaf, j)
+            rs.append(comm.reduce_scatter_dim0_into_async(out[j], y.detach(), group))
+            leaves.append(leaf)
+            ys.append(y)
+        for w in rs:
+            w.wait()
+        ctx.leaves, ctx.ys, ctx.group, ctx.k, ctx.n_params = leaves, ys, group, k, len(params)
+        return out.view(Tl, H)
+
+    @staticmethod
+    def backward(ctx, dout):
+        group, k = ctx.group, ctx.k
+        n = comm.world(group)
+        Tl, H = dout.shape
+        Tc = Tl // k
+        ds = dout.contiguous().view(k, Tc, H)
+        dx = torch.empty_like(ds)
+        g = torch.empty((n * Tc, H), dtype=dout.dtype, device=dout.device)
+        work = comm.all_gather_dim0_into_async(g, ds[0], group)
+        rs = []
+        with deferred_notifications():
+            for j in range(k):
+                work.wait()
+                cur = g
+                if j + 1 < k:
+                    g = torch.empty((n * Tc, H), dtype=dout.dtype, device=dout.device)
+                    work = comm.all_gather_dim0_into_async(g, ds[j + 1], group)
+                y, leaf = ctx.ys[j], ctx.leaves[j]
+                torch.autograd.backward(y, cur)
+                gx = leaf.grad
+                ctx.ys[j] = ctx.leaves[j] = None  # release chunk j's graph and saved activations
+                rs.append(comm.reduce_scatter_dim0_into_async(dx[j], gx, group))
+                del y, leaf, gx
+            for w in rs:
+                w.wait()
+        return (dx.view(Tl, H), None, None, None) + (None,) * ctx.n_params
+
+
+def sp_region(x, fn, group, k, params):
+    """reduce_scatter(fn(all_gather(x))) with k-chunk compute/communication overlap.
+
+    fn(x_chunk_gathered, j) -> partial output of the same row count; `params` are the weights
+    fn uses (passed so the region is part of the autograd graph even when x needs no grad)."""
+    return _Region.apply(x, fn, group, int(k), *params)
+
+
+def region_chunks(rows_local: int, k: int, row_len: int = 1) -> int:
+    """Largest chunk count <= k that splits rows_local into whole `row_len` multiples (1 = off)."""
+    units = rows_local // row_len if row_len and rows_local % row_len == 0 else 0
+    for c in range(max(1, k), 1, -1):
+        if units and units % c == 0:
+            return c
+    return 1

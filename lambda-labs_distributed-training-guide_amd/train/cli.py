@@ -47,6 +47,9 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                        help="TP/SP all-gather / reduce-scatter / all-reduce: RCCL, or the direct-peer xGMI "
                             "library (csrc/comm/xgmi.hip; one node per TP group)")
         p.add_argument("--tp-comm-mb", default=256, type=int, help="xGMI workspace per rank (largest TP message)")
+        p.add_argument("--tp-overlap-chunks", default=2, type=int,
+                       help="row chunks of the overlapped sequence-parallel regions (parallel/async_tp.py): the "
+                            "all-gather / reduce-scatter of one chunk runs under the GEMMs of the next; 1 = off")
     if chapter == "deepspeed":
         p.add_argument("--local_rank", type=int, default=None)
         p.add_argument("--deepspeed", action="store_true", help="accepted for launcher compatibility")

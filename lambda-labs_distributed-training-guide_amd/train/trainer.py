@@ -137,6 +137,9 @@ def _build(args, chapter, device, world):
         model = build_model(cfg, device=device, **{f"{seq[0]}_group": seq[1]})
     else:
         model = build_model(cfg, device=device, tp_group=tp_group)
+    if tp_group is not None and hasattr(model, "tp"):
+        model.tp.overlap_chunks = max(1, getattr(args, "tp_overlap_chunks", 2))
+        LOGGER.info(f"tp overlap: {model.tp.overlap_chunks} chunks per sequence-parallel region")
     model._dtg_seq = seq
     model._dtg_pp = None
     if pp > 1:

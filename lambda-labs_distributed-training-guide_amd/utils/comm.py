@@ -129,3 +129,78 @@ def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group=None, async
         out.copy_(full.view(-1)[r * n:(r + 1) * n].view_as(out))
         return _DoneWork() if async_op else None
     return dist.reduce_scatter_tensor(out, full, group=group, async_op=async_op)
+
+
+# ------------------------------------------------------------------------------------------------
+# Asynchronous dim-0 gather / scatter for the overlapped tensor-parallel regions
+# (parallel/async_tp.py).  Each returns a work object whose wait() makes the CURRENT stream wait
+# for the result (RCCL: the PG's own stream; xGMI: a side stream of this module), so compute
+# issued between the call and wait() overlaps the transfer.
+# ------------------------------------------------------------------------------------------------
+_SIDE = {}
+
+
+def _side_stream(device):
+    s = _SIDE.get(device.index)
+    if s is None:
+        s = _SIDE[device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
+class _StreamWork:
+    def __init__(self, event, device):
+        self.event, self.device = event, device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_event(self.event)
+        return True
+
+    def is_completed(self):
+        return self.event.query()
+
+
+def _on_side_stream(fn, *tensors):
+    dev = tensors[0].device
+    cur = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        fn()
+    for t in tensors:  # the caching allocator must not hand these out before the side stream is done
+        t.record_stream(side)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    return _StreamWork(ev, dev)
+
+
+def all_gather_dim0_into_async(out: torch.Tensor, x: torch.Tensor, group=None):
+    """out [n * c, ...] <- the c-row x of every rank, rank-major."""
+    if world(group) == 1:
+        out.copy_(x)
+        return _DoneWork()
+    c = _xgmi_for(group, x, x.numel() * x.element_size())
+    if c is not None:
+        return _on_side_stream(lambda: c.all_gather_into(out, x), out, x)
+    if backend_of(group) == "gloo":
+        dist.all_gather_into_tensor(out, x, group=group)
+        return _DoneWork()
+    return dist.all_gather_into_tensor(out, x, group=group, async_op=True)
+
+
+def reduce_scatter_dim0_into_async(out: torch.Tensor, x: torch.Tensor, group=None):
+    """out [c, ...] <- sum over ranks of rows [rank * c, (rank + 1) * c) of x [n * c, ...].
+    `x` is not modified."""
+    n = world(group)
+    if n == 1:
+        out.copy_(x)
+        return _DoneWork()
+    c = _xgmi_for(group, x, x.numel() * x.element_size())
+    if c is not None:
+        return _on_side_stream(lambda: c.reduce_scatter_into(out, x), out, x)
+    if backend_of(group) == "gloo":
+        y = x.clone()
+        dist.all_reduce(y, group=group)
+        r, rows = rank(group), out.shape[0]
+        out.copy_(y[r * rows:(r + 1) * rows])
+        return _DoneWork()
+    return dist.reduce_scatter_tensor(out, x, group=group, async_op=True)

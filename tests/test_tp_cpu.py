@@ -10,7 +10,7 @@ from test_engines_cpu import _batches, _train
 TOL = dict(atol=3e-4, rtol=1e-3)
 
 
-def _tp_worker(rank, world, tp, model_name, batches, engine_mode, steps_loss_only=False):
+def _tp_worker(rank, world, tp, model_name, batches, engine_mode, chunks=None):
     import torch.distributed as dist
 
     from dtg.models import build_model, resolve_config
@@ -23,6 +23,13 @@ def _tp_worker(rank, world, tp, model_name, batches, engine_mode, steps_loss_onl
     full = build_model(cfg, device="cpu", dtype=torch.float32)
     model = build_model(cfg, device="cpu", dtype=torch.float32, tp_group=tp_group, init=False)
     model.load_state_dict(shard_full_state_dict(full.state_dict(), cfg, tp_rank, tp))
+    calls = []
+    if chunks is not None:
+        model.tp.overlap_chunks = chunks
+        import dtg.parallel.async_tp as atp
+
+        orig = atp.sp_region
+        atp.sp_region = lambda x, fn, g, k, params: calls.append(k) or orig(x, fn, g, k, params)
     if engine_mode == "fsdp":
         from dtg.parallel.fsdp import FullyShard
 
@@ -42,10 +49,10 @@ def _tp_worker(rank, world, tp, model_name, batches, engine_mode, steps_loss_onl
         losses.append(out.loss.item())
     if engine_mode == "fsdp":
         sd = eng.full_state_dict(rank0_only=False)
-        return sd, losses, tp_rank
+        return sd, losses, tp_rank, calls
     if hasattr(eng, "wait_param_gather"):
         eng.wait_param_gather()  # ZeRO leaves the last all-gather in flight until the next forward
-    return {n: p.detach().clone() for n, p in model.named_parameters()}, losses, tp_rank
+    return {n: p.detach().clone() for n, p in model.named_parameters()}, losses, tp_rank, calls
 
 
 @pytest.mark.parametrize("world,tp,mode", [(2, 2, "ddp"), (4, 2, "zero"), (4, 2, "ddp"), (4, 2, "fsdp"), (2, 1, "fsdp")])
@@ -66,6 +73,37 @@ def test_tp_sp_matches_single(world, tp, mode):
     for r in res[tp:]:
         for n, v in r[0].items():
             assert torch.equal(v, res[r[2]][0][n])
+
+
+@pytest.mark.parametrize("chunks,mode", [(1, "ddp"), (4, "ddp"), (4, "fsdp")])
+def test_tp_overlap_chunks_match_single(chunks, mode):
+    """The overlapped SP regions (parallel/async_tp.py) at k = 4 chunks -- attention regions of
+    one sequence per chunk, MLP regions of 16 rows -- and the synchronous path (k = 1) both
+    train like the single-process model; engine notifications fire once per weight."""
+    from dtg.models import resolve_config
+    from dtg.parallel.tensor_parallel import unshard_state_dicts
+
+    model_name = "llama-tiny-d128"
+    cfg = resolve_config(model_name)
+    batches = _batches(cfg.vocab_size, 8, 16)
+    ref, ref_losses = _train(model_name, "single", 0, 1, batches)
+    res = run_distributed(_tp_worker, 2, 2, model_name, batches, mode, chunks)
+    # every layer ran both regions overlapped (k = 4), or none did (k = 1)
+    assert res[0][3] == ([4] * (2 * cfg.num_hidden_layers * len(batches)) if chunks > 1 else []), res[0][3]
+    for a, b in zip(res[0][1], ref_losses):
+        assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (res[0][1], ref_losses)
+    shards = [r[0] for r in sorted(res, key=lambda r: r[2])]
+    full = unshard_state_dicts(shards, cfg)
+    for n in ref:
+        torch.testing.assert_close(full[n], ref[n], **TOL, msg=n)
+
+
+def test_region_chunks():
+    from dtg.parallel.async_tp import region_chunks
+
+    assert region_chunks(64, 4) == 4 and region_chunks(64, 3) == 2 and region_chunks(63, 2) == 1
+    assert region_chunks(2048, 4, 1024) == 2 and region_chunks(1024, 4, 1024) == 1
+    assert region_chunks(100, 4, 64) == 1 and region_chunks(64, 1) == 1
 
 
 def test_shard_unshard_roundtrip():

@@ -14,9 +14,9 @@ pytestmark = pytest.mark.gpu
 MODEL = "llama-tiny-d128"
 
 
-def _ids(vocab):
+def _ids(vocab, rows=2):
     g = torch.Generator().manual_seed(0)
-    return torch.randint(0, vocab, (2, 64), generator=g)
+    return torch.randint(0, vocab, (rows, 64), generator=g)
 
 
 def _grads(model):
@@ -30,7 +30,7 @@ def _run(model, eng, ids):
     return out.loss.item()
 
 
-def _worker(rank, world):
+def _worker(rank, world, rows=2, chunks=1):
     import torch.distributed as dist
 
     from dtg.models import build_model, resolve_config
@@ -48,8 +48,9 @@ def _worker(rank, world):
     full = build_model(cfg, device="cpu", dtype=torch.bfloat16)
     model = build_model(cfg, device=dev, tp_group=tp_group, init=False)
     model.load_state_dict(shard_full_state_dict(full.state_dict(), cfg, tp_rank, 2))
+    model.tp.overlap_chunks = chunks  # > 1: overlapped SP regions, xGMI collectives on a side stream
     eng = DataParallel(model, mode="single", tp_group=tp_group, broadcast_from_rank0=False)
-    loss = _run(model, eng, _ids(cfg.vocab_size).to(dev))
+    loss = _run(model, eng, _ids(cfg.vocab_size, rows).to(dev))
     torch.cuda.synchronize()
     dcomm._XGMI[tp_group].check()
     res = (loss, _grads(model), tp_rank)
@@ -57,7 +58,8 @@ def _worker(rank, world):
     return res
 
 
-def test_tp2_xgmi_matches_single_device(cuda):
+@pytest.mark.parametrize("rows,chunks", [(2, 1), (4, 2)])
+def test_tp2_xgmi_matches_single_device(cuda, rows, chunks):
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel
     from dtg.parallel.tensor_parallel import unshard_state_dicts
@@ -66,9 +68,9 @@ def test_tp2_xgmi_matches_single_device(cuda):
     torch.manual_seed(0)
     ref = build_model(cfg, device="cpu", dtype=torch.bfloat16).to(cuda)
     eng = DataParallel(ref, mode="single")
-    ref_loss = _run(ref, eng, _ids(cfg.vocab_size).to(cuda))
+    ref_loss = _run(ref, eng, _ids(cfg.vocab_size, rows).to(cuda))
     ref_g = _grads(ref)
-    res = run_distributed(_worker, 2)
+    res = run_distributed(_worker, 2, rows, chunks)
     assert abs(res[0][0] - ref_loss) < 2e-2 * abs(ref_loss) and res[0][0] == res[1][0]
     shards = [r[1] for r in sorted(res, key=lambda r: r[2])]
     full = unshard_state_dicts(shards, cfg)
