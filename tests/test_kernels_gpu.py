@@ -216,12 +216,14 @@ def test_adamw(cuda, state_dtype, master, n):
         assert (tp.detach().float() - pm.float()).abs().max().item() <= 2 * 2**-7 * tp.detach().float().abs().max().item()
 
 
-def _attn_case(cuda, seqlens, hq, hkv, D, causal, stride_extra=0):
+def _attn_case(cuda, seqlens, hq, hkv, D, causal, stride_extra=0, qscale=1.0):
     torch.manual_seed(0)
     T = sum(seqlens)
     cu = torch.tensor([0] + list(torch.tensor(seqlens).cumsum(0).tolist()), dtype=torch.int32)
     cols = (hq + 2 * hkv) * D + stride_extra
-    qkv = torch.randn(T, cols).bfloat16()
+    qkv = torch.randn(T, cols)
+    qkv[:, : hq * D] *= qscale
+    qkv = qkv.bfloat16()
     q = qkv[:, : hq * D].view(T, hq, D)
     k = qkv[:, hq * D:(hq + hkv) * D].view(T, hkv, D)
     v = qkv[:, (hq + hkv) * D:(hq + 2 * hkv) * D].view(T, hkv, D)
@@ -251,6 +253,18 @@ def test_flash_attn_d128_gqa(cuda, seqlens, causal):
 @pytest.mark.parametrize("seqlens", [[512, 300]])
 def test_flash_attn_d64_mha(cuda, seqlens):
     _attn_case(cuda, seqlens, hq=4, hkv=4, D=64, causal=True)
+
+
+@pytest.mark.parametrize("variant", ["narrow", "wide", "qlds"])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attn_fwd_variants(cuda, variant, causal, monkeypatch):
+    """Every forward variant (DTG_FA_FWD, read per call) against the fp32 reference, including
+    logits with a large dynamic range (qscale 8: the running max keeps growing by more than the
+    lazy-rescale threshold, so the rescale path runs on many tiles)."""
+    monkeypatch.setenv("DTG_FA_FWD", variant)
+    _attn_case(cuda, [100, 257, 667], hq=8, hkv=2, D=128, causal=causal, stride_extra=8)
+    _attn_case(cuda, [512, 300], hq=4, hkv=4, D=64, causal=causal)
+    _attn_case(cuda, [1024, 77], hq=4, hkv=2, D=128, causal=causal, qscale=8.0)
 
 
 def test_flash_attn_bwd_qkv_fused(cuda):
