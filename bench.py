@@ -63,6 +63,10 @@ def parse(argv=None):
     ap.add_argument("--fsdp-mem-seq", type=int, default=1024)
     ap.add_argument("--fsdp-mem-steps", type=int, default=3, help="0 skips the FSDP memory phase")
     ap.add_argument("--numel-to-wrap", type=int, default=100_000_000)
+    # After the timed region, N > 1 only: RCCL reduce-scatter / all-gather / all-reduce bus
+    # bandwidth at these message sizes (MiB), so the multi-GPU run also measures the curve the
+    # 256 MiB gradient-bucket default is chosen from.  Empty string = off.
+    ap.add_argument("--coll-sweep-mb", default="16,64,256,1024")
     return ap.parse_args(argv)
 
 
@@ -200,6 +204,38 @@ def fsdp_memory_phase(args, torch, dist, device, world, rank, cuda):
     return dict(valley=valley, peak=peak, ms=ms, model=cfg.hf_name or args.fsdp_mem_model)
 
 
+def collective_sweep(args, torch, dist, device, world, cuda):
+    """[{op, mib, us, busbw_gbs}] measured on every rank (rank 0's numbers reported), nccl-tests
+    bus-bandwidth conventions: reduce-scatter / all-gather x (W-1)/W, all-reduce x 2(W-1)/W."""
+    sizes = [int(x) for x in args.coll_sweep_mb.split(",") if x.strip()]
+    out = []
+    dt_ = torch.bfloat16 if cuda else torch.float32
+    esz = 2 if cuda else 4
+    for mib in sizes:
+        n = (mib << 20) // esz // world * world
+        x = torch.randn(n, device=device).to(dt_)
+        shard = torch.empty(n // world, device=device, dtype=dt_)
+        full = torch.empty(n, device=device, dtype=dt_)
+        ops = {"reduce_scatter": (lambda: dist.reduce_scatter_tensor(shard, x), (world - 1) / world),
+               "all_gather": (lambda: dist.all_gather_into_tensor(full, shard), (world - 1) / world),
+               "all_reduce": (lambda: dist.all_reduce(x), 2 * (world - 1) / world)}
+        if not cuda:  # gloo (CPU rehearsal) has no reduce-scatter
+            ops.pop("reduce_scatter")
+        for op, (fn, factor) in ops.items():
+            iters = 5 if mib >= 256 else 10
+            fn()
+            _sync(dist, world, cuda)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            _sync(dist, world, cuda)
+            dt = (time.perf_counter() - t0) / iters
+            out.append({"op": op, "mib": mib, "us": round(dt * 1e6, 1),
+                        "busbw_gbs": round((n * esz) / dt / 1e9 * factor, 1)})
+        del x, shard, full
+    return out
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -253,6 +289,7 @@ def main(argv=None):
     gc.collect()
     if cuda:
         torch.cuda.empty_cache()
+    coll = collective_sweep(args, torch, dist, device, world, cuda) if (world > 1 and args.coll_sweep_mb) else None
     mem = None
     if args.fsdp_mem_steps > 0:
         mem = fsdp_memory_phase(args, torch, dist, device, world, rank, cuda)
@@ -308,6 +345,8 @@ def main(argv=None):
             "rank_ms_per_step": {"max": round(1000 * elapsed / args.steps, 2),
                                  "min": round(1000 * min(r[0] for r in rows) / args.steps, 2)},
         }
+        if coll is not None:
+            rec["collectives"] = coll
         if mem is not None:
             rec["fsdp_mem"] = {"model": mem["model"], "batch_per_gpu": args.fsdp_mem_batch,
                                "seq_len": args.fsdp_mem_seq, "wrap": f"size>={args.numel_to_wrap}",

@@ -13,7 +13,7 @@ from _dist import free_port
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--batch-size", "2", "--seq-len", "64",
         "--tunableop", "off", "--fsdp-mem-model", "llama-tiny", "--fsdp-mem-batch", "2", "--fsdp-mem-seq", "64",
-        "--fsdp-mem-steps", "1", "--numel-to-wrap", "10000"]
+        "--fsdp-mem-steps", "1", "--numel-to-wrap", "10000", "--coll-sweep-mb", "1,2"]
 
 
 def _json_lines(out):
@@ -29,6 +29,12 @@ def _check(rec, n):
     assert rec["world_size_seen_by_pg"] == n and len(rec["rank_devices"]) == n
     assert rec["rank_ms_per_step"]["max"] >= rec["rank_ms_per_step"]["min"] > 0
     assert rec["fsdp_mem"]["peak_gb_max_rank"] >= rec["fsdp_mem"]["valley_gb_max_rank"] >= 0
+    if n > 1:  # the collective sweep after the timed region (gloo: all-gather + all-reduce)
+        ops = {(c["op"], c["mib"]) for c in rec["collectives"]}
+        assert {("all_gather", 1), ("all_reduce", 2)} <= ops
+        assert all(c["busbw_gbs"] > 0 for c in rec["collectives"])
+    else:
+        assert "collectives" not in rec
 
 
 @pytest.mark.slow
