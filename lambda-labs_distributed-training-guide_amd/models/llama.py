@@ -167,6 +167,11 @@ class LlamaDecoderLayer(nn.Module):
         return ka, km
 
 
+def tp_seed_offset(tp_rank: int) -> int:
+    """Seed offset of TP rank `tp_rank`'s sharded-weight initialisation (0 for rank 0)."""
+    return 1_000_003 * int(tp_rank)
+
+
 def _chunk_ctx(rc: RunCtx, rows: int) -> RunCtx:
     """RunCtx of a gathered chunk of whole dense rows (`rows` tokens = rows // S sequences)."""
     S = rc.max_seqlen
@@ -234,8 +239,22 @@ class LlamaForCausalLM(nn.Module):
 
     @torch.no_grad()
     def init_weights(self):
+        """Under TP every rank holds a different slice of each sharded matrix, so every rank must
+        draw different values: the ranks of a TP group share the global RNG seed (same data order,
+        same replicated norms), and the sharded weights are drawn with that seed offset by the TP
+        rank (`tp_seed_offset`).  With identical draws the column / row blocks of all TP ranks
+        would be copies of each other, receive identical gradients and never diverge."""
+        off = tp_seed_offset(self.tp.rank) if self.tp.enabled else 0
         for name, p in self.named_parameters():
-            if p.device.type != "meta":
+            if p.device.type == "meta":
+                continue
+            if off:
+                state = torch.random.get_rng_state()
+                torch.manual_seed((int(torch.randint(0, 2**62, (1,)).item()) + off) % 2**63)
+                self.init_param(name, p)
+                torch.random.set_rng_state(state)
+                torch.randint(0, 2**62, (1,))  # advance the shared stream identically on all ranks
+            else:
                 self.init_param(name, p)
 
     def lm_head_weight(self):

@@ -202,6 +202,13 @@ class FullyShard:
                 if p is not None:
                     where.setdefault(id(p), []).append((mm, pn))
         init_fn = init_fn or getattr(model, "init_param", None) or _default_init(model)
+        # 2-D (FSDP x TP): each TP rank initialises its own slice of every sharded matrix, so the
+        # per-parameter seed is offset by the TP rank (see LlamaForCausalLM.init_weights)
+        tp_off = 0
+        if tp_group is not None and comm.world(tp_group) > 1:
+            from ..models.llama import tp_seed_offset
+
+            tp_off = tp_seed_offset(comm.rank(tp_group))
         for u in all_units:
             full = torch.zeros(u.numel, dtype=self.dtype, device=self.device)
             u.full = full
@@ -210,7 +217,7 @@ class FullyShard:
                 n = math.prod(u.shapes[i])
                 view = full[u.offsets[i]:u.offsets[i] + n].view(u.shapes[i])
                 if src.device.type == "meta":
-                    torch.manual_seed(seed + 7919 * u.idx + i)
+                    torch.manual_seed(seed + 7919 * u.idx + i + tp_off)
                     init_fn(u.names[i], view)
                 else:
                     with torch.no_grad():

@@ -98,6 +98,41 @@ def test_tp_overlap_chunks_match_single(chunks, mode):
         torch.testing.assert_close(full[n], ref[n], **TOL, msg=n)
 
 
+def _init_worker(rank, world, engine):
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.tensor_parallel import make_mesh
+
+    dp_group, tp_group, _, tp_rank, _ = make_mesh(world)
+    cfg = resolve_config("llama-tiny")
+    torch.manual_seed(0)
+    if engine == "fsdp":
+        from dtg.parallel.fsdp import FullyShard
+
+        with torch.device("meta"):
+            m = build_model(cfg, tp_group=tp_group, init=False, dtype=torch.float32)
+        eng = FullyShard(m, group=dp_group, tp_group=tp_group, device="cpu", seed=0)
+        sd = eng.full_state_dict(rank0_only=False)
+    else:
+        m = build_model(cfg, device="cpu", dtype=torch.float32, tp_group=tp_group)
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    return sd, tp_rank
+
+
+@pytest.mark.parametrize("engine", ["ddp", "fsdp"])
+def test_tp_random_init_differs_across_tp_ranks(engine):
+    """Random init under TP: every sharded matrix gets different values on each TP rank (else
+    the TP ranks' column / row blocks are copies that receive identical gradients forever);
+    replicated norms stay identical."""
+    res = run_distributed(_init_worker, 2, engine)
+    (a, _), (b, _) = sorted(res, key=lambda r: r[1])
+    for k in a:
+        if k.endswith("layernorm.weight") or k == "norm.weight":
+            assert torch.equal(a[k], b[k]), k
+        else:
+            assert not torch.equal(a[k], b[k]), k
+            assert abs(a[k].std().item() - b[k].std().item()) < 0.2 * a[k].std().item(), k
+
+
 def test_region_chunks():
     from dtg.parallel.async_tp import region_chunks
 
