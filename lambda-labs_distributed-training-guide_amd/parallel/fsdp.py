@@ -133,7 +133,7 @@ class FullyShard:
                  device=None, reshard_after_forward: bool = True, cpu_offload: bool = False,
                  state_dtype=torch.bfloat16, init_fn: Optional[Callable] = None, seed: int = 0,
                  prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None, replicate_group=None,
-                 overlap_cpu_step: bool = True, force_collectives: bool = False):
+                 overlap_cpu_step: bool = True, force_collectives: bool = False, offload_params: bool = True):
         self.module = model
         self.group = group
         # HYBRID_SHARD (ZeRO++-style): shard inside `group` (one node's xGMI island), replicate
@@ -149,6 +149,14 @@ class FullyShard:
         self._coll = self.world > 1 or (force_collectives and dist.is_initialized())
         self.reshard_after_forward = reshard_after_forward
         self.cpu_offload = cpu_offload
+        # offload_params=False (ZeRO-Offload layout, the MI355X default in chapter 05 when it fits):
+        # the bf16 parameter shard stays resident in HBM as well; gradients and AdamW state live
+        # on the host, the host update writes a pinned master copy, and each updated unit shard is
+        # copied back on a side stream while the rest of the backward / host update runs.  Per step
+        # that is one D2H of gradients and one H2D of parameters instead of two H2D parameter passes
+        # (forward and backward gathers) plus the D2H -- and the forward reads HBM only.
+        self.offload_params = bool(cpu_offload and offload_params)
+        self.resident = bool(cpu_offload and not offload_params)
         self.overlap_cpu_step = overlap_cpu_step
         self._hparams = None  # bound by FlatAdamW: () -> (lr, beta1, beta2, eps, weight_decay)
         self._in_no_sync = False
@@ -190,6 +198,9 @@ class FullyShard:
         self.shard_grads = torch.zeros(total, dtype=self.dtype, device=home, pin_memory=pin)
         self.exp_avg = torch.zeros(total, dtype=state_dtype, device=home)
         self.exp_avg_sq = torch.zeros(total, dtype=state_dtype, device=home)
+        # resident mode: the GPU copy every gather reads (the host shard_params is the master)
+        self.gpu_params = torch.zeros(total, dtype=self.dtype, device=self.device) if self.resident else None
+        self._h2d_stream = torch.cuda.Stream(device=self.device) if (self.resident and self.device.type == "cuda") else None
         o = 0
         for u in all_units:
             u.shard_off = o
@@ -240,6 +251,8 @@ class FullyShard:
             self.shard_params[u.shard_off:u.shard_off + u.shard_numel].copy_(my)
             u.params_src = None
             self._free_full(u)
+        if self.resident:
+            self.gpu_params.copy_(self.shard_params)
         # ---- hooks
         for u in self.units:
             u.module.register_forward_pre_hook(self._make_pre_forward(u))
@@ -275,8 +288,15 @@ class FullyShard:
         if u.gathered or u.gather_work is not None:
             return
         self._alloc_full(u)
-        shard = self._shard_view(u, self.shard_params)
-        if self.cpu_offload:
+        if self.resident:
+            ev = getattr(u, "h2d_event", None)
+            if ev is not None:  # the updated shard's copy back from the host update
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                u.h2d_event = None
+            shard = self._shard_view(u, self.gpu_params)
+        else:
+            shard = self._shard_view(u, self.shard_params)
+        if self.cpu_offload and not self.resident:
             shard = shard.to(self.device, non_blocking=True)
         with torch.autograd._unsafe_preserve_version_counter(u.full):
             if not self._coll:
@@ -457,9 +477,26 @@ class FullyShard:
             self._cpu_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="dtg-host-adamw")
         step, scale, (lr, b1, b2, eps, wd) = self._bwd_step
         sl = slice(u.shard_off, u.shard_off + u.shard_numel)
-        self._cpu_futs.append(self._cpu_pool.submit(
-            adamw_step_cpu, self.shard_params[sl], self.shard_grads[sl], self.exp_avg[sl], self.exp_avg_sq[sl],
-            lr=lr, step=step, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, grad_scale=scale))
+
+        def update():
+            adamw_step_cpu(self.shard_params[sl], self.shard_grads[sl], self.exp_avg[sl], self.exp_avg_sq[sl],
+                           lr=lr, step=step, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, grad_scale=scale)
+            if self.resident:
+                self._copy_back(u, sl)
+
+        self._cpu_futs.append(self._cpu_pool.submit(update))
+
+    def _copy_back(self, u, sl):
+        """Resident mode: updated host shard -> its HBM copy on the H2D side stream; the next
+        gather of the unit waits for the event (`_issue_gather`)."""
+        if self._h2d_stream is None:
+            self.gpu_params[sl].copy_(self.shard_params[sl])
+            return
+        with torch.cuda.device(self.device), torch.cuda.stream(self._h2d_stream):
+            self.gpu_params[sl].copy_(self.shard_params[sl], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._h2d_stream)
+        u.h2d_event = ev
 
     def backward(self, loss, last_microbatch: Optional[bool] = None):
         """Backward of one micro-batch.  With CPU offload and `overlap_cpu_step`, the host AdamW
@@ -547,9 +584,22 @@ class FullyShard:
             adamw_step_cpu(self.shard_params, self.shard_grads, self.exp_avg, self.exp_avg_sq, lr=lr,
                            step=self.step_count, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
                            grad_scale=grad_scale)
+            if self.resident:
+                self.sync_params_after_load()
         else:
             adamw_step(self.shard_params, self.shard_grads, self.exp_avg, self.exp_avg_sq, lr=lr, step=self.step_count,
                        beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale)
+
+    def sync_params_after_load(self):
+        """Resident offload: the host master shard changed (checkpoint / pretrained load, a
+        post-backward host step) -> refresh the HBM copy the gathers read."""
+        if not self.resident:
+            return
+        for u in self.all_units:
+            u.h2d_event = None
+            if not u.in_backward:
+                self._free_full(u)
+        self.gpu_params.copy_(self.shard_params)
 
     # ------------------------------------------------------------------ state
     def optimizer_state(self):

@@ -40,6 +40,10 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                        help="full: FULL_SHARD over all ranks; hybrid: shard within --shard-size ranks (one node), "
                             "replicate across nodes (HYBRID_SHARD)")
         p.add_argument("--shard-size", default=None, type=int, help="ranks per shard group (default LOCAL_WORLD_SIZE)")
+        p.add_argument("--offload-params", default="auto", choices=["auto", "on", "off"],
+                       help="with --cpu-offload on: on = parameters on the host too (reference); off = parameter "
+                            "shard resident in HBM, only gradients + AdamW state offloaded; auto = off when the "
+                            "shard fits a third of HBM")
     if chapter == "07":
         p.add_argument("--tp", default=8, type=int)
     if chapter in ("06", "07"):

@@ -59,8 +59,25 @@ def _deepspeed_overrides(args):
     args.zero_stage = int(zero.get("stage", 3))
     off = (zero.get("offload_optimizer") or {}).get("device", "none")
     args.cpu_offload = "on" if (off == "cpu" and args.zero_stage == 3) else "off"
+    # ZeRO-Offload (optimizer only) keeps parameters on the device; offload_param moves them too
+    args.offload_params = "on" if (zero.get("offload_param") or {}).get("device", "none") == "cpu" else "off"
     args.grad_accum = int(cfg.get("gradient_accumulation_steps", args.grad_accum))
     return args
+
+
+def _offload_params(args, model, dp_group, device) -> bool:
+    """--offload-params on|off|auto for CPU offload.  auto (default): keep the bf16 parameter
+    shard resident in HBM when it takes at most a third of the device's memory -- on a 288 GB
+    MI355X that is every model up to ~430 B parameters per 8 GPUs -- and offload it too beyond."""
+    mode = getattr(args, "offload_params", "auto")
+    if mode != "auto":
+        return mode == "on"
+    n = sum(p.numel() for p in model.parameters())
+    w = torch.distributed.get_world_size(dp_group) if torch.distributed.is_initialized() else 1
+    if device.type != "cuda":
+        return True
+    hbm = torch.cuda.get_device_properties(device).total_memory
+    return 2 * n / w > hbm / 3
 
 
 def _scheduler(args, opt):
@@ -157,10 +174,15 @@ def _build(args, chapter, device, world):
         from ..parallel.fsdp import FullyShard
 
         policy = "size" if chapter == "04" else "transformer"
+        cpu_offload = getattr(args, "cpu_offload", "off") == "on"
+        offload_params = _offload_params(args, model, dp_group, device) if cpu_offload else True
+        if cpu_offload:
+            LOGGER.info("cpu offload: " + ("parameters, gradients and AdamW state on the host" if offload_params else
+                                           "gradients and AdamW state on the host, parameter shard resident in HBM"))
         engine = FullyShard(model, group=dp_group, tp_group=tp_group, policy=policy,
                             min_num_params=getattr(args, "numel_to_wrap", 100_000_000), device=device,
                             reshard_after_forward=args.reshard_after_forward == "on",
-                            cpu_offload=getattr(args, "cpu_offload", "off") == "on", seed=args.seed,
+                            cpu_offload=cpu_offload, offload_params=offload_params, seed=args.seed,
                             replicate_group=replicate_group)
         style = "sharded"
     else:

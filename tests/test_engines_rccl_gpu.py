@@ -115,7 +115,7 @@ def test_rccl_world1_grad_accumulation(cuda, kind):
         assert torch.equal(params[n], v), (kind, n)
 
 
-def _offload_worker(rank, world, overlap, accum):
+def _offload_worker(rank, world, overlap, accum, offload_params=True):
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import FlatAdamW
     from dtg.parallel.fsdp import FullyShard
@@ -125,7 +125,7 @@ def _offload_worker(rank, world, overlap, accum):
     cfg = resolve_config(MODEL)
     torch.manual_seed(0)
     model = build_model(cfg, device=dev)
-    eng = FullyShard(model, device=dev, cpu_offload=True, overlap_cpu_step=overlap)
+    eng = FullyShard(model, device=dev, cpu_offload=True, overlap_cpu_step=overlap, offload_params=offload_params)
     opt = FlatAdamW(eng, lr=1e-3)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))  # lr changes every step
     stepped = []
@@ -153,3 +153,15 @@ def test_fsdp_cpu_offload_overlap_bit_identical_on_gpu(cuda, accum):
         assert all(on[r][1]) and not any(off[r][1])
         for n, t in off[r][0].items():
             assert torch.equal(on[r][0][n], t), (r, n)
+
+
+@pytest.mark.parametrize("overlap,accum", [(True, 1), (True, 2), (False, 1)])
+def test_fsdp_resident_param_offload_bit_identical_on_gpu(cuda, overlap, accum):
+    """offload_params=False: shards resident in HBM, host AdamW from the worker thread copying
+    each updated unit back on the H2D side stream while backward kernels are still running; the
+    next forward's gathers wait on those copies == the full offload, bit for bit."""
+    res = run_distributed(_offload_worker, 2, overlap, accum, False)
+    full = run_distributed(_offload_worker, 2, overlap, accum, True)
+    for r in range(2):
+        for n, t in full[r][0].items():
+            assert torch.equal(res[r][0][n], t), (r, n)

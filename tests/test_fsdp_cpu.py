@@ -123,14 +123,15 @@ def test_hybrid_shard_matches_single():
             torch.testing.assert_close(sd[n], ref[n], **TOL, msg=f"rank {r} {n}")
 
 
-def _offload_train(rank, world, batches, overlap, accum, offload=True):
+def _offload_train(rank, world, batches, overlap, accum, offload=True, offload_params=True):
     from dtg.models import build_model
     from dtg.parallel.data_parallel import FlatAdamW
     from dtg.parallel.fsdp import FullyShard
 
     torch.manual_seed(0)
     model = build_model("llama-tiny", device="cpu", dtype=torch.float32)
-    eng = FullyShard(model, cpu_offload=offload, device="cpu", overlap_cpu_step=overlap)
+    eng = FullyShard(model, cpu_offload=offload, device="cpu", overlap_cpu_step=overlap,
+                     offload_params=offload_params)
     opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))  # lr changes every step
     stepped_in_bwd = []
@@ -160,6 +161,18 @@ def test_fsdp_offload_overlapped_host_step_is_bit_identical(accum):
         assert all(on[r][1]) and not any(off[r][1])
         for n, t in off[r][0].items():
             assert torch.equal(on[r][0][n], t), f"rank {r} {n}"
+
+
+@pytest.mark.parametrize("overlap,accum", [(True, 1), (False, 2), (True, 2)])
+def test_fsdp_resident_param_offload_is_bit_identical(overlap, accum):
+    """offload_params=False (ZeRO-Offload layout: parameter shard resident in device memory,
+    gradients + AdamW on the host, updated shards copied back) == the full offload."""
+    batches = _batches(512, 4, 32, n=3)
+    res = run_distributed(_offload_train, 2, batches, overlap, accum, True, False)
+    full = run_distributed(_offload_train, 2, batches, overlap, accum, True, True)
+    for r in range(2):
+        for n, t in full[r][0].items():
+            assert torch.equal(res[r][0][n], t), f"rank {r} {n}"
 
 
 @pytest.mark.parametrize("offload", [False, True])
