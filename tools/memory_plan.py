@@ -19,7 +19,9 @@ from dtg.models import resolve_config  # noqa: E402
 HBM_GB = 288.0
 
 
-def plan(model, world=8, tp=1, strategy="fsdp", batch=1, seq=4096, ac=False, offload=False):
+def plan(model, world=8, tp=1, strategy="fsdp", batch=1, seq=4096, ac=False, offload=False, resident_params=False):
+    """offload: gradients + AdamW state (+ parameters unless resident_params) in host memory;
+    resident_params keeps the bf16 parameter shard in HBM and a master copy on the host."""
     c = resolve_config(model)
     P = c.num_params()
     H, I, L = c.hidden_size, c.intermediate_size, c.num_hidden_layers
@@ -43,7 +45,9 @@ def plan(model, world=8, tp=1, strategy="fsdp", batch=1, seq=4096, ac=False, off
     host = 0.0
     if offload:
         host = params + grads + opt
-        params = grads = opt = 0.0
+        grads = opt = 0.0
+        if not resident_params:
+            params = 0.0
     total = params + grads + opt + gather + acts + logits
     return {
         "model": c.hf_name or model, "params_B": P / 1e9, "world": world, "tp": tp, "dp": dp, "strategy": strategy,
@@ -63,10 +67,12 @@ def main():
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--ac", action="store_true")
     ap.add_argument("--offload", action="store_true")
+    ap.add_argument("--resident-params", action="store_true",
+                    help="with --offload: parameter shard stays in HBM (--offload-params off / auto)")
     ap.add_argument("--exact", action="store_true",
                     help="also print the exact FSDP unit layout (dtg.parallel.plan on a meta-device model)")
     a = ap.parse_args()
-    r = plan(a.model, a.world, a.tp, a.strategy, a.batch, a.seq, a.ac, a.offload)
+    r = plan(a.model, a.world, a.tp, a.strategy, a.batch, a.seq, a.ac, a.offload, a.resident_params)
     for k, v in r.items():
         print(f"{k:20s} {v:.2f}" if isinstance(v, float) else f"{k:20s} {v}")
     if a.exact and a.tp == 1:
