@@ -201,6 +201,8 @@ class FullyShard:
         # resident mode: the GPU copy every gather reads (the host shard_params is the master)
         self.gpu_params = torch.zeros(total, dtype=self.dtype, device=self.device) if self.resident else None
         self._h2d_stream = torch.cuda.Stream(device=self.device) if (self.resident and self.device.type == "cuda") else None
+        self._d2h_stream = torch.cuda.Stream(device=self.device) if (cpu_offload and self.device.type == "cuda") else None
+        self._d2h_events = []
         o = 0
         for u in all_units:
             u.shard_off = o
@@ -432,14 +434,28 @@ class FullyShard:
     def _complete_rs(self, u, work, out, first, direct):
         if work is not None:
             work.wait()
+        ev = None
         if not direct:
             gs = self._shard_view(u, self.shard_grads)
-            if first:
+            if first and self._d2h_stream is not None and gs.device.type == "cpu":
+                # offload: the gradient shard goes to pinned host memory on a side stream, so the
+                # host thread keeps queueing backward kernels; the host update (or step()) waits
+                # for the copy's event
+                cur = torch.cuda.current_stream(self.device)
+                self._d2h_stream.wait_stream(cur)
+                with torch.cuda.stream(self._d2h_stream):
+                    gs.copy_(out, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self._d2h_stream)
+                out.record_stream(self._d2h_stream)
+                self._d2h_events.append(ev)
+            elif first:
                 gs.copy_(out)
             else:
+                self._sync_d2h()  # the previous micro-batch's copy into gs must have landed
                 gs.add_(out.to(gs.device))
         if self._bwd_step is not None:
-            self._submit_host_step(u)
+            self._submit_host_step(u, ev)
         u.full_grad = None
         for p in u.params:
             p.main_grad = None
@@ -468,7 +484,12 @@ class FullyShard:
         finally:
             self._in_no_sync = prev
 
-    def _submit_host_step(self, u):
+    def _sync_d2h(self):
+        evs, self._d2h_events = self._d2h_events, []
+        for ev in evs:
+            ev.synchronize()
+
+    def _submit_host_step(self, u, ev=None):
         import concurrent.futures as cf
 
         from ..ops.adamw import adamw_step_cpu
@@ -479,6 +500,8 @@ class FullyShard:
         sl = slice(u.shard_off, u.shard_off + u.shard_numel)
 
         def update():
+            if ev is not None:  # this unit's gradient shard has landed in host memory
+                ev.synchronize()
             adamw_step_cpu(self.shard_params[sl], self.shard_grads[sl], self.exp_avg[sl], self.exp_avg_sq[sl],
                            lr=lr, step=step, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, grad_scale=scale)
             if self.resident:
@@ -539,6 +562,7 @@ class FullyShard:
         futs, self._cpu_futs = self._cpu_futs, []
         for f in futs:
             f.result()
+        self._sync_d2h()
 
     def zero_grad(self):
         self._join_host_steps()  # never let a host update race the next forward's shard reads
@@ -568,6 +592,7 @@ class FullyShard:
             self._join_host_steps()
             return
         self.step_count += 1
+        self._sync_d2h()
         if grad_scale is None:
             grad_scale = 1.0 / (self.world * self.replicas * max(1, self.accum_count))
         if self.replicas > 1:
