@@ -28,6 +28,9 @@ ALIASES = {
     "meta-llama/llama-3.1-405b": "llama-3.1-405b",
     "meta-llama/llama-3.2-3b-instruct": "llama-3.2-3b",
     "meta-llama/llama-3.2-3b": "llama-3.2-3b",
+    "qwen/qwen2.5-0.5b": "qwen2.5-0.5b",
+    "qwen/qwen2.5-7b": "qwen2.5-7b",
+    "mistralai/mistral-7b-v0.3": "mistral-7b-v0.3",
 }
 
 
@@ -48,7 +51,10 @@ class LlamaConfig:
     initializer_range: float = 0.02
     eos_token_id: Optional[int] = None
     hf_name: str = ""
+    # llama (Llama-2/3/3.1/3.2), mistral (Llama layout + sliding_window), qwen2 (+ q/k/v bias)
     model_type: str = "llama"
+    attention_bias: bool = False  # q/k/v projection bias (Qwen2); o_proj never has one here
+    sliding_window: Optional[int] = None  # Mistral: keys within this distance (None = full causal)
 
     def __post_init__(self):
         if self.head_dim is None:
@@ -58,6 +64,8 @@ class LlamaConfig:
         h, i, v, L = self.hidden_size, self.intermediate_size, self.vocab_size, self.num_hidden_layers
         d = self.head_dim
         attn = h * (self.num_attention_heads + 2 * self.num_key_value_heads) * d + self.num_attention_heads * d * h
+        if self.attention_bias:
+            attn += (self.num_attention_heads + 2 * self.num_key_value_heads) * d
         layer = attn + 3 * h * i + 2 * h
         return v * h * (1 if self.tie_word_embeddings else 2) + L * layer + h
 
@@ -108,10 +116,28 @@ class GPT2Config:
         return 6 * (self.num_params() - self.n_positions * self.n_embd) + 6 * self.n_layer * self.n_embd * seq_len
 
 
+LLAMA_FAMILY = ("llama", "mistral", "qwen2")
+
+
 def _from_dict(d: dict):
+    """HF config dict -> our config.  The Llama layout covers llama, mistral and qwen2
+    (RMSNorm, RoPE, GQA, SwiGLU); anything else is refused instead of silently mis-built."""
     d = dict(d)
     mt = d.get("model_type", "llama")
-    cls = GPT2Config if mt == "gpt2" else LlamaConfig
+    if mt == "gpt2":
+        cls = GPT2Config
+    elif mt in LLAMA_FAMILY:
+        cls = LlamaConfig
+        if mt == "qwen2":
+            d.setdefault("attention_bias", True)  # Qwen2 always has q/k/v biases
+            if not d.get("use_sliding_window", False):
+                d["sliding_window"] = None
+        if mt == "llama":
+            d["sliding_window"] = None
+        if d.get("mlp_bias"):
+            raise ValueError("mlp_bias=True is not supported (no Llama-family checkpoint uses it)")
+    else:
+        raise ValueError(f"unsupported model_type {mt!r}; supported: {', '.join(LLAMA_FAMILY)}, gpt2")
     fields = {f.name for f in dataclasses.fields(cls)}
     return cls(**{k: v for k, v in d.items() if k in fields})
 

@@ -21,6 +21,12 @@ def llama_to_hf(sd: dict, cfg: LlamaConfig) -> dict:
             out["model." + pre + "q_proj.weight"] = q
             out["model." + pre + "k_proj.weight"] = kk
             out["model." + pre + "v_proj.weight"] = vv
+        elif k.endswith("self_attn.qkv_proj.bias"):
+            pre = k[: -len("qkv_proj.bias")]
+            q, kk, vv = v.reshape(-1).split([nq * d, nkv * d, nkv * d], dim=0)
+            out["model." + pre + "q_proj.bias"] = q
+            out["model." + pre + "k_proj.bias"] = kk
+            out["model." + pre + "v_proj.bias"] = vv
         elif k.endswith("mlp.gate_up_proj.weight"):
             pre = k[: -len("gate_up_proj.weight")]
             g, u = v.chunk(2, dim=0)
@@ -42,6 +48,10 @@ def llama_from_hf(hf_sd: dict, cfg: LlamaConfig) -> dict:
         p = f"model.layers.{i}."
         out[f"layers.{i}.self_attn.qkv_proj.weight"] = torch.cat(
             [hf_sd[p + "self_attn.q_proj.weight"], hf_sd[p + "self_attn.k_proj.weight"], hf_sd[p + "self_attn.v_proj.weight"]], 0)
+        if p + "self_attn.q_proj.bias" in hf_sd:
+            out[f"layers.{i}.self_attn.qkv_proj.bias"] = torch.cat(
+                [hf_sd[p + "self_attn.q_proj.bias"], hf_sd[p + "self_attn.k_proj.bias"],
+                 hf_sd[p + "self_attn.v_proj.bias"]], 0)[:, None]
         out[f"layers.{i}.self_attn.o_proj.weight"] = hf_sd[p + "self_attn.o_proj.weight"]
         out[f"layers.{i}.mlp.gate_up_proj.weight"] = torch.cat([hf_sd[p + "mlp.gate_proj.weight"], hf_sd[p + "mlp.up_proj.weight"]], 0)
         out[f"layers.{i}.mlp.down_proj.weight"] = hf_sd[p + "mlp.down_proj.weight"]
@@ -73,15 +83,31 @@ def gpt2_to_hf(sd: dict, cfg: GPT2Config) -> dict:
 
 
 def hf_llama_config(cfg: LlamaConfig):
-    from transformers import LlamaConfig as HFLlamaConfig
-
-    return HFLlamaConfig(
+    """The transformers config of the same architecture (LlamaConfig / MistralConfig / Qwen2Config)."""
+    common = dict(
         vocab_size=cfg.vocab_size, hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
         num_hidden_layers=cfg.num_hidden_layers, num_attention_heads=cfg.num_attention_heads,
-        num_key_value_heads=cfg.num_key_value_heads, head_dim=cfg.head_dim, rms_norm_eps=cfg.rms_norm_eps,
+        num_key_value_heads=cfg.num_key_value_heads, rms_norm_eps=cfg.rms_norm_eps,
         rope_theta=cfg.rope_theta, rope_scaling=cfg.rope_scaling, max_position_embeddings=cfg.max_position_embeddings,
-        tie_word_embeddings=cfg.tie_word_embeddings, use_cache=False, attention_bias=False, mlp_bias=False,
-    )
+        tie_word_embeddings=cfg.tie_word_embeddings, use_cache=False)
+    if cfg.model_type == "qwen2":
+        from transformers import Qwen2Config
+
+        return Qwen2Config(use_sliding_window=cfg.sliding_window is not None, sliding_window=cfg.sliding_window, **common)
+    if cfg.model_type == "mistral":
+        from transformers import MistralConfig
+
+        return MistralConfig(head_dim=cfg.head_dim, sliding_window=cfg.sliding_window, **common)
+    from transformers import LlamaConfig as HFLlamaConfig
+
+    return HFLlamaConfig(head_dim=cfg.head_dim, attention_bias=cfg.attention_bias, mlp_bias=False, **common)
+
+
+def hf_causal_lm_class(cfg: LlamaConfig):
+    import transformers
+
+    return {"qwen2": transformers.Qwen2ForCausalLM, "mistral": transformers.MistralForCausalLM}.get(
+        cfg.model_type, transformers.LlamaForCausalLM)
 
 
 def hf_gpt2_config(cfg: GPT2Config):

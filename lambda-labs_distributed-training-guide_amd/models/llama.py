@@ -78,10 +78,15 @@ class LlamaAttention(nn.Module):
         self.d = cfg.head_dim
         h = cfg.hidden_size
         self.qkv_proj = Weight((self.nq + 2 * self.nkv) * self.d, h, device=device, dtype=dtype)
+        if cfg.attention_bias:  # Qwen2: q/k/v biases, fused like the weight; a [rows, 1] column so
+            # that tensor-parallel sharding and checkpoint geometry treat it like the weight's rows
+            self.qkv_proj.bias = nn.Parameter(torch.empty((self.nq + 2 * self.nkv) * self.d, 1, device=device,
+                                                          dtype=dtype))
         self.o_proj = Weight(h, self.nq * self.d, device=device, dtype=dtype)
 
     def forward(self, x, rc: RunCtx):
-        qkv = ops.linear(x, self.qkv_proj.weight)
+        b = getattr(self.qkv_proj, "bias", None)
+        qkv = ops.linear(x, self.qkv_proj.weight, None if b is None else b.view(-1))
         if rc.cp_group is not None:  # context parallel: zig-zag sequence shards
             from ..parallel.context_parallel import cp_attention
 
@@ -136,7 +141,7 @@ class LlamaDecoderLayer(nn.Module):
         ka, km = self._overlap_chunks(n.shape[0], rc) if g is not None else (1, 1)
         if ka > 1:
             a = async_tp.sp_region(n, lambda xg, j: self.self_attn(xg, _chunk_ctx(rc, xg.shape[0])), g, ka,
-                                   (self.self_attn.qkv_proj.weight, self.self_attn.o_proj.weight))
+                                   tuple(p for p in self.self_attn.parameters()))
         else:
             if g is not None:
                 n = tp_comm.gather_seq(n, g)
@@ -234,6 +239,8 @@ class LlamaForCausalLM(nn.Module):
         """HF Llama init: normal(0, initializer_range) for matrices/embeddings, ones for norms."""
         if name.endswith("layernorm.weight") or name == "norm.weight":
             t.fill_(1.0)
+        elif name.endswith(".bias"):
+            t.zero_()
         else:
             t.normal_(0.0, self.config.initializer_range)
 
@@ -299,6 +306,10 @@ class LlamaForCausalLM(nn.Module):
         B, S = input_ids.shape
         T = B * S
         dev = input_ids.device
+        sw = self.config.sliding_window
+        if sw is not None and max(S, int(max_seqlen or 0)) > sw:
+            raise ValueError(f"{self.config.model_type}: sequences of {max(S, int(max_seqlen or 0))} tokens exceed the "
+                             f"sliding window ({sw}); only full-causal attention is implemented (rows <= window)")
         sp = self.sp_group is not None
         if sp:  # attention sees the full rows: describe them (positions gathered from the slices)
             from ..parallel.ulysses import sp_world

@@ -48,11 +48,12 @@ def _segments(name: str, cfg, tp_rank: int, tp_size: int):
     """Our (TP-local, fused) parameter as a stack of row segments of HF tensors:
     [(hf_name, local_rows, hf_row_offset, (c0, c1) or None)]."""
     d = cfg.head_dim
-    if name.endswith("self_attn.qkv_proj.weight"):
-        p = "model." + name[: -len("qkv_proj.weight")]
+    if name.endswith("self_attn.qkv_proj.weight") or name.endswith("self_attn.qkv_proj.bias"):
+        suf = name.rsplit(".", 1)[1]  # weight | bias
+        p = "model." + name[: -len("qkv_proj." + suf)]
         nq, nkv = cfg.num_attention_heads * d // tp_size, cfg.num_key_value_heads * d // tp_size
-        return [(p + "q_proj.weight", nq, tp_rank * nq, None), (p + "k_proj.weight", nkv, tp_rank * nkv, None),
-                (p + "v_proj.weight", nkv, tp_rank * nkv, None)]
+        return [(p + "q_proj." + suf, nq, tp_rank * nq, None), (p + "k_proj." + suf, nkv, tp_rank * nkv, None),
+                (p + "v_proj." + suf, nkv, tp_rank * nkv, None)]
     if name.endswith("mlp.gate_up_proj.weight"):
         p = "model." + name[: -len("gate_up_proj.weight")]
         i = cfg.intermediate_size // tp_size
@@ -143,6 +144,8 @@ def _row_width(name: str, cfg, tp_size: int):
     """Columns of our TP-local parameter (None for 1-D)."""
     if name.endswith("layernorm.weight") or name == "norm.weight":
         return None
+    if name.endswith("qkv_proj.bias"):
+        return 1  # stored as a [rows, 1] column
     if name.endswith("self_attn.o_proj.weight"):
         return cfg.num_attention_heads * cfg.head_dim // tp_size
     if name.endswith("mlp.down_proj.weight"):

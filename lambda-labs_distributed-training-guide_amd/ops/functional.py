@@ -84,9 +84,17 @@ class _LinearBias(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, b = ctx.saved_tensors
-        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
-        dw = route_weight_grad_mm(w, dy, x) if ctx.needs_input_grad[1] else None
-        db = route_param_grad(b, dy.sum(0)) if ctx.needs_input_grad[2] else None
+        dx_tn, dw_tn = _bwd_layout(x, w)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy, ops.transpose2d(w).t()) if dx_tn else torch.mm(dy, w)
+        if ctx.needs_input_grad[1]:
+            if dw_tn and _tn_ok(dy):
+                dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
+            else:
+                dw = route_weight_grad_mm(w, dy, x)
+        if ctx.needs_input_grad[2]:
+            db = route_param_grad(b, dy.sum(0, dtype=torch.float32).to(dy.dtype))
         return dx, dw, db
 
 

@@ -60,7 +60,7 @@ def shard_full_state_dict(full: Dict[str, torch.Tensor], cfg, tp_rank: int, tp_s
     nq, nkv = cfg.num_attention_heads, cfg.num_key_value_heads
     out = {}
     for k, v in full.items():
-        if k.endswith("self_attn.qkv_proj.weight"):
+        if k.endswith("self_attn.qkv_proj.weight") or k.endswith("self_attn.qkv_proj.bias"):
             q, kk, vv = v.split([nq * d, nkv * d, nkv * d], 0)
             out[k] = torch.cat([_rows(q, tp_rank, tp_size), _rows(kk, tp_rank, tp_size), _rows(vv, tp_rank, tp_size)], 0)
         elif k.endswith("mlp.gate_up_proj.weight"):
@@ -83,7 +83,7 @@ def unshard_state_dicts(shards, cfg) -> Dict[str, torch.Tensor]:
     out = {}
     for k in shards[0]:
         parts = [s[k] for s in shards]
-        if k.endswith("self_attn.qkv_proj.weight"):
+        if k.endswith("self_attn.qkv_proj.weight") or k.endswith("self_attn.qkv_proj.bias"):
             qs, ks, vs = zip(*[p.split([nq * d, nkv * d, nkv * d], 0) for p in parts])
             out[k] = torch.cat(list(qs) + list(ks) + list(vs), 0)
         elif k.endswith("mlp.gate_up_proj.weight"):

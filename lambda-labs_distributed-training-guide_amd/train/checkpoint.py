@@ -5,7 +5,7 @@ Directory layout under `{save_dir}/{experiment_name}/` follows the reference per
   * dp   (02):        model.pt (rank 0), lr_scheduler.pt, state.json, rng.pt + the optimizer
                       state as a sharded `checkpoint/` (the reference never saved it and then
                       crashed on resume)
-  * sharded (04-07):  checkpoint/ (.metadata + one file per rank), lr_scheduler.pt, state.json, rng.pt
+  * sharded (04-07):  checkpoint/ (index.json + shard_rNNNNN.pt per rank), lr_scheduler.pt, state.json, rng.pt
 
 Sharded format `dtg-sharded-v2` (this framework's own; not torch DCP, whose file names it does
 not borrow): every rank writes `checkpoint/shard_rNNNNN.pt` holding, for each parameter slice it
@@ -106,7 +106,7 @@ def _shard_file(rank: int) -> str:
 
 def param_kind(name: str) -> str:
     """How the tensor-parallel plan (parallel/tensor_parallel.py) splits a Llama parameter."""
-    if name.endswith("self_attn.qkv_proj.weight"):
+    if name.endswith("self_attn.qkv_proj.weight") or name.endswith("self_attn.qkv_proj.bias"):
         return "qkv"
     if name.endswith("mlp.gate_up_proj.weight"):
         return "gate_up"

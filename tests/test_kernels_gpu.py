@@ -282,14 +282,21 @@ def test_flash_attn_bwd_qkv_fused(cuda):
     _close(fused, ref, 0, 0, "fused dqkv layout")
 
 
-def test_llama_tiny_gpu_matches_cpu(cuda):
+@pytest.mark.parametrize("name", ["llama-tiny-d128", "qwen2-tiny"])
+def test_llama_tiny_gpu_matches_cpu(cuda, name):
+    """Whole model on the GPU kernels (bf16) vs the fp32 CPU model: loss and gradient norm
+    (qwen2-tiny adds the q/k/v bias through the fused linear-with-bias backward)."""
     from dtg.models import build_model
 
     torch.manual_seed(0)
-    cpu = build_model("llama-tiny-d128", device="cpu", dtype=torch.float32)
-    gpu = build_model("llama-tiny-d128", device=cuda)
+    cpu = build_model(name, device="cpu", dtype=torch.float32)
+    with torch.no_grad():
+        for n, p in cpu.named_parameters():
+            if n.endswith(".bias"):
+                p.normal_(0, 0.1)
+    gpu = build_model(name, device=cuda)
     gpu.load_state_dict({k: v.bfloat16() for k, v in cpu.state_dict().items()})
-    ids = torch.randint(0, 1000, (2, 256))
+    ids = torch.randint(0, cpu.config.vocab_size, (2, 256))
     lc = cpu(input_ids=ids, labels=ids).loss
     lg = gpu(input_ids=ids.to(cuda), labels=ids.to(cuda)).loss
     assert abs(lc.item() - lg.item()) < 0.05

@@ -24,7 +24,12 @@ def _write_hf(d, model_name):
 
     cfg = resolve_config(model_name)
     torch.manual_seed(123)
-    sd = build_model(cfg, device="cpu", dtype=torch.float32).state_dict()
+    m = build_model(cfg, device="cpu", dtype=torch.float32)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith(".bias"):
+                p.normal_(0, 0.1)  # non-zero biases, so a mis-sliced bias cannot pass
+    sd = m.state_dict()
     hf = llama_to_hf(sd, cfg)
     if cfg.tie_word_embeddings:
         hf.pop("lm_head.weight")  # HF tied checkpoints store the matrix once
@@ -57,7 +62,8 @@ def _load_worker(rank, world, kind, model_name, d):
 
 
 @pytest.mark.parametrize("kind,world,model_name", [("single", 1, "llama-tiny"), ("zero", 2, "llama-tiny"),
-                                                   ("fsdp", 2, "llama-tiny"), ("fsdp", 2, "llama-tiny-d128")])
+                                                   ("fsdp", 2, "llama-tiny"), ("fsdp", 2, "llama-tiny-d128"),
+                                                   ("fsdp", 2, "qwen2-tiny")])
 def test_load_pretrained_engines(kind, world, model_name):
     with tempfile.TemporaryDirectory() as d:
         ref = _write_hf(d, model_name)
@@ -84,7 +90,7 @@ def _tp_worker(rank, world, model_name, d):
     return {k: v.detach().clone() for k, v in m.state_dict().items()}, tp_rank
 
 
-@pytest.mark.parametrize("model_name", ["llama-tiny", "llama-tiny-d128"])
+@pytest.mark.parametrize("model_name", ["llama-tiny", "llama-tiny-d128", "qwen2-tiny"])
 def test_load_pretrained_tp2(model_name):
     from dtg.models import resolve_config
     from dtg.parallel.tensor_parallel import unshard_state_dicts

@@ -4,17 +4,23 @@ import torch
 
 import dtg  # noqa: F401
 from dtg.models import build_model, count_valid_labels, resolve_config
-from dtg.models.hf_compat import gpt2_to_hf, hf_gpt2_config, hf_llama_config, llama_from_hf, llama_to_hf
+from dtg.models.hf_compat import (gpt2_to_hf, hf_causal_lm_class, hf_gpt2_config, hf_llama_config, llama_from_hf,
+                                  llama_to_hf)
 
 
-@pytest.mark.parametrize("name", ["llama-tiny", "llama-tiny-d128"])
+@pytest.mark.parametrize("name", ["llama-tiny", "llama-tiny-d128", "qwen2-tiny", "mistral-tiny"])
 def test_llama_matches_hf_loss_logits_grads(name):
-    from transformers import LlamaForCausalLM as HF
-
+    """Llama-family models (Llama, Qwen2 with q/k/v biases, Mistral within its window) against
+    the transformers implementation of the same architecture."""
     torch.manual_seed(0)
     cfg = resolve_config(name)
     m = build_model(cfg, device="cpu", dtype=torch.float32)
-    hf = HF(hf_llama_config(cfg)).float()
+    if cfg.attention_bias:  # zero-initialised like HF; random here so the bias path is exercised
+        with torch.no_grad():
+            for n_, p in m.named_parameters():
+                if n_.endswith(".bias"):
+                    p.normal_(0, 0.1)
+    hf = hf_causal_lm_class(cfg)(hf_llama_config(cfg)).float()
     hf.load_state_dict(llama_to_hf(m.state_dict(), cfg), strict=True)
     ids = torch.randint(0, cfg.vocab_size, (2, 40))
     a = m(input_ids=ids, labels=ids, return_logits=True)
@@ -30,8 +36,22 @@ def test_llama_matches_hf_loss_logits_grads(name):
         torch.testing.assert_close(ga[n], p.grad, atol=1e-4, rtol=1e-3, msg=n)
 
 
-def test_llama_hf_roundtrip_state_dict():
-    cfg = resolve_config("llama-tiny")
+def test_unsupported_model_type_is_refused():
+    with pytest.raises(ValueError, match="unsupported model_type"):
+        resolve_config("llama-tiny", model_type="gemma")
+
+
+def test_sliding_window_beyond_window_is_refused():
+    cfg = resolve_config("mistral-tiny")  # sliding_window 64
+    m = build_model(cfg, device="cpu", dtype=torch.float32)
+    ids = torch.randint(0, cfg.vocab_size, (1, 65))
+    with pytest.raises(ValueError, match="sliding window"):
+        m(input_ids=ids, labels=ids)
+
+
+@pytest.mark.parametrize("name", ["llama-tiny", "qwen2-tiny"])
+def test_llama_hf_roundtrip_state_dict(name):
+    cfg = resolve_config(name)
     m = build_model(cfg, device="cpu", dtype=torch.float32)
     sd = m.state_dict()
     back = llama_from_hf(llama_to_hf(sd, cfg), cfg)

@@ -55,12 +55,16 @@ def _tp_worker(rank, world, tp, model_name, batches, engine_mode, chunks=None):
     return {n: p.detach().clone() for n, p in model.named_parameters()}, losses, tp_rank, calls
 
 
-@pytest.mark.parametrize("world,tp,mode", [(2, 2, "ddp"), (4, 2, "zero"), (4, 2, "ddp"), (4, 2, "fsdp"), (2, 1, "fsdp")])
-def test_tp_sp_matches_single(world, tp, mode):
+@pytest.mark.parametrize("world,tp,mode,model_name", [(2, 2, "ddp", "llama-tiny-d128"), (4, 2, "zero", "llama-tiny-d128"),
+                                                      (4, 2, "ddp", "llama-tiny-d128"), (4, 2, "fsdp", "llama-tiny-d128"),
+                                                      (2, 1, "fsdp", "llama-tiny-d128"), (2, 2, "ddp", "qwen2-tiny"),
+                                                      (4, 2, "fsdp", "qwen2-tiny")])
+def test_tp_sp_matches_single(world, tp, mode, model_name):
+    """llama-tiny-d128: tied embeddings + GQA (4 q / 2 kv heads), llama3 rope; qwen2-tiny adds
+    the q/k/v biases (column-parallel, split like the weight's q / k / v row blocks)."""
     from dtg.models import resolve_config
     from dtg.parallel.tensor_parallel import unshard_state_dicts
 
-    model_name = "llama-tiny-d128"  # tied embeddings + GQA (4 q / 2 kv heads), llama3 rope
     cfg = resolve_config(model_name)
     batches = _batches(cfg.vocab_size, 4, 32)
     ref, ref_losses = _train(model_name, "single", 0, 1, batches)
