@@ -107,7 +107,9 @@ def test_num_valid_hint_matches_internal_count():
 def test_bundled_configs_param_counts():
     # parameter counts of the reference's models
     expect = {"gpt2": 124.44e6, "llama-2-7b": 6.74e9, "llama-2-70b": 68.98e9, "llama-3-8b": 8.03e9,
-              "llama-3.1-405b": 405.85e9, "llama-3.2-3b": 3.21e9}
+              "llama-3.1-405b": 405.85e9, "llama-3.2-3b": 3.21e9,
+              # published sizes of the other bundled Llama-layout families
+              "qwen2.5-0.5b": 0.494e9, "qwen2.5-7b": 7.62e9, "mistral-7b-v0.3": 7.25e9}
     for name, n in expect.items():
         got = resolve_config(name).num_params()
         assert abs(got - n) / n < 0.01, (name, got)
