@@ -1,8 +1,9 @@
 // Flash-style causal attention, forward and backward, for gfx950 (replaces
 // the flash-attn / SDPA dependencies N2, N3 of the reference).
 //
-// Supports GQA (Hq a multiple of Hkv), head_dim 64/128, and variable-length packed
-// sequences through `cu_seqlens` (the rime packed path: documents restart their position
+// Supports GQA (Hq a multiple of Hkv), head_dim 64/128, causal sliding windows (Mistral; a
+// separate WIN instantiation, so the plain causal kernels are unchanged), and variable-length
+// packed sequences through `cu_seqlens` (the rime packed path: documents restart their position
 // ids at each EOS) -- a dense [B, S] batch is just cu_seqlens = arange(B+1)*S.
 // Layout: token-major q [T, Hq, D], k/v [T, Hkv, D] with an arbitrary token stride, so q, k
 // and v are read straight out of the fused QKV projection output with no copies.
@@ -27,6 +28,7 @@
 //    sequence read as zeros from the range check, with no per-row branches.
 #include "common.h"
 
+#include <climits>
 #include <cstdlib>
 #include <type_traits>
 
@@ -229,6 +231,7 @@ struct FwdParams {
   float c2;  // softmax scale * log2(e)
   long long* stamps;  // diagnostic path only (flash_attn_fwd_stamped): 6 words per workgroup
   const int *kstart, *klen;  // optional per-sequence key ranges (see KeyRange)
+  int window;  // causal sliding window (Mistral): query i sees keys in (i + off - window, i + off]; 0 = none
 };
 
 // In-kernel timeline stamps (CDNA guide §7 'In-kernel stamps'): constant-rate 100 MHz clock,
@@ -246,7 +249,9 @@ __device__ __forceinline__ void fa_stamp(long long* st, int slot, int k) {
 constexpr int kFwdBQ = 128;  // query rows per work item (4 waves x 32)
 constexpr int kFwdBK = 64;   // keys per K/V tile
 
-template <int D, bool CAUSAL, bool WIDE, bool QLDS>
+// WIN: sliding-window instantiation (only launched with P.window > 0); without it every window
+// term folds to a compile-time 0 and the kernel is the plain causal one.
+template <int D, bool CAUSAL, bool WIDE, bool QLDS, bool WIN = false>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int TILE = kFwdBK * RB;
@@ -283,6 +288,9 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
 
   const int kv_end = CAUSAL ? min(klen, q0 + kFwdBQ + koff_c) : klen;
   const int ntiles = (kv_end + kFwdBK - 1) / kFwdBK;
+  // sliding window: the first key any query of this block sees is q0 + koff_c - window + 1
+  const int win = (CAUSAL && WIN) ? P.window : 0;
+  const int t_begin = win > 0 ? max(0, q0 + koff_c - win + 1) / kFwdBK : 0;
   const uint16_t* kbase = P.k + (int64_t)kr.start * P.sk + (int64_t)kvh * D;
   const uint16_t* vbase = P.v + (int64_t)kr.start * P.sv + (int64_t)kvh * D;
 
@@ -292,8 +300,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   float m = -INFINITY, l = 0.f;
 
   Stager<kFwdBK, D, 256> sk, sv;
-  sk.load(kbase, P.sk, klen);
-  sv.load(vbase, P.sv, klen);
+  sk.load(kbase + (int64_t)t_begin * kFwdBK * P.sk, P.sk, klen - t_begin * kFwdBK);
+  sv.load(vbase + (int64_t)t_begin * kFwdBK * P.sv, P.sv, klen - t_begin * kFwdBK);
   if constexpr (QLDS) sq.store(smem + 2 * TILE);  // the second K/V buffer is free until tile 0 ends
   sk.store(smem);
   sv.store(smem + TILE);
@@ -318,7 +326,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
     }
     const char* K = smem + B * 2 * TILE;
     const char* V = K + TILE;
-    if (!CAUSAL || kt0 <= wave_qmax + koff_c) {  // wave-uniform skip of tiles above the diagonal
+    // wave-uniform skip of tiles above the diagonal (or entirely before every query's window)
+    if ((!CAUSAL || kt0 <= wave_qmax + koff_c) && (win == 0 || kt0 + kFwdBK - 1 >= wave_q0 + koff_c - win + 1)) {
       f32x16 s[2];
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -332,13 +341,17 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       }
       pipeline_reads<2 * NC, 1, 4>();
       __builtin_amdgcn_sched_barrier(0);
-      if ((CAUSAL && kt0 + kFwdBK - 1 > wave_q0 + koff_c) || kt0 + kFwdBK > klen) {
+      if ((CAUSAL && kt0 + kFwdBK - 1 > wave_q0 + koff_c) || kt0 + kFwdBK > klen ||
+          (win > 0 && kt0 < wave_qmax + koff_c - win + 1)) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-          // key = kt0 + 32 kt + acc_row is masked when key > min(qrow + koff_c, klen - 1)
+          // key = kt0 + 32 kt + acc_row is masked when key > min(qrow + koff_c, klen - 1), or
+          // (sliding window) key < qrow + koff_c - win + 1
           const int lim = (CAUSAL ? min(qrow + koff_c, klen - 1) : klen - 1) - (kt0 + 32 * kt + 4 * h);
+          const int llim = win > 0 ? qrow + koff_c - win + 1 - (kt0 + 32 * kt + 4 * h) : INT_MIN;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) s[kt][i] = acc_row0(i) > lim ? -INFINITY : s[kt][i];
+          for (int i = 0; i < 16; ++i)
+            s[kt][i] = (acc_row0(i) > lim || acc_row0(i) < llim) ? -INFINITY : s[kt][i];
         }
       }
       float mx = s[0][0];
@@ -391,7 +404,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
     }
     __syncthreads();
   };
-  int t = 0;
+  int t = t_begin;
   for (; t + 1 < ntiles; t += 2) {
     tile_step(t, std::integral_constant<int, 0>{});
     tile_step(t + 1, std::integral_constant<int, 1>{});
@@ -439,6 +452,7 @@ struct BwdParams {
   int hq, hkv;
   float scale, c2;
   const int *kstart, *klen;  // optional per-sequence key ranges (see KeyRange)
+  int window;                // causal sliding window, as FwdParams::window
 };
 
 constexpr int kDqBQ = 128;  // query rows per workgroup (4 waves x 32)
@@ -448,7 +462,7 @@ constexpr int kKvBQ = 32;   // query rows per item
 
 // dQ = scale * sum_keys dS K, query-stationary (the forward's structure).  Also writes
 // delta = rowsum(dO * O) for its rows, which bwd_dkdv_kernel (launched after it) reads.
-template <int D, bool CAUSAL, int OCC>
+template <int D, bool CAUSAL, int OCC, bool WIN = false>
 __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int TILE = kDqBK * RB;
@@ -479,6 +493,8 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 
   const int kv_end = CAUSAL ? min(klen, q0 + kDqBQ + koff_c) : klen;
   const int ntiles = (kv_end + kDqBK - 1) / kDqBK;
+  const int win = (CAUSAL && WIN) ? P.window : 0;  // sliding window: first key of this block's queries
+  const int t_begin = win > 0 ? max(0, q0 + koff_c - win + 1) / kDqBK : 0;
   const uint16_t* kbase = P.k + (int64_t)kr.start * P.sk + (int64_t)kvh * D;
   const uint16_t* vbase = P.v + (int64_t)kr.start * P.sv + (int64_t)kvh * D;
 
@@ -498,8 +514,8 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     sq.load(P.q + srow * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
     sdo.load(P.dout + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
     so.load(P.o + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
-    sk.load(kbase, P.sk, klen);
-    sv.load(vbase, P.sv, klen);
+    sk.load(kbase + (int64_t)t_begin * kDqBK * P.sk, P.sk, klen - t_begin * kDqBK);
+    sv.load(vbase + (int64_t)t_begin * kDqBK * P.sv, P.sv, klen - t_begin * kDqBK);
     constexpr int NCH = D / 8, RSTEP = 256 / NCH, PER = kDqBQ / RSTEP;
     const int row0 = threadIdx.x / NCH, ch = threadIdx.x % NCH;
 #pragma unroll
@@ -549,8 +565,10 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       const int key0 = kt0 + 32 * kt;
-      // Wave-uniform skip of 32-key halves entirely above the diagonal or past the end.
+      // Wave-uniform skip of 32-key halves entirely above the diagonal, past the end, or before
+      // every query's sliding window.
       if ((CAUSAL && key0 > wave_qmax + koff_c) || key0 >= klen) continue;
+      if (win > 0 && key0 + 31 < wave_q0 + koff_c - win + 1) continue;
       f32x16 s = f32x16{}, dp = f32x16{};
       __builtin_amdgcn_sched_barrier(0);
       {
@@ -568,10 +586,12 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = fexp2(__builtin_fmaf(s[i], P.c2, -lse2));
-      if ((CAUSAL && key0 + 31 > wave_q0 + koff_c) || key0 + 32 > klen) {
+      if ((CAUSAL && key0 + 31 > wave_q0 + koff_c) || key0 + 32 > klen ||
+          (win > 0 && key0 < wave_qmax + koff_c - win + 1)) {
         const int lim = (CAUSAL ? min(qrow + koff_c, klen - 1) : klen - 1) - (key0 + 4 * h);
+        const int llim = win > 0 ? qrow + koff_c - win + 1 - (key0 + 4 * h) : INT_MIN;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = acc_row0(i) > lim ? 0.f : s[i];
+        for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) > lim || acc_row0(i) < llim) ? 0.f : s[i];
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] *= dp[i] - delta;  // dS^T / scale
@@ -596,7 +616,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     }
     __syncthreads();
   };
-  int t = 0;
+  int t = t_begin;
   for (; t + 1 < ntiles; t += 2) {
     tile_step(t, std::integral_constant<int, 0>{});
     tile_step(t + 1, std::integral_constant<int, 1>{});
@@ -612,7 +632,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 // double-buffered in LDS.  S and dP start from the row constants
 // (-lse/scale, -delta) so p = exp2(c2 S') and dS = p dP' need no per-element subtraction;
 // only the causal diagonal is masked (padded query rows carry Q = dO = 0 and contribute 0).
-template <int D, bool CAUSAL, int PF>
+template <int D, bool CAUSAL, int PF, bool WIN = false>
 __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int NC = D / 16;
@@ -656,7 +676,10 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
   }
 
   const int first_slice = CAUSAL ? (max(0, kb - koff_c) / kKvBQ) : 0;
-  const int per_head = (seqlen + kKvBQ - 1) / kKvBQ - first_slice;
+  const int win = (CAUSAL && WIN) ? P.window : 0;  // sliding window: the last query that sees this block
+  const int end_slice = win > 0 ? min((seqlen + kKvBQ - 1) / kKvBQ, (kb + kKvBK - 1 - koff_c + win - 1) / kKvBQ + 1)
+                                : (seqlen + kKvBQ - 1) / kKvBQ;
+  const int per_head = max(0, end_slice - first_slice);
   const int nitems = per_head * group;
   const float inv_scale = 1.f / P.scale;
 
@@ -724,10 +747,12 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
-      if (CAUSAL && wkey0 + 31 > qs + koff_c) {
+      if ((CAUSAL && wkey0 + 31 > qs + koff_c) || (win > 0 && qs + kKvBQ - 1 > wkey0 - koff_c + win - 1)) {
         const int lim = key - koff_c - qs - 4 * h;  // query row qs + acc_row < key - koff_c is masked
+        // sliding window: query row qs + acc_row > key - koff_c + win - 1 is masked
+        const int ulim = win > 0 ? key - koff_c + win - 1 - qs - 4 * h : INT_MAX;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) < lim) ? 0.f : s[i];
+        for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) < lim || acc_row0(i) > ulim) ? 0.f : s[i];
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) dp[i] *= s[i];  // dS / scale
@@ -834,7 +859,7 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
                                                               const at::Tensor& v, const at::Tensor& cu_seqlens,
                                                               int64_t max_seqlen, double scale, bool causal,
                                                               at::Tensor* stamps, const at::Tensor* k_start = nullptr,
-                                                              const at::Tensor* k_len = nullptr) {
+                                                              const at::Tensor* k_len = nullptr, int64_t window = 0) {
   const int64_t T = q.size(0), hq = q.size(1), D = q.size(2), hkv = k.size(1);
   check_qkv(q, "q", hq, D);
   check_qkv(k, "k", hkv, D);
@@ -853,8 +878,10 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
   const int nqb = (int)((max_seqlen + fa::kFwdBQ - 1) / fa::kFwdBQ);
   fa::FwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), q.stride(0), k.stride(0), v.stride(0),
                   bf16_mut(o), lse.data_ptr<float>(), cu_seqlens.data_ptr<int>(), T, (int)hq, (int)hkv,
-                  (float)(scale * fa::kLog2e), nullptr, nullptr, nullptr};
+                  (float)(scale * fa::kLog2e), nullptr, nullptr, nullptr, 0};
   key_range_ptrs(k_start, k_len, nseq, &P.kstart, &P.klen);
+  DTG_CHECK(window >= 0 && window < (1ll << 30), "flash_attn: window must be >= 0 (0 = full causal)");
+  P.window = causal ? (int)window : 0;
   dim3 grid(hq, nseq, nqb);
   if (stamps != nullptr) {
     *stamps = at::zeros({(int64_t)grid.x * grid.y * grid.z, 6}, q.options().dtype(at::kLong));
@@ -872,7 +899,12 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
 #define DTG_FWD_W(DD, C)                                                                  \
   do { if (!wide) DTG_FWD(DD, C, false, false); else if (!qlds) DTG_FWD(DD, C, true, false);   \
        else DTG_FWD(DD, C, true, true); } while (0)
-  if (D == 128) { if (causal) DTG_FWD_W(128, true); else DTG_FWD_W(128, false); }
+  if (P.window > 0) {  // sliding window (causal only): the WIN instantiation of the default variant
+    if (D == 128) { set_lds_limit((const void*)&fa::fwd_kernel<128, true, true, true, true>, lds);
+                    hipLaunchKernelGGL((fa::fwd_kernel<128, true, true, true, true>), grid, dim3(256), lds, stream(), P); }
+    else { set_lds_limit((const void*)&fa::fwd_kernel<64, true, true, true, true>, lds);
+           hipLaunchKernelGGL((fa::fwd_kernel<64, true, true, true, true>), grid, dim3(256), lds, stream(), P); }
+  } else if (D == 128) { if (causal) DTG_FWD_W(128, true); else DTG_FWD_W(128, false); }
   else { if (causal) DTG_FWD_W(64, true); else DTG_FWD_W(64, false); }
 #undef DTG_FWD_W
 #undef DTG_FWD
@@ -882,8 +914,8 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
 
 std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k,
                                                   const at::Tensor& v, const at::Tensor& cu_seqlens,
-                                                  int64_t max_seqlen, double scale, bool causal) {
-  return flash_attn_fwd_impl(q, k, v, cu_seqlens, max_seqlen, scale, causal, nullptr);
+                                                  int64_t max_seqlen, double scale, bool causal, int64_t window) {
+  return flash_attn_fwd_impl(q, k, v, cu_seqlens, max_seqlen, scale, causal, nullptr, nullptr, nullptr, window);
 }
 
 // Diagnostic: the same launch with per-workgroup timeline stamps [start, prologue done, tile
@@ -903,7 +935,8 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
                                 const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale,
                                 bool causal, const at::Tensor& dq, const at::Tensor& dk,
                                 const at::Tensor& dv, const at::Tensor* k_start = nullptr,
-                                const at::Tensor* k_len = nullptr, int64_t max_seqlen_k = -1) {
+                                const at::Tensor* k_len = nullptr, int64_t max_seqlen_k = -1,
+                                int64_t window = 0) {
   auto dout = dout_.contiguous();
   const int64_t T = q.size(0), hq = q.size(1), D = q.size(2), hkv = k.size(1);
   check_qkv(q, "q", hq, D);
@@ -935,8 +968,10 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   fa::BwdParams P{bf16_ptr(q), bf16_ptr(k), bf16_ptr(v), bf16_ptr(dout), bf16_ptr(o), q.stride(0), k.stride(0),
                   v.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), bf16_mut(dq), bf16_mut(dk),
                   bf16_mut(dv), dq.stride(0), dk.stride(0), dv.stride(0), cu_seqlens.data_ptr<int>(), T, (int)hq,
-                  (int)hkv, (float)scale, (float)(scale * fa::kLog2e), nullptr, nullptr};
+                  (int)hkv, (float)scale, (float)(scale * fa::kLog2e), nullptr, nullptr, 0};
   key_range_ptrs(k_start, k_len, nseq, &P.kstart, &P.klen);
+  DTG_CHECK(window >= 0 && window < (1ll << 30), "flash_attn: window must be >= 0 (0 = full causal)");
+  P.window = causal ? (int)window : 0;
   if (max_seqlen_k < 0) max_seqlen_k = max_seqlen;
   // Waves per SIMD of the dq kernel at head_dim 128 (DTG_FA_OCC=1|2; measured in profiles/).
   static const int occ = [] {
@@ -953,10 +988,12 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   {
     dim3 grid(hq, nseq, (max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ);
     const size_t lds = 4 * fa::kDqBK * D * 2 + fa::kDqBQ * 4;  // + the per-row delta
-#define DTG_BWD_DQ(DD, C, O)                                                              \
-  do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O>, lds);                        \
-       hipLaunchKernelGGL((fa::bwd_dq_kernel<DD, C, O>), grid, dim3(256), lds, stream(), P); } while (0)
-    if (D == 128) {
+#define DTG_BWD_DQ(DD, C, O, ...)                                                         \
+  do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>, lds);         \
+       hipLaunchKernelGGL((fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>), grid, dim3(256), lds, stream(), P); } while (0)
+    if (P.window > 0) {  // sliding window (causal only)
+      if (D == 128) DTG_BWD_DQ(128, true, 1, true); else DTG_BWD_DQ(64, true, 2, true);
+    } else if (D == 128) {
       if (occ == 2) { if (causal) DTG_BWD_DQ(128, true, 2); else DTG_BWD_DQ(128, false, 2); }
       else { if (causal) DTG_BWD_DQ(128, true, 1); else DTG_BWD_DQ(128, false, 1); }
     } else { if (causal) DTG_BWD_DQ(64, true, 2); else DTG_BWD_DQ(64, false, 2); }
@@ -966,10 +1003,12 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   {
     dim3 grid(hkv, nseq, (max_seqlen_k + fa::kKvBK - 1) / fa::kKvBK);
     const size_t lds = 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
-#define DTG_BWD_KV(DD, C, PF)                                                             \
-  do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF>, lds);                     \
-       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C, PF>), grid, dim3(256), lds, stream(), P); } while (0)
-    if (kv_pf == 2) {
+#define DTG_BWD_KV(DD, C, PF, ...)                                                        \
+  do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>, lds);      \
+       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>), grid, dim3(256), lds, stream(), P); } while (0)
+    if (P.window > 0) {  // sliding window (causal only)
+      if (D == 128) DTG_BWD_KV(128, true, 1, true); else DTG_BWD_KV(64, true, 1, true);
+    } else if (kv_pf == 2) {
       if (D == 128) { if (causal) DTG_BWD_KV(128, true, 2); else DTG_BWD_KV(128, false, 2); }
       else { if (causal) DTG_BWD_KV(64, true, 2); else DTG_BWD_KV(64, false, 2); }
     } else {
@@ -984,11 +1023,12 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
 std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(
     const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cu_seqlens, int64_t max_seqlen,
-    double scale, bool causal) {
+    double scale, bool causal, int64_t window) {
   auto dq = at::empty(q.sizes(), q.options());
   auto dk = at::empty(k.sizes(), k.options());
   auto dv = at::empty(v.sizes(), v.options());
-  flash_attn_bwd_impl(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, dq, dk, dv);
+  flash_attn_bwd_impl(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, dq, dk, dv, nullptr, nullptr, -1,
+                      window);
   return {dq, dk, dv};
 }
 
@@ -996,7 +1036,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(
 // comes back in the same fused layout so the QKV GEMM backward consumes it directly.
 at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& qkv, int64_t nq, int64_t nkv,
                               int64_t head_dim, const at::Tensor& o, const at::Tensor& lse,
-                              const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale, bool causal) {
+                              const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale, bool causal,
+                              int64_t window) {
   DTG_CHECK_CUDA_BF16(qkv);
   const int64_t T = qkv.size(0), D = head_dim;
   DTG_CHECK(qkv.dim() == 2 && qkv.size(1) == (nq + 2 * nkv) * D && qkv.stride(1) == 1,
@@ -1007,7 +1048,7 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& qkv, int
   };
   flash_attn_bwd_impl(dout, view3(qkv, 0, nq), view3(qkv, nq, nkv), view3(qkv, nq + nkv, nkv), o, lse,
                       cu_seqlens, max_seqlen, scale, causal, view3(dqkv, 0, nq), view3(dqkv, nq, nkv),
-                      view3(dqkv, nq + nkv, nkv));
+                      view3(dqkv, nq + nkv, nkv), nullptr, nullptr, -1, window);
   return dqkv;
 }
 

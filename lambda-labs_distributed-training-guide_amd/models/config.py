@@ -51,7 +51,7 @@ class LlamaConfig:
     initializer_range: float = 0.02
     eos_token_id: Optional[int] = None
     hf_name: str = ""
-    # llama (Llama-2/3/3.1/3.2), mistral (Llama layout + sliding_window), qwen2 (+ q/k/v bias)
+    # llama (Llama-2/3/3.1/3.2), mistral (Llama layout + sliding-window attention), qwen2 (+ q/k/v bias)
     model_type: str = "llama"
     attention_bias: bool = False  # q/k/v projection bias (Qwen2); o_proj never has one here
     sliding_window: Optional[int] = None  # Mistral: keys within this distance (None = full causal)

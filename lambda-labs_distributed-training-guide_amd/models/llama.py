@@ -83,6 +83,7 @@ class LlamaAttention(nn.Module):
             self.qkv_proj.bias = nn.Parameter(torch.empty((self.nq + 2 * self.nkv) * self.d, 1, device=device,
                                                           dtype=dtype))
         self.o_proj = Weight(h, self.nq * self.d, device=device, dtype=dtype)
+        self.window = int(cfg.sliding_window or 0)
 
     def forward(self, x, rc: RunCtx):
         b = getattr(self.qkv_proj, "bias", None)
@@ -102,7 +103,8 @@ class LlamaAttention(nn.Module):
             o = ulysses_attention(qkv, self.nq, self.nkv, self.d, rc.sp_group, rc.rows, rc.cu_seqlens,
                                   rc.max_seqlen, rc.cos, rc.sin, rc.pos)
         else:
-            o = ops.attention(qkv, self.nq, self.nkv, self.d, rc.cu_seqlens, rc.max_seqlen, rc.cos, rc.sin, rc.pos)
+            o = ops.attention(qkv, self.nq, self.nkv, self.d, rc.cu_seqlens, rc.max_seqlen, rc.cos, rc.sin, rc.pos,
+                              window=self.window)
         return ops.linear(o, self.o_proj.weight)
 
 
@@ -307,9 +309,9 @@ class LlamaForCausalLM(nn.Module):
         T = B * S
         dev = input_ids.device
         sw = self.config.sliding_window
-        if sw is not None and max(S, int(max_seqlen or 0)) > sw:
-            raise ValueError(f"{self.config.model_type}: sequences of {max(S, int(max_seqlen or 0))} tokens exceed the "
-                             f"sliding window ({sw}); only full-causal attention is implemented (rows <= window)")
+        if sw is not None and (self.cp_group is not None or self.sp_group is not None) and S > sw:
+            raise ValueError(f"{self.config.model_type}: context / Ulysses parallelism with rows longer than the "
+                             f"sliding window ({sw}) is not supported; the single-rank and TP paths are")
         sp = self.sp_group is not None
         if sp:  # attention sees the full rows: describe them (positions gathered from the slices)
             from ..parallel.ulysses import sp_world

@@ -143,14 +143,17 @@ def _key_ranges(cu_seqlens, k_start=None, k_len=None):
     return out
 
 
-def _mask(nq, nk):
-    # True = masked: key j > query i + (nk - nq)
+def _mask(nq, nk, window=0):
+    # True = masked: key j > query i + (nk - nq), or (sliding window) j <= i + (nk - nq) - window
     i = torch.arange(nq)[:, None]
     j = torch.arange(nk)[None, :]
-    return j > i + (nk - nq)
+    m = j > i + (nk - nq)
+    if window > 0:
+        m = m | (j <= i + (nk - nq) - window)
+    return m
 
 
-def _attn_ref(q, k, v, cu_seqlens, scale, causal, k_start=None, k_len=None):
+def _attn_ref(q, k, v, cu_seqlens, scale, causal, k_start=None, k_len=None, window=0):
     """Per-sequence f32 attention; returns o (bf16/in dtype) and lse [Hq, T] (natural log)."""
     T, hq, d = q.shape
     hkv = k.shape[1]
@@ -165,7 +168,7 @@ def _attn_ref(q, k, v, cu_seqlens, scale, causal, k_start=None, k_len=None):
         vs = v[ka:kb].float().transpose(0, 1).repeat_interleave(rep, 0)
         sc = qs @ ks.transpose(1, 2) * scale
         if causal:
-            sc = sc.masked_fill(_mask(b - a, kb - ka), float("-inf"))
+            sc = sc.masked_fill(_mask(b - a, kb - ka, window), float("-inf"))
         l_ = torch.logsumexp(sc, -1)
         p = torch.exp(sc - l_[..., None])
         o[a:b] = (p @ vs).transpose(0, 1)
@@ -173,8 +176,8 @@ def _attn_ref(q, k, v, cu_seqlens, scale, causal, k_start=None, k_len=None):
     return o, lse
 
 
-def flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal):
-    o, lse = _attn_ref(q, k, v, cu_seqlens, scale, causal)
+def flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal, window=0):
+    o, lse = _attn_ref(q, k, v, cu_seqlens, scale, causal, window=window)
     return o.to(q.dtype), lse
 
 
@@ -183,7 +186,7 @@ def flash_attn_varlen_fwd(q, k, v, cu_seqlens_q, k_start, k_len, max_seqlen_q, m
     return o.to(q.dtype), lse
 
 
-def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, k_start=None, k_len=None):
+def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, window=0, k_start=None, k_len=None):
     """The kernel's semantics: P = exp(S*scale - lse) with the GIVEN lse, delta = rowsum(dO*O)
     with the GIVEN o (so a block of a larger softmax -- context parallelism -- gets the
     gradient of the full softmax)."""
@@ -203,7 +206,7 @@ def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal,
         os_ = o[a:b].float().transpose(0, 1)
         sc = qs @ ks.transpose(1, 2) * scale
         if causal:
-            sc = sc.masked_fill(_mask(b - a, kb - ka), float("-inf"))
+            sc = sc.masked_fill(_mask(b - a, kb - ka, window), float("-inf"))
         p = torch.exp(sc - lse[:, a:b].float()[..., None])
         dvh = p.transpose(1, 2) @ dos
         dp = dos @ vs.transpose(1, 2)
@@ -219,16 +222,16 @@ def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal,
 
 def flash_attn_varlen_bwd(dout, q, k, v, o, lse, cu_seqlens_q, k_start, k_len, max_seqlen_q, max_seqlen_k, scale,
                           causal):
-    return flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens_q, max_seqlen_q, scale, causal, k_start, k_len)
+    return flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens_q, max_seqlen_q, scale, causal, 0, k_start, k_len)
 
 
-def flash_attn_bwd_qkv(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal):
+def flash_attn_bwd_qkv(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal, window=0):
     T = qkv.shape[0]
     d = head_dim
     q = qkv[:, : nq * d].reshape(T, nq, d)
     k = qkv[:, nq * d : (nq + nkv) * d].reshape(T, nkv, d)
     v = qkv[:, (nq + nkv) * d :].reshape(T, nkv, d)
-    dq, dk, dv = flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal)
+    dq, dk, dv = flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, window)
     return torch.cat([dq.reshape(T, -1), dk.reshape(T, -1), dv.reshape(T, -1)], dim=1)
 
 

@@ -24,11 +24,13 @@ _DEFS = [
     "float beta2, float eps, float wd, int step, float grad_scale, Tensor? hyper=None) -> ()",
     "adamw_cpu_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float lr, float beta1, float beta2, "
     "float eps, float wd, int step, float grad_scale) -> ()",
-    "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> (Tensor, Tensor)",
+    # window > 0 (causal only): sliding window, query i sees keys (i - window, i]
+    "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, bool causal, "
+    "int window=0) -> (Tensor, Tensor)",
     "flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor cu_seqlens, "
-    "int max_seqlen, float scale, bool causal) -> (Tensor, Tensor, Tensor)",
+    "int max_seqlen, float scale, bool causal, int window=0) -> (Tensor, Tensor, Tensor)",
     "flash_attn_bwd_qkv(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
-    "Tensor cu_seqlens, int max_seqlen, float scale, bool causal) -> Tensor",
+    "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, int window=0) -> Tensor",
     "transpose2d(Tensor x) -> Tensor",
     "embedding_bwd_(Tensor(a!) out, Tensor ids, Tensor dy) -> ()",
     # FlashAttention-2-style varlen with explicit per-sequence key ranges (disjoint), causal mask

@@ -184,7 +184,7 @@ def rope_tables(head_dim, theta, max_pos, scaling=None, device=None):
 # --------------------------------------------------------------------------------------------
 class _AttentionQKV(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cos, sin, pos, cu_seqlens, max_seqlen, nq, nkv, head_dim, scale, causal, rope):
+    def forward(ctx, qkv, cos, sin, pos, cu_seqlens, max_seqlen, nq, nkv, head_dim, scale, causal, rope, window):
         T = qkv.shape[0]
         d = head_dim
         if rope:
@@ -192,20 +192,21 @@ class _AttentionQKV(torch.autograd.Function):
         q = qkv.as_strided((T, nq, d), (qkv.stride(0), d, 1), qkv.storage_offset())
         k = qkv.as_strided((T, nkv, d), (qkv.stride(0), d, 1), qkv.storage_offset() + nq * d)
         v = qkv.as_strided((T, nkv, d), (qkv.stride(0), d, 1), qkv.storage_offset() + (nq + nkv) * d)
-        o, lse = ops.flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal)
+        o, lse = ops.flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal, window)
         ctx.save_for_backward(qkv, o, lse, cu_seqlens, cos, sin, pos)
-        ctx.meta = (max_seqlen, nq, nkv, d, scale, causal, rope)
+        ctx.meta = (max_seqlen, nq, nkv, d, scale, causal, rope, window)
         return o.view(T, nq * d)
 
     @staticmethod
     def backward(ctx, do):
         qkv, o, lse, cu, cos, sin, pos = ctx.saved_tensors
-        max_seqlen, nq, nkv, d, scale, causal, rope = ctx.meta
+        max_seqlen, nq, nkv, d, scale, causal, rope, window = ctx.meta
         T = qkv.shape[0]
-        dqkv = ops.flash_attn_bwd_qkv(do.contiguous().view(T, nq, d), qkv, nq, nkv, d, o, lse, cu, max_seqlen, scale, causal)
+        dqkv = ops.flash_attn_bwd_qkv(do.contiguous().view(T, nq, d), qkv, nq, nkv, d, o, lse, cu, max_seqlen, scale,
+                                      causal, window)
         if rope:
             ops.rope_(dqkv, cos, sin, pos, nq + nkv, d, True)
-        return dqkv, None, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _Rope(torch.autograd.Function):
@@ -231,17 +232,20 @@ def rope(qkv, cos, sin, pos, nheads, head_dim):
     return _Rope.apply(qkv, cos, sin, pos, int(nheads), int(head_dim))
 
 
-def attention(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos=None, sin=None, pos=None, causal=True, scale=None):
+def attention(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos=None, sin=None, pos=None, causal=True, scale=None,
+              window=0):
     """Causal (varlen) GQA attention on a fused [T, (nq+2nkv)*d] QKV activation -> [T, nq*d].
 
-    If cos/sin/pos are given, RoPE is applied to q and k first (in place on qkv)."""
+    If cos/sin/pos are given, RoPE is applied to q and k first (in place on qkv).  window > 0:
+    sliding-window attention (query i sees keys i - window < j <= i; Mistral)."""
     if scale is None:
         scale = 1.0 / math.sqrt(head_dim)
     rope = cos is not None
     if not rope:
         cos = sin = torch.empty(0, device=qkv.device)
         pos = torch.empty(0, dtype=torch.long, device=qkv.device)
-    return _AttentionQKV.apply(qkv, cos, sin, pos, cu_seqlens, int(max_seqlen), nq, nkv, head_dim, float(scale), causal, rope)
+    return _AttentionQKV.apply(qkv, cos, sin, pos, cu_seqlens, int(max_seqlen), nq, nkv, head_dim, float(scale), causal, rope,
+                               int(window or 0))
 
 
 # --------------------------------------------------------------------------------------------

@@ -216,7 +216,7 @@ def test_adamw(cuda, state_dtype, master, n):
         assert (tp.detach().float() - pm.float()).abs().max().item() <= 2 * 2**-7 * tp.detach().float().abs().max().item()
 
 
-def _attn_case(cuda, seqlens, hq, hkv, D, causal, stride_extra=0, qscale=1.0):
+def _attn_case(cuda, seqlens, hq, hkv, D, causal, stride_extra=0, qscale=1.0, window=0):
     torch.manual_seed(0)
     T = sum(seqlens)
     cu = torch.tensor([0] + list(torch.tensor(seqlens).cumsum(0).tolist()), dtype=torch.int32)
@@ -228,17 +228,17 @@ def _attn_case(cuda, seqlens, hq, hkv, D, causal, stride_extra=0, qscale=1.0):
     k = qkv[:, hq * D:(hq + hkv) * D].view(T, hkv, D)
     v = qkv[:, (hq + hkv) * D:(hq + 2 * hkv) * D].view(T, hkv, D)
     scale = 1 / math.sqrt(D)
-    o_ref, lse_ref = dops.flash_attn_fwd(q, k, v, cu, max(seqlens), scale, causal)
+    o_ref, lse_ref = dops.flash_attn_fwd(q, k, v, cu, max(seqlens), scale, causal, window)
     g = qkv.to(cuda)
     gq = g[:, : hq * D].view(T, hq, D)
     gk = g[:, hq * D:(hq + hkv) * D].view(T, hkv, D)
     gv = g[:, (hq + hkv) * D:(hq + 2 * hkv) * D].view(T, hkv, D)
-    o, lse = dops.flash_attn_fwd(gq, gk, gv, cu.to(cuda), max(seqlens), scale, causal)
+    o, lse = dops.flash_attn_fwd(gq, gk, gv, cu.to(cuda), max(seqlens), scale, causal, window)
     _close(o, o_ref, 2e-2, 2e-2, "attn out")
     _close(lse, lse_ref, 2e-3, 1e-3, "lse")
     do = torch.randn(T, hq, D).bfloat16()
-    dq_ref, dk_ref, dv_ref = dops.flash_attn_bwd(do, q, k, v, o_ref, lse_ref, cu, max(seqlens), scale, causal)
-    dq, dk, dv = dops.flash_attn_bwd(do.to(cuda), gq, gk, gv, o, lse, cu.to(cuda), max(seqlens), scale, causal)
+    dq_ref, dk_ref, dv_ref = dops.flash_attn_bwd(do, q, k, v, o_ref, lse_ref, cu, max(seqlens), scale, causal, window)
+    dq, dk, dv = dops.flash_attn_bwd(do.to(cuda), gq, gk, gv, o, lse, cu.to(cuda), max(seqlens), scale, causal, window)
     for a, b, n in ((dq, dq_ref, "dq"), (dk, dk_ref, "dk"), (dv, dv_ref, "dv")):
         assert _rel(a, b) < 2e-2, f"{n} rel err {_rel(a, b)}"
     return qkv, cu
@@ -267,6 +267,15 @@ def test_flash_attn_fwd_variants(cuda, variant, causal, monkeypatch):
     _attn_case(cuda, [1024, 77], hq=4, hkv=2, D=128, causal=causal, qscale=8.0)
 
 
+@pytest.mark.parametrize("window", [2, 64, 200, 5000])
+@pytest.mark.parametrize("D,hq,hkv", [(128, 8, 2), (64, 4, 4)])
+def test_flash_attn_sliding_window(cuda, window, D, hq, hkv):
+    """Causal sliding window (query i sees keys i - window < j <= i): forward and both backward
+    kernels vs the fp32 reference, windows inside one tile (2; a window of 1 makes dQ exactly 0), crossing tiles (64, 200) and
+    longer than every sequence (5000 == full causal); varlen sequences, GQA and MHA."""
+    _attn_case(cuda, [1024, 77, 300], hq=hq, hkv=hkv, D=D, causal=True, window=window)
+
+
 def test_flash_attn_bwd_qkv_fused(cuda):
     torch.manual_seed(0)
     T, hq, hkv, D = 384, 4, 1, 128
@@ -282,10 +291,11 @@ def test_flash_attn_bwd_qkv_fused(cuda):
     _close(fused, ref, 0, 0, "fused dqkv layout")
 
 
-@pytest.mark.parametrize("name", ["llama-tiny-d128", "qwen2-tiny"])
+@pytest.mark.parametrize("name", ["llama-tiny-d128", "qwen2-tiny", "mistral-tiny"])
 def test_llama_tiny_gpu_matches_cpu(cuda, name):
     """Whole model on the GPU kernels (bf16) vs the fp32 CPU model: loss and gradient norm
-    (qwen2-tiny adds the q/k/v bias through the fused linear-with-bias backward)."""
+    (qwen2-tiny adds the q/k/v bias through the fused linear-with-bias backward; mistral-tiny
+    runs 256-token rows through its 64-token sliding window)."""
     from dtg.models import build_model
 
     torch.manual_seed(0)

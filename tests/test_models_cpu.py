@@ -41,12 +41,21 @@ def test_unsupported_model_type_is_refused():
         resolve_config("llama-tiny", model_type="gemma")
 
 
-def test_sliding_window_beyond_window_is_refused():
-    cfg = resolve_config("mistral-tiny")  # sliding_window 64
+def test_mistral_sliding_window_matches_hf_beyond_window():
+    """Rows longer than the window (mistral-tiny: 64) use sliding-window attention, like HF."""
+    torch.manual_seed(0)
+    cfg = resolve_config("mistral-tiny")
     m = build_model(cfg, device="cpu", dtype=torch.float32)
-    ids = torch.randint(0, cfg.vocab_size, (1, 65))
-    with pytest.raises(ValueError, match="sliding window"):
-        m(input_ids=ids, labels=ids)
+    hf = hf_causal_lm_class(cfg)(hf_llama_config(cfg)).float()
+    hf.load_state_dict(llama_to_hf(m.state_dict(), cfg), strict=True)
+    ids = torch.randint(0, cfg.vocab_size, (2, 150))
+    a = m(input_ids=ids, labels=ids, return_logits=True)
+    b = hf(input_ids=ids, labels=ids)
+    torch.testing.assert_close(a.logits, b.logits, atol=1e-4, rtol=1e-4)
+    full = resolve_config("mistral-tiny", sliding_window=None)
+    m2 = build_model(full, device="cpu", dtype=torch.float32)
+    m2.load_state_dict(m.state_dict())
+    assert not torch.allclose(m2(input_ids=ids, return_logits=True).logits[:, 100:], a.logits[:, 100:], atol=1e-3)
 
 
 @pytest.mark.parametrize("name", ["llama-tiny", "qwen2-tiny"])
