@@ -61,11 +61,12 @@ class TPInfo:
 class RunCtx:
     """Per-forward runtime data shared by all layers."""
 
-    __slots__ = ("cos", "sin", "pos", "cu_seqlens", "max_seqlen", "cp_group", "rows", "sp_group")
+    __slots__ = ("cos", "sin", "pos", "cu_seqlens", "max_seqlen", "cp_group", "rows", "sp_group", "cp_ranges")
 
-    def __init__(self, cos, sin, pos, cu_seqlens, max_seqlen, cp_group=None, rows=0, sp_group=None):
+    def __init__(self, cos, sin, pos, cu_seqlens, max_seqlen, cp_group=None, rows=0, sp_group=None, cp_ranges=None):
         self.cos, self.sin, self.pos, self.cu_seqlens, self.max_seqlen = cos, sin, pos, cu_seqlens, max_seqlen
         self.cp_group, self.rows, self.sp_group = cp_group, rows, sp_group
+        self.cp_ranges = cp_ranges  # context parallel over packed rows (parallel/context_parallel.py)
 
 
 class LlamaAttention(nn.Module):
@@ -96,7 +97,7 @@ class LlamaAttention(nn.Module):
             q = qkv[:, :self.nq * d].reshape(T, self.nq, d)
             k = qkv[:, self.nq * d:(self.nq + self.nkv) * d].reshape(T, self.nkv, d)
             v = qkv[:, (self.nq + self.nkv) * d:].reshape(T, self.nkv, d)
-            o = cp_attention(q, k, v, rc.cp_group, rc.rows).reshape(T, self.nq * d)
+            o = cp_attention(q, k, v, rc.cp_group, rc.rows, ranges=rc.cp_ranges).reshape(T, self.nq * d)
         elif rc.sp_group is not None:  # Ulysses: all-to-all to full sequences x local heads
             from ..parallel.ulysses import ulysses_attention
 
@@ -325,7 +326,16 @@ class LlamaForCausalLM(nn.Module):
                 cu_seqlens = None
             S = S * n
             T = B * S
-        if self.cp_group is not None:  # attention is block-wise over zig-zag chunks: no cu_seqlens
+        cp_ranges = None
+        if self.cp_group is not None:  # attention over zig-zag chunks; cu_seqlens (if given) are the
+            # FULL rows' document boundaries of a packed batch (cp_batch keeps the collator's)
+            if cu_seqlens is not None:
+                from ..parallel.context_parallel import cp_ranges as _cp_ranges, row_doc_starts
+                from ..utils import comm
+
+                n = comm.world(self.cp_group)
+                docs = row_doc_starts(cu_seqlens, B, S * n)
+                cp_ranges = _cp_ranges(comm.rank(self.cp_group), n, B, S // 2, dev, docs)
             pos, cu, max_seqlen = position_ids.reshape(-1).to(torch.long), None, 0
         elif position_ids is None:
             pos, cu = self._dense_meta(B, S, dev)
@@ -349,7 +359,7 @@ class LlamaForCausalLM(nn.Module):
         else:
             cos, sin = self._rope_tables(S, dev)
         return RunCtx(cos, sin, pos, cu, int(max_seqlen), self.cp_group if cp else None, B,
-                      self.sp_group if sp else None)
+                      self.sp_group if sp else None, cp_ranges)
 
     def embed(self, input_ids):
         ids = input_ids.reshape(-1)

@@ -16,8 +16,12 @@ other ranks' keys and values:
             dK / dV of the two added, one index_select back to rank order and one
             reduce-scatter to the owners: O(1) launches per layer in both passes.
 
-Work per rank: the causal work of chunks r and 2cp-1-r, equal on every rank.  Dense rows only
-(packed documents would need block masks per document).
+Work per rank: the causal work of chunks r and 2cp-1-r, equal on every rank.
+
+Packed rows (several documents per row, 00-rime): a local chunk is cut at the document
+boundaries into pieces, and each piece is a varlen "sequence" whose keys are its document's
+prefix up to the piece's end (bottom-right causal alignment again) -- attention never crosses a
+document, RoPE uses the per-document positions, and the launch count stays O(1) per layer.
 """
 from __future__ import annotations
 
@@ -55,16 +59,18 @@ def unshard_zigzag(shards: List[torch.Tensor], cp: int) -> torch.Tensor:
     return torch.cat(chunks, dim=1)
 
 
-def cp_batch(input_ids: torch.Tensor, rank: int, cp: int, ignore_index: int = -100, labels=None):
+def cp_batch(input_ids: torch.Tensor, rank: int, cp: int, ignore_index: int = -100, labels=None,
+             position_ids=None):
     """Shard a full [B, S] batch for context parallelism.
 
     Returns (ids, shifted_labels, position_ids, num_valid_total): labels are shifted on the
     FULL sequence first (the next token of a chunk's last token lives on another rank),
-    positions are the global ones (RoPE), and num_valid_total is the global label count."""
+    positions are the global ones -- or, for packed rows, the given per-document positions
+    (RoPE) -- and num_valid_total is the global label count."""
     B, S = input_ids.shape
     shifted = torch.full_like(input_ids, ignore_index)
     shifted[:, :-1] = (input_ids if labels is None else labels)[:, 1:]
-    pos = torch.arange(S, device=input_ids.device).expand(B, S)
+    pos = torch.arange(S, device=input_ids.device).expand(B, S) if position_ids is None else position_ids
     n_valid = int((shifted != ignore_index).sum())
     return (shard_zigzag(input_ids, rank, cp), shard_zigzag(shifted, rank, cp), shard_zigzag(pos, rank, cp), n_valid)
 
@@ -88,6 +94,52 @@ def _gather_kv(k, v, group, cp, B, c):
     full = rs.index_select(1, _chunk_perm(cp, kv.device)).reshape(B * 2 * cp * c, H2, D)
     H = H2 // 2
     return full[:, :H].contiguous(), full[:, H:].contiguous()
+
+
+def row_doc_starts(cu_seqlens, B: int, S: int):
+    """Per-row document start offsets (row coordinates, 0 included) from the flattened [B*S]
+    document boundaries of a packed batch (`PackedCollator`'s cu_seqlens)."""
+    cu = [int(x) for x in torch.as_tensor(cu_seqlens).tolist()]
+    rows = [[0] for _ in range(B)]
+    for x in cu:
+        b, off = divmod(x, S)
+        if b < B and off > 0:
+            rows[b].append(off)
+    return [sorted(set(r)) for r in rows]
+
+
+def packed_ranges(rank, cp, B, c, row_docs, device, slots=(0, 1)):
+    """Varlen description of the local query chunks of `slots` for packed rows: every (row, slot)
+    chunk is cut at document boundaries; a piece is one sequence whose keys are its document's
+    prefix in the gathered full rows, up to the piece's last token.  Returns (cu_seqlens_q,
+    k_start, k_len, max_q, max_k)."""
+    S = 2 * cp * c
+    g = zigzag_chunks(rank, cp)
+    qlens, starts, lens = [], [], []
+    for b in range(B):
+        docs = row_docs[b] + [S]
+        for s in slots:
+            lo, hi = g[s] * c, (g[s] + 1) * c
+            for ds, de in zip(docs[:-1], docs[1:]):
+                a, e = max(ds, lo), min(de, hi)
+                if a < e:
+                    qlens.append(e - a)
+                    starts.append(b * S + ds)
+                    lens.append(e - ds)
+    cu = [0]
+    for n in qlens:
+        cu.append(cu[-1] + n)
+    mk = lambda xs: torch.tensor(xs, dtype=torch.int32, device=device)
+    return mk(cu), mk(starts), mk(lens), max(qlens), max(lens)
+
+
+def cp_ranges(rank, cp, B, c, device, row_docs=None):
+    """{"all": ranges of both local slots, 0: slot 0, 1: slot 1} for the forward and the two
+    per-slot backward calls (dense rows: one sequence per chunk)."""
+    if row_docs is None:
+        f = lambda sl: _ranges(rank, cp, B, c, device, sl)
+        return {k: (*f(sl)[:3], c, f(sl)[3]) for k, sl in (("all", (0, 1)), (0, (0,)), (1, (1,)))}
+    return {k: packed_ranges(rank, cp, B, c, row_docs, device, sl) for k, sl in (("all", (0, 1)), (0, (0,)), (1, (1,)))}
 
 
 def _ranges(rank, cp, B, c, device, slots=(0, 1)):
@@ -114,22 +166,24 @@ class _CPAttention(torch.autograd.Function):
     reduce-scatter of the full-row dK|dV to the owners."""
 
     @staticmethod
-    def forward(ctx, q, k, v, group, cp, rank, B, scale):
+    def forward(ctx, q, k, v, group, cp, rank, B, scale, ranges):
         # q [B*2c, Hq, D], k / v [B*2c, Hkv, D] (local zig-zag shard, row-major over rows)
         T, Hq, D = q.shape
         c = T // (2 * B)
         kf, vf = _gather_kv(k, v, group, cp, B, c)
         q = q.contiguous()
-        cu, ks, kl, maxk = _ranges(rank, cp, B, c, q.device)
-        out, lse = torch.ops.dtg.flash_attn_varlen_fwd(q, kf, vf, cu, ks, kl, c, maxk, scale, True)
+        if ranges is None:
+            ranges = cp_ranges(rank, cp, B, c, q.device)
+        cu, ks, kl, maxq, maxk = ranges["all"]
+        out, lse = torch.ops.dtg.flash_attn_varlen_fwd(q, kf, vf, cu, ks, kl, maxq, maxk, scale, True)
         ctx.save_for_backward(q, kf, vf, out, lse)
-        ctx.meta = (group, cp, rank, B, c, scale, k.shape[1])
+        ctx.meta = (group, cp, rank, B, c, scale, k.shape[1], ranges)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         q, kf, vf, out, lse = ctx.saved_tensors
-        group, cp, rank, B, c, scale, Hkv = ctx.meta
+        group, cp, rank, B, c, scale, Hkv, ranges = ctx.meta
         T, Hq, D = q.shape
         sl = lambda t: t.view(B, 2, c, *t.shape[1:])
         q5, o5, do5 = sl(q), sl(out), sl(dout.contiguous())
@@ -137,10 +191,10 @@ class _CPAttention(torch.autograd.Function):
         dq = torch.empty_like(q5)
         dk = dv = None
         for s in (0, 1):
-            cu, ks, kl, maxk = _ranges(rank, cp, B, c, q.device, slots=(s,))
+            cu, ks, kl, maxq, maxk = ranges[s]
             flat = lambda t: t[:, s].reshape(B * c, *t.shape[3:])
             dqs, dks, dvs = torch.ops.dtg.flash_attn_varlen_bwd(
-                flat(do5), flat(q5), kf, vf, flat(o5), lse4[:, :, s].reshape(Hq, B * c), cu, ks, kl, c, maxk,
+                flat(do5), flat(q5), kf, vf, flat(o5), lse4[:, :, s].reshape(Hq, B * c), cu, ks, kl, maxq, maxk,
                 scale, True)
             dq[:, s] = dqs.view(B, c, Hq, D)
             dk = dks.float() if dk is None else dk + dks.float()
@@ -152,16 +206,17 @@ class _CPAttention(torch.autograd.Function):
         send = dkv.index_select(1, inv).view(B, cp, 2, c, 2 * Hkv, D).transpose(0, 1).reshape(cp * B * 2 * c, 2 * Hkv, D)
         mine = comm.reduce_scatter_dim0(send.contiguous(), group) if cp > 1 else send  # [B*2c, 2Hkv, D]
         return (dq.view(T, Hq, D), mine[:, :Hkv].contiguous(), mine[:, Hkv:].contiguous(),
-                None, None, None, None, None)
+                None, None, None, None, None, None)
 
 
-def cp_attention(q, k, v, group, batch_rows: int, scale: float | None = None):
+def cp_attention(q, k, v, group, batch_rows: int, scale: float | None = None, ranges=None):
     """Exact causal attention over zig-zag context-parallel shards.
 
     q [B*S/cp, Hq, D], k / v [B*S/cp, Hkv, D]: this rank's tokens, rows concatenated, each row
-    holding its two chunks; returns this rank's attention output [B*S/cp, Hq, D]."""
+    holding its two chunks; returns this rank's attention output [B*S/cp, Hq, D].  `ranges`
+    (`cp_ranges(..., row_docs)`) describes packed rows; None = dense rows."""
     cp = comm.world(group) if dist.is_initialized() else 1
     rank = comm.rank(group) if cp > 1 else 0
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
-    return _CPAttention.apply(q, k, v, group, cp, rank, batch_rows, float(scale))
+    return _CPAttention.apply(q, k, v, group, cp, rank, batch_rows, float(scale), ranges)

@@ -73,7 +73,8 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                        help="Ulysses sequence parallel degree: each row is split over this many ranks, "
                             "all-to-all seq<->heads around attention (packed rows supported)")
         g.add_argument("--cp", default=1, type=int,
-                       help="context parallel degree: zig-zag row shards, all-gathered K/V (dense rows)")
+                       help="context parallel degree: zig-zag row shards, all-gathered K/V, one varlen flash call "
+                            "per layer (dense or packed rows)")
         g.add_argument("--pp", default=1, type=int,
                        help="pipeline parallel degree: contiguous ranks form a pipeline of decoder-layer stages "
                             "(1F1B schedule, point-to-point activations); the rest is data parallel")

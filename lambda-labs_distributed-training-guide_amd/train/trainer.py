@@ -441,11 +441,12 @@ def _seq_sharder(seq):
 
             ids, lab, pos, nv = ulysses_batch(b["input_ids"], r, n, b.get("position_ids"), labels=b.get("labels"))
         else:
-            assert "position_ids" not in b, "--cp takes dense rows (use --sp for packed sequences)"
             from ..parallel.context_parallel import cp_batch
 
-            ids, lab, pos, nv = cp_batch(b["input_ids"], r, n, labels=b.get("labels"))
+            ids, lab, pos, nv = cp_batch(b["input_ids"], r, n, labels=b.get("labels"), position_ids=b.get("position_ids"))
         out = {"input_ids": ids, "labels": lab, "num_valid": nv}
+        if kind == "cp" and "cu_seqlens" in b:  # packed rows: the full rows' document boundaries
+            out["cu_seqlens"] = b["cu_seqlens"]
         if pos is not None:
             out["position_ids"] = pos
         return out

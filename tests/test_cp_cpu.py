@@ -102,3 +102,68 @@ def test_llama_context_parallel_training_matches_single(world):
     for r in range(world):
         for n, v in ref.items():
             torch.testing.assert_close(res[r][0][n], v, atol=3e-4, rtol=1e-3, msg=f"rank {r} {n}")
+
+
+def _packed_batches(n=2, B=2, S=32, eos=511):
+    from dtg.data import PackedCollator
+
+    g = torch.Generator().manual_seed(5)
+    out = []
+    for _ in range(n):
+        rows = []
+        for _ in range(B):
+            x = torch.randint(0, eos, (S,), generator=g)
+            cuts = torch.randint(1, S - 1, (3,), generator=g)  # three interior EOS: 4 documents
+            x[cuts] = eos
+            rows.append({"input_ids": x})
+        out.append(PackedCollator(eos)(rows))
+    return out
+
+
+def _train_cp_packed(rank, world, batches):
+    from dtg.models import build_model
+    from dtg.parallel.context_parallel import cp_batch
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    torch.manual_seed(0)
+    model = build_model("llama-tiny-d128", device="cpu", dtype=torch.float32,
+                        cp_group=torch.distributed.group.WORLD if world > 1 else None)
+    eng = DataParallel(model, mode="ddp" if world > 1 else "single", bucket_mb=1, grad_divisor=1)
+    opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
+    losses = []
+    for b in batches:
+        opt.zero_grad()
+        if world > 1:
+            x, lab, pos, nv = cp_batch(b["input_ids"], rank, world, labels=b["labels"], position_ids=b["position_ids"])
+            out = model(input_ids=x, labels=lab, position_ids=pos, cu_seqlens=b["cu_seqlens"], num_valid=nv)
+        else:
+            out = model(input_ids=b["input_ids"], labels=b["labels"], position_ids=b["position_ids"],
+                        cu_seqlens=b["cu_seqlens"], max_seqlen=b["max_seqlen"])
+        eng.backward(out.loss)
+        opt.step()
+        losses.append(out.loss.item())
+    return {n: p.detach().clone() for n, p in model.named_parameters()}, losses
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_llama_context_parallel_packed_rows_matches_single(world):
+    """Packed rows (documents separated by EOS, positions restarting per document) under context
+    parallelism == one process running the varlen packed path: local chunks are cut at document
+    boundaries, each piece attends only its own document's prefix."""
+    batches = _packed_batches()
+    ref, ref_losses = _train_cp_packed(0, 1, batches)
+    res = run_distributed(_train_cp_packed, world, batches)
+    assert abs(sum(r[1][0] for r in res) - ref_losses[0]) < 1e-4 * abs(ref_losses[0])
+    for r in range(world):
+        for n, v in ref.items():
+            torch.testing.assert_close(res[r][0][n], v, atol=3e-4, rtol=1e-3, msg=f"rank {r} {n}")
+
+
+def test_packed_ranges_cut_chunks_at_documents():
+    from dtg.parallel.context_parallel import packed_ranges
+
+    # one row of 16 tokens, cp=2 -> chunks of 4: rank 0 holds chunks 0 and 3 ([0,4) and [12,16));
+    # documents start at 0, 3 and 10
+    cu, ks, kl, mq, mk = packed_ranges(0, 2, 1, 4, [[0, 3, 10]], "cpu")
+    assert cu.tolist() == [0, 3, 4, 8]          # pieces [0,3) [3,4) | [12,16)
+    assert ks.tolist() == [0, 3, 10] and kl.tolist() == [3, 1, 6] and (mq, mk) == (4, 6)

@@ -14,31 +14,44 @@ def _full():
     return [torch.randn(B, S, h, D, generator=g).bfloat16() for h in (HQ, HKV, HKV, HQ)]
 
 
-def _worker(rank, world):
+DOCS = [[0, 100, 333, 700], [0, 517]]  # packed rows: document starts per row
+
+
+def _worker(rank, world, docs=None):
     import dtg.ops  # noqa: F401
-    from dtg.parallel.context_parallel import cp_attention, shard_zigzag
+    from dtg.parallel.context_parallel import cp_attention, cp_ranges, shard_zigzag
 
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
     loc = [shard_zigzag(t, rank, world).to(dev) for t in _full()]
     ql, kl, vl = (t.reshape(-1, *t.shape[2:]).clone().requires_grad_() for t in loc[:3])
-    o = cp_attention(ql, kl, vl, None, B)
+    ranges = cp_ranges(rank, world, B, S // (2 * world), dev, docs) if docs else None
+    o = cp_attention(ql, kl, vl, None, B, ranges=ranges)
     o.backward(loc[3].reshape(-1, HQ, D))
     torch.cuda.synchronize()
     return [t.view(B, -1, *t.shape[1:]).detach().float().cpu() for t in (o, ql.grad, kl.grad, vl.grad)]
 
 
-def test_cp_attention_gpu_matches_full(cuda):
+@pytest.mark.parametrize("packed", [False, True])
+def test_cp_attention_gpu_matches_full(cuda, packed):
+    """Dense rows, and packed rows (documents cut across the zig-zag chunks) against the
+    varlen flash attention over the full rows' documents."""
     import dtg.ops  # noqa: F401
     from dtg.parallel.context_parallel import unshard_zigzag
 
     q, k, v, do = (t.to(cuda) for t in _full())
     qs, ks, vs = (t.reshape(B * S, *t.shape[2:]) for t in (q, k, v))
-    cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=cuda)
-    o, lse = torch.ops.dtg.flash_attn_fwd(qs, ks, vs, cu, S, D ** -0.5, True)
-    grads = torch.ops.dtg.flash_attn_bwd(do.reshape(B * S, HQ, D), qs, ks, vs, o, lse, cu, S, D ** -0.5, True)
+    if packed:
+        bounds = [b * S + d for b in range(B) for d in DOCS[b]] + [B * S]
+        cu = torch.tensor(bounds, dtype=torch.int32, device=cuda)
+        mx = max(int(x) for x in (cu[1:] - cu[:-1]).tolist())
+    else:
+        cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=cuda)
+        mx = S
+    o, lse = torch.ops.dtg.flash_attn_fwd(qs, ks, vs, cu, mx, D ** -0.5, True)
+    grads = torch.ops.dtg.flash_attn_bwd(do.reshape(B * S, HQ, D), qs, ks, vs, o, lse, cu, mx, D ** -0.5, True)
     ref = [t.view(B, S, *t.shape[1:]).float().cpu() for t in (o,) + tuple(grads)]
-    res = run_distributed(_worker, 2)
+    res = run_distributed(_worker, 2, DOCS if packed else None)
     for i, name in enumerate(("out", "dq", "dk", "dv")):
         got = unshard_zigzag([r[i] for r in res], 2)
         rel = ((got - ref[i]).norm() / ref[i].norm()).item()

@@ -98,10 +98,11 @@ def _losses(path):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("flag,dataset", [("--sp", "synthetic:packed"), ("--cp", "synthetic")])
+@pytest.mark.parametrize("flag,dataset", [("--sp", "synthetic:packed"), ("--cp", "synthetic"),
+                                          ("--cp", "synthetic:packed:20")])
 def test_sequence_parallel_chapter_matches_single_process(tmp_path, flag, dataset):
     """rime chapter with each row split over 2 ranks (Ulysses on packed rows, context parallel on
-    dense rows) logs the same losses as one process reading the same batches."""
+    dense and packed rows) logs the same losses as one process reading the same batches."""
     base = ["-d", dataset, "-m", "llama-tiny-d128", "-s", "64", "--num-samples", "16", "--log-freq", "1",
             "--ckpt-freq", "100", "--num-workers", "0", "--max-steps", "3", "--lr", "1e-3"]
     one = _torchrun("00-rime", ["-e", "one", "--save-dir", str(tmp_path)] + base, nproc=1)
