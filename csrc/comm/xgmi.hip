@@ -301,6 +301,30 @@ void all_gather(int64_t id, const at::Tensor& out, const at::Tensor& inp) {
   barrier(c, 1, st);
 }
 
+// Copy-engine all-gather: the same stage -> barrier -> pull -> barrier protocol, but the stage
+// and the pulls are hipMemcpyAsync transfers (SDMA engines between GPUs) instead of kernels, so
+// an all-gather issued on a side stream while GEMMs run (parallel/async_tp.py) takes no CU time;
+// only the two one-wave barrier kernels touch the shader array.
+void all_gather_dma(int64_t id, const at::Tensor& out, const at::Tensor& inp) {
+  Comm& c = get(id);
+  check_io(c, inp, "input");
+  check_io(c, out, "output");
+  TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == inp.numel() * c.world, "xgmi all_gather: shape");
+  const int64_t bytes = inp.numel() * inp.element_size();
+  TORCH_CHECK(bytes <= c.capacity, "xgmi: message of ", bytes, " B exceeds the workspace (", c.capacity, " B)");
+  c10::DeviceGuard g(inp.device());
+  hipStream_t st = cur_stream();
+  ++c.epoch;
+  XGMI_CHECK(hipMemcpyAsync(c.base, inp.data_ptr(), bytes, hipMemcpyDeviceToDevice, st));
+  barrier(c, 0, st);
+  auto* o = static_cast<uint8_t*>(out.data_ptr());
+  for (int k = 0; k < c.world; ++k) {  // own shard first, then the peers in ring order
+    const int p = (c.rank + k) % c.world;
+    XGMI_CHECK(hipMemcpyAsync(o + (int64_t)p * bytes, c.peers.data[p], bytes, hipMemcpyDeviceToDevice, st));
+  }
+  barrier(c, 1, st);
+}
+
 void reduce_scatter(int64_t id, const at::Tensor& out, const at::Tensor& inp) {
   Comm& c = get(id);
   check_io(c, inp, "input");
@@ -351,6 +375,7 @@ TORCH_LIBRARY(dtg_xgmi, m) {
   m.def("error(int id) -> int", &error);
   m.def("destroy(int id) -> ()", &destroy);
   m.def("all_gather(int id, Tensor(a!) out, Tensor inp) -> ()", &all_gather);
+  m.def("all_gather_dma(int id, Tensor(a!) out, Tensor inp) -> ()", &all_gather_dma);
   m.def("reduce_scatter(int id, Tensor(a!) out, Tensor inp) -> ()", &reduce_scatter);
   m.def("all_reduce(int id, Tensor(a!) inout) -> ()", &all_reduce);
 }

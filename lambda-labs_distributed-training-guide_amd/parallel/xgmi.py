@@ -29,8 +29,13 @@ class XgmiError(RuntimeError):
 
 
 class XgmiCommunicator:
-    def __init__(self, group=None, capacity_bytes: int = 64 << 20, device=None, timeout_s: float = 10.0):
+    def __init__(self, group=None, capacity_bytes: int = 64 << 20, device=None, timeout_s: float = 10.0,
+                 gather_engine: str = "kernel"):
+        """gather_engine: "kernel" (pull kernels over all links at once) or "dma" (hipMemcpyAsync
+        copies on the copy engines: no CU time, for all-gathers overlapped with GEMMs)."""
         _native.require()
+        assert gather_engine in ("kernel", "dma"), gather_engine
+        self.gather_engine = gather_engine
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -57,7 +62,8 @@ class XgmiCommunicator:
         return nbytes <= self.capacity and nbytes % 16 == 0
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
-        torch.ops.dtg_xgmi.all_gather(self.id, out, inp.contiguous())
+        op = torch.ops.dtg_xgmi.all_gather_dma if self.gather_engine == "dma" else torch.ops.dtg_xgmi.all_gather
+        op(self.id, out, inp.contiguous())
         return out
 
     def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:

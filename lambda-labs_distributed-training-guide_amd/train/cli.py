@@ -47,9 +47,10 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     if chapter == "07":
         p.add_argument("--tp", default=8, type=int)
     if chapter in ("06", "07"):
-        p.add_argument("--tp-comm", default="rccl", choices=["rccl", "xgmi"],
+        p.add_argument("--tp-comm", default="rccl", choices=["rccl", "xgmi", "xgmi-dma"],
                        help="TP/SP all-gather / reduce-scatter / all-reduce: RCCL, or the direct-peer xGMI "
-                            "library (csrc/comm/xgmi.hip; one node per TP group)")
+                            "library (csrc/comm/xgmi.hip; one node per TP group); xgmi-dma moves the "
+                            "all-gathers on the copy engines (no CU time under the overlapped GEMMs)")
         p.add_argument("--tp-comm-mb", default=256, type=int, help="xGMI workspace per rank (largest TP message)")
         p.add_argument("--tp-overlap-chunks", default=2, type=int,
                        help="row chunks of the overlapped sequence-parallel regions (parallel/async_tp.py): the "

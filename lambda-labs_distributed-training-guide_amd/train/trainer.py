@@ -112,12 +112,15 @@ def _build(args, chapter, device, world):
         tp = max(1, min(tp, world))
         dp_group, tp_group, dp_rank, tp_rank, dp_size = make_mesh(tp)
         LOGGER.info(f"mesh: dp={dp_size} tp={tp} (dp_rank={dp_rank}, tp_rank={tp_rank})")
-        if getattr(args, "tp_comm", "rccl") == "xgmi" and tp_group is not None and device.type == "cuda":
+        if getattr(args, "tp_comm", "rccl").startswith("xgmi") and tp_group is not None and device.type == "cuda":
             from ..parallel.xgmi import XgmiCommunicator
             from ..utils import comm as _comm
 
-            _comm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=args.tp_comm_mb << 20, device=device))
-            LOGGER.info(f"tp collectives: direct-peer xGMI ({args.tp_comm_mb} MiB workspace per rank)")
+            engine = "dma" if args.tp_comm == "xgmi-dma" else "kernel"
+            _comm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=args.tp_comm_mb << 20, device=device,
+                                                           gather_engine=engine))
+            LOGGER.info(f"tp collectives: direct-peer xGMI ({args.tp_comm_mb} MiB workspace per rank, "
+                        f"all-gathers on {'copy engines' if engine == 'dma' else 'pull kernels'})")
     seq = None  # (kind, group, rank, degree): Ulysses / context parallel over each row
     nseq = max(getattr(args, "sp", 1), getattr(args, "cp", 1))
     if nseq > 1:

@@ -13,7 +13,7 @@ from _dist import run_distributed
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world):
+def _worker(rank, world, engine="kernel"):
     import torch.distributed as dist
 
     from dtg.parallel.xgmi import XgmiCommunicator
@@ -21,7 +21,7 @@ def _worker(rank, world):
 
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
-    c = XgmiCommunicator(None, capacity_bytes=8 << 20, device=dev, timeout_s=5.0)
+    c = XgmiCommunicator(None, capacity_bytes=8 << 20, device=dev, timeout_s=5.0, gather_engine=engine)
     out = {}
     for dtype in (torch.bfloat16, torch.float32):
         for n in (8, 4096, 1 << 20):
@@ -69,8 +69,10 @@ def _worker(rank, world):
     return out
 
 
-def test_xgmi_collectives_two_ranks(cuda):
-    res = run_distributed(_worker, 2)
+@pytest.mark.parametrize("engine", ["kernel", "dma"])
+def test_xgmi_collectives_two_ranks(cuda, engine):
+    """engine="dma": the all-gather's stage and pulls are copy-engine transfers (hipMemcpyAsync)."""
+    res = run_distributed(_worker, 2, engine)
     for r in range(2):
         for k, v in res[r].items():
             if k == "repeat":

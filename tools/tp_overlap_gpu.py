@@ -25,7 +25,7 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, ROOT)
 
 
-def _worker(rank, world, port, chunks_list, layers, batch, seq, steps, outdir):
+def _worker(rank, world, port, chunks_list, layers, batch, seq, steps, outdir, engine="kernel"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import torch
@@ -45,7 +45,7 @@ def _worker(rank, world, port, chunks_list, layers, batch, seq, steps, outdir):
     cfg = resolve_config("llama-3-8b", num_hidden_layers=layers)
     torch.manual_seed(0)
     model = build_model(cfg, device=dev, tp_group=tp_group)
-    dcomm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=512 << 20, device=dev))
+    dcomm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=512 << 20, device=dev, gather_engine=engine))
     eng = DataParallel(model, mode="single", tp_group=tp_group, broadcast_from_rank0=False)
     opt = FlatAdamW(eng, lr=1e-5)
     g = torch.Generator().manual_seed(0)
@@ -133,6 +133,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--out", default="gpurun_out/tp_overlap")
     ap.add_argument("--trace", default=None, help="summarise a rocprofv3 --kernel-trace directory instead")
+    ap.add_argument("--engine", default="kernel", choices=["kernel", "dma"], help="xGMI all-gather engine")
     a = ap.parse_args()
     if a.trace:
         print(json.dumps(trace_overlap(a.trace), indent=1))
@@ -146,7 +147,7 @@ def main():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.start_processes(_worker, args=(2, port, a.chunks, a.layers, a.batch, a.seq, a.steps, a.out), nprocs=2,
+    mp.start_processes(_worker, args=(2, port, a.chunks, a.layers, a.batch, a.seq, a.steps, a.out, a.engine), nprocs=2,
                        join=True, start_method="spawn")
     print(open(os.path.join(a.out, "result.json")).read())
 
