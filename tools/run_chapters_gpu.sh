@@ -2,12 +2,13 @@
 # Every chapter's train_llm.py end to end on one MI355X (synthetic data, short runs; checkpoints
 # are covered by the CPU tests: an 8B sharded checkpoint is ~64 GB), logs under gpurun_out/<tag>.
 # Usage: gpurun -- bash tools/run_chapters_gpu.sh <tag> [name-regex]
+# EXTRA_ARGS is appended to every command (e.g. EXTRA_ARGS="--tunableop tune").
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-chapters}
 mkdir -p $OUT
 export TMPDIR=/tmp
 TR="python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29571"
-COMMON="-d synthetic --save-dir ${TMPDIR:-/tmp}/dtg_chapters_out --ckpt-freq 1000 --num-workers 2"
+COMMON="-d synthetic --save-dir ${TMPDIR:-/tmp}/dtg_chapters_out --ckpt-freq 1000 --num-workers 2 ${EXTRA_ARGS:-}"
 ONLY=${2:-.}
 run() {  # name, dir, command...
   local name=$1 dir=$2; shift 2
