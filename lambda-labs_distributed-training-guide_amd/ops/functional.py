@@ -232,6 +232,33 @@ def rope(qkv, cos, sin, pos, nheads, head_dim):
     return _Rope.apply(qkv, cos, sin, pos, int(nheads), int(head_dim))
 
 
+FA_HEAD_DIMS = (64, 128)  # head dims the flash-attention kernels are instantiated for
+
+
+def _attention_padded(qkv, nq, nkv, d, cu_seqlens, max_seqlen, cos, sin, pos, causal, scale, window):
+    """Head dims without a kernel instantiation (e.g. 80, 96, 48): zero-pad every head to the next
+    instantiated width.  Zero columns add nothing to q.k (the scale keeps 1/sqrt(d) of the true
+    width) and give zero output columns, which are sliced off; autograd drops their gradients.
+    Costs the padded width's FLOPs, not a second code path."""
+    dp = next((x for x in FA_HEAD_DIMS if x >= d), None)
+    if dp is None or d % 2:
+        raise ValueError(f"attention: head_dim {d} unsupported (kernels: {FA_HEAD_DIMS}; smaller even dims are padded)")
+    T = qkv.shape[0]
+    x = qkv.reshape(T, nq + 2 * nkv, d)
+    if cos is not None:  # RoPE out of place in torch (the rope kernel is instantiated for 64/128 too)
+        h = d // 2
+        qk = x[:, : nq + nkv].float()
+        c, s = cos[pos][:, None, :], sin[pos][:, None, :]
+        x1, x2 = qk[..., :h], qk[..., h:]
+        rot = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1).to(x.dtype)
+        x = torch.cat([rot, x[:, nq + nkv:]], 1)
+    xp = F.pad(x, (0, dp - d)).reshape(T, (nq + 2 * nkv) * dp)
+    e = torch.empty(0, device=qkv.device)
+    o = _AttentionQKV.apply(xp, e, e, torch.empty(0, dtype=torch.long, device=qkv.device), cu_seqlens, int(max_seqlen),
+                            nq, nkv, dp, float(scale), causal, False, int(window or 0))
+    return o.view(T, nq, dp)[..., :d].reshape(T, nq * d)
+
+
 def attention(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos=None, sin=None, pos=None, causal=True, scale=None,
               window=0):
     """Causal (varlen) GQA attention on a fused [T, (nq+2nkv)*d] QKV activation -> [T, nq*d].
@@ -240,6 +267,8 @@ def attention(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos=None, sin=None
     sliding-window attention (query i sees keys i - window < j <= i; Mistral)."""
     if scale is None:
         scale = 1.0 / math.sqrt(head_dim)
+    if qkv.is_cuda and head_dim not in FA_HEAD_DIMS:  # the CPU reference takes any width
+        return _attention_padded(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos, sin, pos, causal, scale, window)
     rope = cos is not None
     if not rope:
         cos = sin = torch.empty(0, device=qkv.device)

@@ -276,6 +276,30 @@ def test_flash_attn_sliding_window(cuda, window, D, hq, hkv):
     _attn_case(cuda, [1024, 77, 300], hq=hq, hkv=hkv, D=D, causal=True, window=window)
 
 
+@pytest.mark.parametrize("d", [80, 96])
+def test_attention_padded_head_dims(cuda, d):
+    """ops.attention with head dims the kernels are not instantiated for (zero-padded to 128 on
+    the GPU) vs the fp32 CPU reference: output and the fused qkv gradient, RoPE on."""
+    from dtg import ops as fops
+
+    torch.manual_seed(0)
+    lens = [300, 77]
+    T, hq, hkv = sum(lens), 8, 2
+    cu = torch.tensor([0, 300, 377], dtype=torch.int32)
+    cos, sin = fops.rope_tables(d, 10000.0, 512)
+    pos = torch.cat([torch.arange(n) for n in lens])
+    qkv = torch.randn(T, (hq + 2 * hkv) * d).bfloat16()
+    do = torch.randn(T, hq * d).bfloat16()
+    ref_in = qkv.float().requires_grad_()
+    o_ref = fops.attention(ref_in.clone(), hq, hkv, d, cu, 300, cos, sin, pos)
+    o_ref.backward(do.float())
+    g_in = qkv.to(cuda).requires_grad_()
+    o = fops.attention(g_in, hq, hkv, d, cu.to(cuda), 300, cos.to(cuda), sin.to(cuda), pos.to(cuda))
+    o.backward(do.to(cuda))
+    _close(o, o_ref, 2e-2, 2e-2, "padded attn out")
+    assert _rel(g_in.grad, ref_in.grad) < 2e-2, _rel(g_in.grad, ref_in.grad)
+
+
 def test_flash_attn_bwd_qkv_fused(cuda):
     torch.manual_seed(0)
     T, hq, hkv, D = 384, 4, 1, 128

@@ -134,6 +134,38 @@ def test_attention_op_matches_sdpa_varlen_gqa():
     torch.testing.assert_close(qkv.grad, qkv2.grad, atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("d,window", [(48, 0), (80, 0), (96, 5), (112, 0)])
+def test_attention_padded_head_dim_matches_direct(d, window):
+    """Head dims without a flash-kernel instantiation run zero-padded to 64/128 on the GPU
+    (ops.functional._attention_padded): same output and qkv gradient as the unpadded op,
+    RoPE included."""
+    from dtg.ops.functional import _attention_padded
+
+    torch.manual_seed(0)
+    lens = [9, 23]
+    T, hq, hkv = sum(lens), 4, 2
+    cu = torch.tensor([0, 9, 32], dtype=torch.int32)
+    cos, sin = ops.rope_tables(d, 10000.0, 64)
+    pos = torch.cat([torch.arange(n) for n in lens])
+    qkv = torch.randn(T, (hq + 2 * hkv) * d, requires_grad=True)
+    qkv2 = qkv.detach().clone().requires_grad_()
+    o = _attention_padded(qkv, hq, hkv, d, cu, max(lens), cos, sin, pos, True, 1 / math.sqrt(d), window)
+    o2 = ops.attention(qkv2.clone(), hq, hkv, d, cu, max(lens), cos, sin, pos, window=window)
+    torch.testing.assert_close(o, o2, atol=1e-5, rtol=1e-5)
+    g = torch.randn_like(o)
+    o.backward(g)
+    o2.backward(g)
+    torch.testing.assert_close(qkv.grad, qkv2.grad, atol=1e-4, rtol=1e-4)
+
+
+def test_attention_padded_rejects_wide_heads():
+    from dtg.ops.functional import _attention_padded
+
+    with pytest.raises(ValueError, match="head_dim 256"):
+        _attention_padded(torch.zeros(4, 3 * 256), 1, 1, 256, torch.tensor([0, 4], dtype=torch.int32), 4,
+                          None, None, None, True, 0.1, 0)
+
+
 def test_adamw_cpu_matches_torch_adamw():
     torch.manual_seed(0)
     p = torch.randn(1000)
