@@ -17,6 +17,11 @@ TABLE = os.path.join(ROOT, "tunableop", "tunableop_results_partial.csv")
 def enable_tunableop(tune: bool = False, max_tuning_ms: int = 30, table: str = TABLE):
     os.makedirs(os.path.dirname(table), exist_ok=True)
     t = torch.cuda.tunable
+    record = os.environ.get("DTG_TUNABLEOP_RECORD")
+    if record:
+        # list the GEMM shapes the table lacks, for offline tuning with tools/tune_gemms.py
+        os.environ["PYTORCH_TUNABLEOP_UNTUNED_FILENAME"] = record
+        t.record_untuned_enable(True)
     t.enable(True)
     if not tune:
         # Read-only use: point TunableOp's own results file at a per-process scratch copy so

@@ -1,87 +1,147 @@
 #!/usr/bin/env python3
-"""Tune the hipBLASLt/rocBLAS solution of every Linear GEMM of a model with PyTorch TunableOp,
-one shape at a time, and merge the winners into the committed table (tunableop/).
+"""Offline GEMM tuning on one MI355X: tune the GEMM shapes a run recorded, one shape at a time,
+saving the winners after every shape so that a time limit never loses finished work.
 
-Each GEMM is issued exactly as the training step issues it (ops.functional._Linear: forward
-x @ w^T, dX = dY @ w, dW = dY^T @ x into a preallocated gradient), so the TunableOp keys match.
-A heartbeat line is printed every 30 s while a shape is being tuned.
+Two steps (the framework's runs read the committed table `tunableop/tunableop_results_partial.csv`):
 
-    python tools/tune_gemms.py --model llama-3-8b --tokens 16384 --which dw
+    # 1. record: any training/bench run with DTG_TUNABLEOP_RECORD set lists the GEMM shapes the
+    #    committed table lacks (dtg.utils.gemm_tuning.enable_tunableop)
+    DTG_TUNABLEOP_RECORD=/tmp/untuned.csv python bench.py --model llama-2-7b --batch-size 10
+    # 2. tune them (rewrites <out> after each shape), then merge into the committed table
+    python tools/tune_gemms.py "/tmp/untuned*.csv" --out gpurun_out/tuned.csv --budget-s 600
+    python tools/merge_tunableop.py tunableop/tunableop_results_partial.csv gpurun_out/tuned.csv
+
+The tuning runs in a worker process; the parent (which never touches the GPU) prints progress,
+and kills and restarts the worker past a shape that exceeds --shape-timeout-s (e.g. a head GEMM
+over an odd 156,939-wide vocabulary where some library candidates are pathologically slow), so
+one bad shape costs its timeout and nothing else.  Online tuning inside a training step
+(`--tunableop tune`) does the same work, but a run killed by its time limit keeps none of it.
 """
 import argparse
+import glob
+import json
 import os
+import subprocess
 import sys
-import threading
+import tempfile
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
-def shapes(cfg):
-    h, i = cfg.hidden_size, cfg.intermediate_size
-    hd = h // cfg.num_attention_heads
-    qkv = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * hd
-    return {"qkv": (qkv, h), "o": (h, h), "gate_up": (2 * i, h), "down": (h, i), "lm_head": (cfg.vocab_size, h)}
+def _shapes(patterns, known):
+    seen, out = set(), []
+    for pat in patterns:
+        for f in sorted(glob.glob(pat)):
+            for line in open(f):
+                parts = line.strip().split(",")
+                if len(parts) < 2 or not parts[0].startswith("Gemm"):
+                    continue
+                key = (parts[0], parts[1])
+                if key in seen or key in known:
+                    continue
+                seen.add(key)
+                out.append(line.strip())
+    return out
+
+
+def _known(table):
+    if not os.path.exists(table):
+        return set()
+    return {tuple(l.split(",")[:2]) for l in open(table) if l.startswith("Gemm")}
+
+
+def _worker(shapes_file, results_file, max_tuning_ms):
+    """Tune every shape in shapes_file in order; after each, append its result line (JSON)."""
+    import torch
+
+    t = torch.cuda.tunable
+    t.enable(True)
+    t.set_filename(os.path.join(tempfile.gettempdir(), f"dtg_tune_{os.getpid()}.csv"), insert_device_ordinal=False)
+    t.tuning_enable(True)
+    t.set_max_tuning_duration(max_tuning_ms)
+    t.set_max_tuning_iterations(50)
+    one = os.path.join(tempfile.gettempdir(), f"dtg_tune_one_{os.getpid()}.csv")
+    for line in open(shapes_file).read().splitlines():
+        with open(one, "w") as fp:
+            fp.write(line + "\n")
+        s = time.time()
+        t.tune_gemm_in_file(one)
+        torch.cuda.synchronize()
+        key = tuple(line.split(",")[:2])
+        best = next((list(r) for r in t.get_results() if (r[0], r[1]) == key), None)
+        with open(results_file, "a") as fp:
+            fp.write(json.dumps({"shape": line, "result": best, "s": round(time.time() - s, 1)}) + "\n")
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="llama-3-8b")
-    ap.add_argument("--tokens", type=int, default=16384)
-    ap.add_argument("--which", default="dw", help="comma list of fwd,dx,dw,dx_tn,dw_tn")
-    ap.add_argument("--only", default="", help="comma list of qkv,o,gate_up,down")
-    ap.add_argument("--out", default="gpurun_out/tunableop_new.csv")
-    ap.add_argument("--max-ms", type=int, default=20)
-    ap.add_argument("--iters", type=int, default=10)
-    a = ap.parse_args()
-    import torch
+    ap.add_argument("untuned", nargs="*", help="untuned-shape CSV files (globs ok)")
+    ap.add_argument("--out", help="results CSV (rewritten after every shape)")
+    ap.add_argument("--table", default=None, help="committed table; its shapes are skipped")
+    ap.add_argument("--budget-s", type=float, default=600.0, help="stop starting new shapes after this")
+    ap.add_argument("--shape-timeout-s", type=float, default=90.0)
+    ap.add_argument("--max-tuning-ms", type=int, default=30)
+    ap.add_argument("--worker", nargs=2, metavar=("SHAPES", "RESULTS"), help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.worker:
+        return _worker(args.worker[0], args.worker[1], args.max_tuning_ms)
 
-    import dtg  # noqa: F401
-    from dtg.models import resolve_config
-
-    cfg = resolve_config(a.model)
-    t = torch.cuda.tunable
-    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
-    t.enable(True)
-    t.set_filename(a.out, insert_device_ordinal=False)
-    t.tuning_enable(True)
-    t.set_max_tuning_duration(a.max_ms)
-    t.set_max_tuning_iterations(a.iters)
-    current = {"name": "", "t0": time.time()}
-
-    def beat():
+    table = args.table or os.path.join(ROOT, "tunableop", "tunableop_results_partial.csv")
+    todo = _shapes(args.untuned, _known(table))
+    print(f"[tune_gemms] {len(todo)} new GEMM shapes", flush=True)
+    header = [l for l in open(table) if l.startswith("Validator")] if os.path.exists(table) else []
+    work = tempfile.mkdtemp(prefix="dtg_tune_")
+    results_file = os.path.join(work, "results.jsonl")
+    open(results_file, "w").close()
+    tuned, skipped = {}, []
+    n_seen = 0
+    t0 = time.time()
+    while todo and time.time() - t0 < args.budget_s:
+        shapes_file = os.path.join(work, "shapes.csv")
+        with open(shapes_file, "w") as fp:
+            fp.write("\n".join(todo) + "\n")
+        proc = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--worker", shapes_file, results_file,
+                                 "--max-tuning-ms", str(args.max_tuning_ms)])
+        last = time.time()
         while True:
-            time.sleep(30)
-            print(f"[tune] {current['name']} ... {time.time() - current['t0']:.0f}s", flush=True)
-
-    threading.Thread(target=beat, daemon=True).start()
-    dev = torch.device("cuda")
-    T = a.tokens
-    which = a.which.split(",")
-    only = [s for s in a.only.split(",") if s]
-    for name, (out_f, in_f) in shapes(cfg).items():
-        if (only and name not in only) or (not only and name == "lm_head"):
-            continue  # the loss head runs per chunk: tune it with --only lm_head --tokens <chunk>
-        x = torch.randn(T, in_f, device=dev, dtype=torch.bfloat16)
-        w = torch.randn(out_f, in_f, device=dev, dtype=torch.bfloat16) * 0.02
-        dy = torch.randn(T, out_f, device=dev, dtype=torch.bfloat16)
-        mg = torch.empty(out_f, in_f, device=dev, dtype=torch.bfloat16)
-        wt, dyt, xt = w.t().contiguous(), dy.t().contiguous(), x.t().contiguous()
-        jobs = {"fwd": lambda: torch.mm(x, w.t()), "dx": lambda: torch.mm(dy, w),
-                "dw": lambda: torch.mm(dy.t(), x, out=mg),
-                # the TN forms issued by ops.functional._Linear (DTG_LINEAR_BWD=tn, the default)
-                "dx_tn": lambda: torch.mm(dy, wt.t()), "dw_tn": lambda: torch.mm(dyt, xt.t(), out=mg)}
-        for k in which:
-            current["name"], current["t0"] = f"{name}/{k}", time.time()
-            jobs[k]()
-            torch.cuda.synchronize()
-            print(f"[tune] {name}/{k} done in {time.time() - current['t0']:.1f}s", flush=True)
-        del x, w, dy, mg, wt, dyt, xt
-        torch.cuda.empty_cache()
-    from dtg.utils.gemm_tuning import save_tunableop
-
-    save_tunableop(a.out)
-    print(f"[tune] wrote {a.out}", flush=True)
+            time.sleep(1.0)
+            lines = open(results_file).read().splitlines()
+            for rec in map(json.loads, lines[n_seen:]):
+                todo.remove(rec["shape"])
+                r = rec["result"]
+                if r:
+                    tuned[tuple(r[:2])] = r
+                print(f"[tune_gemms] {len(tuned)} done, {len(todo)} left: {rec['shape'].split(',')[1]} -> "
+                      f"{r[2] if r else '?'} {float(r[3]) if r else 0:.4f} ms ({rec['s']}s)", flush=True)
+                last = time.time()
+            n_seen = len(lines)
+            if args.out and tuned:
+                tmp = args.out + ".tmp"
+                with open(tmp, "w") as fp:
+                    fp.write("".join(header) + "".join(",".join(str(x) for x in r) + "\n" for r in tuned.values()))
+                os.replace(tmp, args.out)
+            if proc.poll() is not None:
+                break
+            if time.time() - last > args.shape_timeout_s or time.time() - t0 > args.budget_s + args.shape_timeout_s:
+                proc.kill()
+                proc.wait()
+                if todo and time.time() - last > args.shape_timeout_s:
+                    bad = todo.pop(0)
+                    skipped.append(bad)
+                    print(f"[tune_gemms] skipped after {args.shape_timeout_s:.0f}s: {bad.split(',')[1]}", flush=True)
+                break
+            if int(time.time() - t0) % 30 == 0:
+                print(f"[tune_gemms] ... {time.time() - t0:.0f}s, tuning {todo[0].split(',')[1] if todo else ''}",
+                      flush=True)
+        if proc.returncode not in (0, -9):
+            # the worker died on its own (a fault, an abort): nothing more goes to the GPU
+            print(f"[tune_gemms] worker exited {proc.returncode} on {todo[0].split(',')[1] if todo else '?'}; stopping",
+                  flush=True)
+            break
+    print(f"[tune_gemms] tuned {len(tuned)}, skipped {len(skipped)}, untouched {len(todo)} "
+          f"in {time.time() - t0:.0f}s -> {args.out}", flush=True)
 
 
 if __name__ == "__main__":
