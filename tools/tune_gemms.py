@@ -97,7 +97,7 @@ def main():
     open(results_file, "w").close()
     tuned, skipped = {}, []
     n_seen = 0
-    t0 = time.time()
+    t0 = last_print = time.time()
     while todo and time.time() - t0 < args.budget_s:
         shapes_file = os.path.join(work, "shapes.csv")
         with open(shapes_file, "w") as fp:
@@ -132,7 +132,8 @@ def main():
                     skipped.append(bad)
                     print(f"[tune_gemms] skipped after {args.shape_timeout_s:.0f}s: {bad.split(',')[1]}", flush=True)
                 break
-            if int(time.time() - t0) % 30 == 0:
+            if time.time() - last_print > 30:
+                last_print = time.time()
                 print(f"[tune_gemms] ... {time.time() - t0:.0f}s, tuning {todo[0].split(',')[1] if todo else ''}",
                       flush=True)
         if proc.returncode not in (0, -9):
