@@ -49,6 +49,12 @@ def parse(argv=None):
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--parallel", default="zero", choices=["ddp", "zero", "fsdp"])
     ap.add_argument("--bucket-mb", type=int, default=256)
+    # BASELINE config 06 (Llama-3-8B TP=8 over xGMI): --tp 8 --gpus 8.  Tensor + sequence parallel
+    # inside groups of --tp ranks, data parallel (--parallel) across them; a step is dp x B x S
+    # tokens (the reference's TP tok/s formula, 06-tensor-parallel/train_llm.py:256).
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--tp-comm", default="rccl", choices=["rccl", "xgmi", "xgmi-dma"])
+    ap.add_argument("--tp-overlap-chunks", type=int, default=2)
     ap.add_argument("--overlap-optimizer", type=int, default=0,
                     help="1: per-bucket AdamW (and ZeRO all-gather) on a side stream during backward (measured +0.2%% on 1 GPU, off)")
     ap.add_argument("--lr", type=float, default=3e-5)
@@ -101,19 +107,35 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
 
     cfg = resolve_config(args.model)
-    model = build_model(cfg, device=device)
+    dp_group = tp_group = xgmi = None
+    dp_size, dp_rank = world, rank
+    if args.tp > 1:
+        from dtg.parallel.tensor_parallel import make_mesh
+
+        dp_group, tp_group, dp_rank, _, dp_size = make_mesh(args.tp)
+        if args.tp_comm != "rccl" and cuda:
+            from dtg.parallel.xgmi import XgmiCommunicator
+            from dtg.utils import comm as _comm
+
+            xgmi = XgmiCommunicator(tp_group, capacity_bytes=256 << 20, device=device,
+                                    gather_engine="dma" if args.tp_comm == "xgmi-dma" else "kernel")
+            _comm.register_xgmi(tp_group, xgmi)
+    model = build_model(cfg, device=device, tp_group=tp_group)
+    if tp_group is not None:
+        model.tp.overlap_chunks = max(1, args.tp_overlap_chunks)
     if args.parallel == "fsdp":
         from dtg.parallel.fsdp import FullyShard
 
-        engine = FullyShard(model)
+        engine = FullyShard(model, group=dp_group, tp_group=tp_group)
     else:
-        engine = DataParallel(model, mode=args.parallel if world > 1 else "single", bucket_mb=args.bucket_mb,
+        engine = DataParallel(model, mode=args.parallel if dp_size > 1 else "single", group=dp_group, tp_group=tp_group,
+                              bucket_mb=args.bucket_mb, broadcast_from_rank0=tp_group is None,
                               overlap_optimizer=bool(args.overlap_optimizer))
     opt = FlatAdamW(engine, lr=args.lr)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=1000, eta_min=args.lr * 1e-2)
 
     B, S = args.batch_size, args.seq_len
-    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    g = torch.Generator(device=device).manual_seed(1234 + dp_rank)  # one batch per TP group
     batches = [torch.randint(0, cfg.vocab_size, (B, S), device=device, generator=g) for _ in range(4)]
     num_valid = B * (S - 1)
 
@@ -159,9 +181,16 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
             with open(os.path.join(ROOT, "gpurun_out", "torch_profile.txt"), "w") as fp:
                 fp.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
     res = dict(elapsed=elapsed, peak_gb=peak_gb, loss=float(loss.item()), cfg=cfg,
-               mode=getattr(engine, "mode", args.parallel))
+               mode=getattr(engine, "mode", args.parallel), dp=dp_size)
     if hasattr(engine, "wait_param_gather"):
         engine.wait_param_gather()
+    if xgmi is not None:
+        torch.cuda.synchronize()
+        xgmi.check()
+        from dtg.utils import comm as _comm
+
+        _comm.unregister_xgmi(tp_group)
+        xgmi.close()
     del model, engine, opt, sched, batches, loss
     return res
 
@@ -313,7 +342,8 @@ def main(argv=None):
 
     cfg = res["cfg"]
     B, S = args.batch_size, args.seq_len
-    tokens = world * B * S * args.steps
+    dp = res["dp"]
+    tokens = dp * B * S * args.steps
     tps = tokens / elapsed
     ms = 1000 * elapsed / args.steps
     flops_tok = cfg.flops_per_token(S)
@@ -332,8 +362,8 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (uniform random token ids), random-init weights",
-            "config": {"model": cfg.hf_name or args.model, "global_batch": world * B, "seq_len": S,
-                       "parallelism": f"dp{world}-{res['mode']}"},
+            "config": {"model": cfg.hf_name or args.model, "global_batch": dp * B, "seq_len": S,
+                       "parallelism": f"dp{dp}-{res['mode']}" + (f"-tp{args.tp}-{args.tp_comm}" if args.tp > 1 else "")},
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
             "peak_mem_gb": round(max(r[2] for r in rows), 2),

@@ -80,3 +80,20 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + ARGS,
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+@pytest.mark.slow
+def test_bench_tensor_parallel_two_ranks():
+    """BASELINE config 06 shape: `--tp 2` on 2 ranks is one TP group (dp = 1), so a step is
+    1 x B x S tokens (the reference's TP formula) and both ranks train the same batch."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--tp", "2"] + ARGS
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 2
+    assert rec["config"]["parallelism"] == "dp1-single-tp2-rccl"
+    assert abs(rec["value"] - 2 * 64 * 2 / (rec["ms_per_step"] * 2 / 1000)) < 0.02 * rec["value"]
