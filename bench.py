@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -182,6 +183,9 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
                 fp.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
     res = dict(elapsed=elapsed, peak_gb=peak_gb, loss=float(loss.item()), cfg=cfg,
                mode=getattr(engine, "mode", args.parallel), dp=dp_size)
+    if not math.isfinite(res["loss"]):
+        # a step that produced NaN/inf (e.g. a wrong GEMM solution) is not a measurement
+        raise SystemExit(f"bench.py: rank {rank} final loss is {res['loss']}; refusing to report a throughput")
     if hasattr(engine, "wait_param_gather"):
         engine.wait_param_gather()
     if xgmi is not None:

@@ -98,6 +98,19 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Reductions of x over the lane pair (l, l ^ 32): v_permlane32_swap(x, x) leaves x[l & 31] and
+// x[32 + (l & 31)] in its two results on every lane (VALU only; __shfl_xor compiles to
+// ds_bpermute_b32, whose LDS round trip sits on the softmax's dependency chain).  max and +
+// are commutative, so the result is bitwise the shuffle form's.
+__device__ __forceinline__ float pair_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // Scheduling hints (T19) for a region of n MFMAs fed by n*rpm LDS reads: keep `ahead` reads in
 // flight in front of the MFMA chain instead of hipcc's read -> wait -> MFMA serialisation.
 constexpr int kSchedMfma = 0x008, kSchedDsRead = 0x100;
@@ -360,7 +373,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kt][i]);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * P.c2;
+      mx = pair_max(mx) * P.c2;
       if (__builtin_amdgcn_ballot_w64(mx > m + kRescaleThreshold) != 0) {
         const float mn = fmaxf(m, mx);
         const float alpha = (mn == -INFINITY) ? 1.f : fexp2(m - mn);
@@ -412,7 +425,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   if (t < ntiles) tile_step(t, std::integral_constant<int, 0>{});
   fa_stamp(P.stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), 2);
 
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = pair_sum(l);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   uint16_t* op = P.o + ((int64_t)(s0 + min(qrow, seqlen - 1)) * P.hq + head) * D;
   if constexpr (WIDE) {

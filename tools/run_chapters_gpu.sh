@@ -17,6 +17,9 @@ run() {  # name, dir, command...
   local rc=$?
   echo "$name rc=$rc"; grep -E "global_step" $OUT/$name.log | tail -1 | grep -oE "'(global_step|tok/s|peak_alloc_gb|peak_alloc_in_gb|time/forward|time/backward|time/update)': [0-9.e+-]+" | tr '\n' ' '; echo
   [ $rc -ne 0 ] && tail -40 $OUT/$name.log
+  # a run whose loss went non-finite is not a measurement (r2_s32: two chapters timed with NaN
+  # losses from a wrong pinned GEMM solution, see tools/check_tunableop.py)
+  if [ $rc -eq 0 ] && grep -qE "'running_loss': (nan|inf)" $OUT/$name.log; then echo "$name: non-finite loss"; rc=3; fi
   return $rc
 }
 ( while sleep 30; do echo "[chapters] alive $(date +%T)"; done ) &

@@ -54,6 +54,11 @@ def _known(table):
 
 def _worker(shapes_file, results_file, max_tuning_ms):
     """Tune every shape in shapes_file in order; after each, append its result line (JSON)."""
+    # Compare every candidate's output with the default kernel's and drop the ones that differ:
+    # without this TunableOp ranks on time alone, and one hipBLASLt solution for GPT-2's batched
+    # attention-score GEMM (tn_1024_1024_64_B_96) returned values of order 1e33 -- NaN losses
+    # (found by tools/check_tunableop.py, profiles/r2_s35/).
+    os.environ.setdefault("PYTORCH_TUNABLEOP_NUMERICAL_CHECK", "1")
     import torch
 
     t = torch.cuda.tunable
