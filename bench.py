@@ -352,6 +352,8 @@ def main(argv=None):
     ms = 1000 * elapsed / args.steps
     flops_tok = cfg.flops_per_token(S)
     mfu = tps * flops_tok / (world * 2.5e15) if cuda else 0.0
+    # TP collectives: "rccl" means the process group's own backend (gloo in CPU / shared-GPU rehearsals)
+    tp_comm_label = args.tp_comm if args.tp_comm != "rccl" else ("rccl" if backend in (None, "nccl") else backend)
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -367,7 +369,7 @@ def main(argv=None):
             "dtype": "bf16",
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": cfg.hf_name or args.model, "global_batch": dp * B, "seq_len": S,
-                       "parallelism": f"dp{dp}-{res['mode']}" + (f"-tp{args.tp}-{args.tp_comm}" if args.tp > 1 else "")},
+                       "parallelism": f"dp{dp}-{res['mode']}" + (f"-tp{args.tp}-{tp_comm_label}" if args.tp > 1 else "")},
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
             "peak_mem_gb": round(max(r[2] for r in rows), 2),

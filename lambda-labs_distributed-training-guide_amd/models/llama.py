@@ -202,10 +202,11 @@ class _VocabParallelEmbedding(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         local, mask = ctx.saved_tensors
-        dy = dy.masked_fill(mask[:, None], 0)
         from ..ops.grad_routing import route_embedding_grad
 
-        return None, route_embedding_grad(ctx.w, local, dy.contiguous(), ctx.w.shape[0]), None
+        # out-of-shard tokens get id -1, which embedding_bwd_ skips: no zeroed dy copy, and no
+        # single run of ~(tp-1)/tp of all tokens on row 0 for the segment sum to walk
+        return None, route_embedding_grad(ctx.w, local.masked_fill(mask, -1), dy.contiguous(), ctx.w.shape[0]), None
 
 
 class LlamaForCausalLM(nn.Module):

@@ -245,8 +245,11 @@ def transpose2d(x):
 
 
 def embedding_bwd_(out, ids, dy):
+    """out[id] += sum of dy rows with that id, f32 sums rounded once; ids outside [0, V) skipped."""
     acc = torch.zeros(out.shape, dtype=torch.float32)
-    acc.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).float())
+    ids = ids.reshape(-1)
+    keep = (ids >= 0) & (ids < out.shape[0])
+    acc.index_add_(0, ids[keep], dy.reshape(-1, dy.shape[-1])[keep].float())
     out.copy_((out.float() + acc).to(out.dtype))
 
 

@@ -360,6 +360,31 @@ def test_embedding_bwd_deterministic(cuda, T, V, H):
     _close(outs[0], ref, atol=2e-2, rtol=1e-2, name="embedding_bwd")
 
 
+@pytest.mark.parametrize("T,V,H,skip", [(16384, 16032, 4096, 7 / 8), (20001, 3, 520, 0.0), (4100, 64, 1032, 0.5)])
+def test_embedding_bwd_long_runs_and_skipped_ids(cuda, T, V, H, skip):
+    """Runs far longer than one chunk (a frequent token; T = 20001 over 3 ids) and ids of -1
+    (vocab-parallel out-of-shard tokens, 7/8 of them at TP = 8): chunked partial sums merged in
+    order match the f32 reference, skipped ids add nothing, and two calls agree bit for bit."""
+    torch.manual_seed(1)
+    ids = torch.randint(0, V, (T,))
+    ids[torch.rand(T) < skip] = -1
+    dy = torch.randn(T, H).bfloat16()
+    base = torch.randn(V, H).bfloat16()
+    ref = base.clone()
+    dops.embedding_bwd_(ref, ids, dy)  # CPU f32 reference (skips ids outside [0, V))
+    outs = []
+    for _ in range(2):
+        o = base.to(cuda)
+        dops.embedding_bwd_(o, ids.to(cuda), dy.to(cuda))
+        torch.cuda.synchronize()
+        outs.append(o.cpu())
+    assert torch.equal(outs[0], outs[1])
+    _close(outs[0], ref, atol=5e-2, rtol=1e-2, name="embedding_bwd_long")
+    untouched = torch.ones(V, dtype=torch.bool)
+    untouched[ids[ids >= 0].unique()] = False
+    assert torch.equal(outs[0][untouched], base[untouched])
+
+
 @pytest.mark.parametrize("D,hq,hkv", [(128, 8, 2), (64, 4, 4)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attn_varlen_key_ranges(cuda, D, hq, hkv, causal):
