@@ -176,12 +176,27 @@ def _attn_ref(q, k, v, cu_seqlens, scale, causal, k_start=None, k_len=None, wind
     return o, lse
 
 
+def _check_qkv(t, name, heads, d):
+    """check_qkv of csrc/kernels/flash_attn.hip: [T, H, D], contiguous heads, 16-B token stride."""
+    if not (t.dim() == 3 and t.shape[1] == heads and t.shape[2] == d and t.stride(2) == 1 and t.stride(1) == d
+            and t.stride(0) % 8 == 0):
+        raise RuntimeError(f"dtg: {name} must be [T, H, D] with contiguous heads and 16-B aligned token stride")
+
+
+def _check_attn_inputs(q, k, v):
+    _check_qkv(q, "q", q.shape[1], q.shape[2])
+    _check_qkv(k, "k", k.shape[1], q.shape[2])
+    _check_qkv(v, "v", k.shape[1], q.shape[2])
+
+
 def flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal, window=0):
+    _check_attn_inputs(q, k, v)
     o, lse = _attn_ref(q, k, v, cu_seqlens, scale, causal, window=window)
     return o.to(q.dtype), lse
 
 
 def flash_attn_varlen_fwd(q, k, v, cu_seqlens_q, k_start, k_len, max_seqlen_q, max_seqlen_k, scale, causal):
+    _check_attn_inputs(q, k, v)
     o, lse = _attn_ref(q, k, v, cu_seqlens_q, scale, causal, k_start, k_len)
     return o.to(q.dtype), lse
 
@@ -191,6 +206,14 @@ def flash_attn_bwd(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal,
     with the GIVEN o (so a block of a larger softmax -- context parallelism -- gets the
     gradient of the full softmax)."""
     T, hq, d = q.shape
+    _check_attn_inputs(q, k, v)
+    # the HIP entry point's layout contract (csrc/kernels/flash_attn.hip), checked here too so the
+    # CPU suite catches a caller that would only fail on the GPU (the rime --cp path passed a
+    # strided per-slot view of the LSE at batch 1)
+    if not (lse.dtype == torch.float32 and lse.is_contiguous() and tuple(lse.shape) == (hq, T)):
+        raise RuntimeError("dtg: flash_attn_bwd: lse must be f32 [Hq, T]")
+    if not (o.is_contiguous() and dout.shape == o.shape and o.shape[0] == T):
+        raise RuntimeError("dtg: flash_attn_bwd: o/dout")
     hkv = k.shape[1]
     rep = hq // hkv
     dq = torch.zeros(T, hq, d, dtype=torch.float32)

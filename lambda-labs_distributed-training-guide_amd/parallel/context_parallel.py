@@ -194,7 +194,7 @@ class _CPAttention(torch.autograd.Function):
             cu, ks, kl, maxq, maxk = ranges[s]
             flat = lambda t: t[:, s].reshape(B * c, *t.shape[3:])
             dqs, dks, dvs = torch.ops.dtg.flash_attn_varlen_bwd(
-                flat(do5), flat(q5), kf, vf, flat(o5), lse4[:, :, s].reshape(Hq, B * c), cu, ks, kl, maxq, maxk,
+                flat(do5), flat(q5), kf, vf, flat(o5), lse4[:, :, s].reshape(Hq, B * c).contiguous(), cu, ks, kl, maxq, maxk,
                 scale, True)
             dq[:, s] = dqs.view(B, c, Hq, D)
             dk = dks.float() if dk is None else dk + dks.float()

@@ -369,11 +369,16 @@ def run(chapter: str, argv=None):
                 loss_sum = out.loss.detach() if loss_sum is None else loss_sum + out.loss.detach()
             if model._dtg_pp is not None:
                 micro = micro_pp
+            check = getattr(args, "check_finite", "off") == "on"
+            if check:
+                _report_nonfinite(model, engine, loss_sum, state["global_step"] + 1, rank, "grad")
             if micro:
                 wait_for_peers()
                 with timers["update"]:
                     opt.step()
                     lr_scheduler.step()
+                if check:
+                    _report_nonfinite(model, engine, None, state["global_step"] + 1, rank, "param")
             if seq_shard is not None:  # each sequence rank holds its share of the row losses
                 loss_sum = loss_sum.clone()
                 torch.distributed.all_reduce(loss_sum, group=model._dtg_seq[1])
@@ -429,6 +434,28 @@ def run(chapter: str, argv=None):
         state["running_loss"] += float(run_loss.item())
     mgr.finalize()
     return state
+
+
+def _report_nonfinite(model, engine, loss, step, rank, what):
+    """--check-finite: name the parameters whose gradient (what="grad", after backward) or value
+    (what="param", after the update) holds NaN/inf.  A ZeRO engine owns only its reduced gradient
+    shard (the rest of the flat gradient buffer is scratch), so that shard is what is checked."""
+    bad = []
+    shard = getattr(engine, "grad_shard", None) if what == "grad" and getattr(engine, "mode", "") == "zero" else None
+    if shard is not None:
+        if not bool(torch.isfinite(shard).all()):
+            bad.append(f"<ZeRO gradient shard: {int((~torch.isfinite(shard)).sum())} of {shard.numel()} elements>")
+    else:
+        for n, p in model.named_parameters():
+            g = (p.grad if getattr(p, "main_grad", None) is None else p.main_grad) if what == "grad" else p.detach()
+            if g is None or g.numel() == 0 or g.untyped_storage().size() == 0:  # e.g. a freed FSDP view
+                continue
+            if not bool(torch.isfinite(g).all()):
+                bad.append(n)
+    lf = loss is None or bool(torch.isfinite(loss).all())
+    if bad or not lf:
+        LOGGER.warning(f"[check-finite] step {step} rank {rank}: loss finite={lf}; non-finite {what} in "
+                       f"{len(bad)} tensors: {bad[:12]}")
 
 
 def _seq_sharder(seq):

@@ -47,11 +47,14 @@ def init_distributed(backend: Optional[str] = None, timeout_minutes: int = 30, l
     os.environ.setdefault("LOCAL_RANK", str(local_rank))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
-    device = torch.device(f"cuda:{local_rank}") if cuda else torch.device("cpu")
+    # DTG_SHARED_DEVICE=1: every rank on cuda:0 with gloo collectives -- rehearse a multi-rank
+    # layout (real kernels and per-rank shapes, host-staged communication) on a one-GPU machine
+    shared = cuda and os.environ.get("DTG_SHARED_DEVICE") == "1"
+    device = torch.device("cuda:0" if shared else f"cuda:{local_rank}") if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(device)
     if world > 1 and not dist.is_initialized():
-        backend = backend or ("nccl" if cuda else "gloo")
+        backend = backend or ("nccl" if cuda and not shared else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(minutes=timeout_minutes))
         if backend == "nccl":
             kw["device_id"] = device

@@ -6,10 +6,10 @@ import torch
 from _dist import run_distributed
 
 pytestmark = pytest.mark.gpu
-B, S, HQ, HKV, D = 2, 1024, 8, 2, 128
+S, HQ, HKV, D = 1024, 8, 2, 128
 
 
-def _full():
+def _full(B):
     g = torch.Generator().manual_seed(0)
     return [torch.randn(B, S, h, D, generator=g).bfloat16() for h in (HQ, HKV, HKV, HQ)]
 
@@ -17,13 +17,13 @@ def _full():
 DOCS = [[0, 100, 333, 700], [0, 517]]  # packed rows: document starts per row
 
 
-def _worker(rank, world, docs=None):
+def _worker(rank, world, B, docs=None):
     import dtg.ops  # noqa: F401
     from dtg.parallel.context_parallel import cp_attention, cp_ranges, shard_zigzag
 
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
-    loc = [shard_zigzag(t, rank, world).to(dev) for t in _full()]
+    loc = [shard_zigzag(t, rank, world).to(dev) for t in _full(B)]
     ql, kl, vl = (t.reshape(-1, *t.shape[2:]).clone().requires_grad_() for t in loc[:3])
     ranges = cp_ranges(rank, world, B, S // (2 * world), dev, docs) if docs else None
     o = cp_attention(ql, kl, vl, None, B, ranges=ranges)
@@ -32,14 +32,16 @@ def _worker(rank, world, docs=None):
     return [t.view(B, -1, *t.shape[1:]).detach().float().cpu() for t in (o, ql.grad, kl.grad, vl.grad)]
 
 
+@pytest.mark.parametrize("B", [1, 2])
 @pytest.mark.parametrize("packed", [False, True])
-def test_cp_attention_gpu_matches_full(cuda, packed):
+def test_cp_attention_gpu_matches_full(cuda, packed, B):
     """Dense rows, and packed rows (documents cut across the zig-zag chunks) against the
-    varlen flash attention over the full rows' documents."""
+    varlen flash attention over the full rows' documents.  B = 1 is the rime chapter's shape
+    (one packed row: per-slot views of the LSE are not contiguous without a copy)."""
     import dtg.ops  # noqa: F401
     from dtg.parallel.context_parallel import unshard_zigzag
 
-    q, k, v, do = (t.to(cuda) for t in _full())
+    q, k, v, do = (t.to(cuda) for t in _full(B))
     qs, ks, vs = (t.reshape(B * S, *t.shape[2:]) for t in (q, k, v))
     if packed:
         bounds = [b * S + d for b in range(B) for d in DOCS[b]] + [B * S]
@@ -51,7 +53,7 @@ def test_cp_attention_gpu_matches_full(cuda, packed):
     o, lse = torch.ops.dtg.flash_attn_fwd(qs, ks, vs, cu, mx, D ** -0.5, True)
     grads = torch.ops.dtg.flash_attn_bwd(do.reshape(B * S, HQ, D), qs, ks, vs, o, lse, cu, mx, D ** -0.5, True)
     ref = [t.view(B, S, *t.shape[1:]).float().cpu() for t in (o,) + tuple(grads)]
-    res = run_distributed(_worker, 2, DOCS if packed else None)
+    res = run_distributed(_worker, 2, B, DOCS[:B] if packed else None)
     for i, name in enumerate(("out", "dq", "dk", "dv")):
         got = unshard_zigzag([r[i] for r in res], 2)
         rel = ((got - ref[i]).norm() / ref[i].norm()).item()
