@@ -78,7 +78,10 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
   for (int i = 0; i < PER; ++i) {
     const int c = threadIdx.x + i * kNormThreads;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
+    for (int j = 0; j < 8; ++j) dwacc[i][j] = wv[i][j] = 0.f;
+    // Lanes past the row (H not a multiple of 8 * 256, e.g. 3072 for Llama-3.2-3B) keep w = 0:
+    // their g = dy * w enters the row's dot product, and an uninitialised register there held
+    // NaN/inf often enough to turn whole rows of dx into NaN (rime chapter, profiles/r2_s47).
     if (c < nch) load8(w + c * 8, wv[i]);
   }
   const int r0 = blockIdx.x * rows_per_block;

@@ -82,9 +82,12 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
         g.add_argument("--pp-microbatches", default=4, type=int,
                        help="1F1B micro-batches per step (must divide --batch-size)")
     g.add_argument("--grad-accum", default=1, type=int, help="micro-batches per optimizer step (no_sync)")
-    g.add_argument("--check-finite", default="off", choices=["on", "off"],
-                   help="debugging: after every backward, log the parameters whose gradient holds NaN/inf "
-                        "(and the loss), one device sync per step")
+    g.add_argument("--detect-anomaly", default="off", choices=["on", "off"],
+                   help="debugging: torch.autograd anomaly mode (raises at the first backward op whose output "
+                        "is NaN, with the forward stack that created it); slow")
+    g.add_argument("--check-finite", default="off", choices=["on", "off", "grad", "param"],
+                   help="debugging: log the tensors holding NaN/inf -- gradients after every backward (grad), "
+                        "parameters after every update (param) or both (on); each check syncs the device")
     g.add_argument("--bucket-mb", default=256, type=int, help="gradient bucket size for DDP/ZeRO")
     if chapter == "02":
         g.add_argument("--dp-mode", default="zero", choices=["ddp", "zero"],

@@ -229,6 +229,8 @@ def run(chapter: str, argv=None):
     if chapter == "deepspeed":
         args = _deepspeed_overrides(args)
     rank, local_rank, world, device = udist.init_distributed(local_rank_arg=getattr(args, "local_rank", None))
+    if getattr(args, "detect_anomaly", "off") == "on":
+        torch.autograd.set_detect_anomaly(True, check_nan=True)
     udist.setup_logging(rank, with_rank=chapter not in ("01", "rime"))
     LOGGER.info(os.environ)
     LOGGER.info(args)
@@ -369,15 +371,15 @@ def run(chapter: str, argv=None):
                 loss_sum = out.loss.detach() if loss_sum is None else loss_sum + out.loss.detach()
             if model._dtg_pp is not None:
                 micro = micro_pp
-            check = getattr(args, "check_finite", "off") == "on"
-            if check:
+            check = getattr(args, "check_finite", "off")
+            if check in ("on", "grad"):
                 _report_nonfinite(model, engine, loss_sum, state["global_step"] + 1, rank, "grad")
             if micro:
                 wait_for_peers()
                 with timers["update"]:
                     opt.step()
                     lr_scheduler.step()
-                if check:
+                if check in ("on", "param"):
                     _report_nonfinite(model, engine, None, state["global_step"] + 1, rank, "param")
             if seq_shard is not None:  # each sequence rank holds its share of the row losses
                 loss_sum = loss_sum.clone()

@@ -33,7 +33,7 @@ def test_native_loaded(cuda):
     assert _native.LOADED, "gfx950 extension must be loaded on a GPU box"
 
 
-@pytest.mark.parametrize("T,H", [(257, 4096), (64, 3072), (33, 128), (8, 16384)])
+@pytest.mark.parametrize("T,H", [(257, 4096), (64, 3072), (4096, 3072), (1024, 896), (33, 128), (8, 16384)])
 def test_rmsnorm(cuda, T, H):
     torch.manual_seed(0)
     x = torch.randn(T, H).bfloat16()

@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """Embedding-backward (dtg::embedding_bwd_) timing at the 8B shapes: TP 1, TP 8 (7/8 of the ids
 out of shard, -1), and one token covering 3/4 of the batch (profiles/r2_s39/emb_bench.jsonl)."""
-import torch, time, json, sys, os
+import json
+import os
+import sys
+import time
+
+import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import dtg, dtg.ops
 d = torch.ops.dtg
