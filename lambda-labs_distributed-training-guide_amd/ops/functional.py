@@ -400,17 +400,31 @@ class _FusedLinearCE(torch.autograd.Function):
         # direct: dW goes straight into w.main_grad now (engine-owned loss, grad_output == 1)
         direct = want_dw and _gr.direct_loss_grad() and getattr(w, "main_grad", None) is not None
         dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if (want_dw and not direct) else None
-        tn = need and _ce_tn(h, w) and chunk % 8 == 0
-        w_t = ops.transpose2d(w) if (tn and ctx.needs_input_grad[0]) else None
+        # A vocabulary that is not a multiple of 8 (GPT-2 50,257, the rime 156,939) leaves every
+        # logits row, and the transposed weight, 16-B misaligned: hipBLASLt then drops to slower
+        # kernels and the TN layout cannot be used at all.  Pad the weight with zero rows to the
+        # next multiple of 8: the padded logits columns are exactly 0, the CE kernel sees only the
+        # first V columns (strided view) and leaves the pad at 0, so the GEMMs over the padded K
+        # add nothing.  One 1-GB copy per step for the rime head.
+        V = w.shape[0]
+        pad = (-V) % 8 if (need and h.is_cuda and _LINEAR_BWD != "native" and chunk % 8 == 0
+                           and _tn_ok(h)) else 0
+        wp = w
+        if pad:
+            wp = torch.zeros((V + pad, w.shape[1]), dtype=w.dtype, device=w.device)
+            wp[:V].copy_(w.detach())
+        tn = need and _ce_tn(h, wp) and chunk % 8 == 0
+        w_t = ops.transpose2d(wp) if (tn and ctx.needs_input_grad[0]) else None
         for s in range(0, T, chunk):
             e = min(T, s + chunk)
-            logits = torch.mm(h[s:e], w.t())
+            lp = torch.mm(h[s:e], wp.t())
+            logits = lp[:, :V] if pad else lp
             rows = ops.ce_fwd_bwd_(logits, labels[s:e], ignore_index, scale, need)
             loss_sum += rows.sum()
             if need:
-                _ce_dx(logits, w, w_t, dh[s:e])
+                _ce_dx(lp, wp, w_t, dh[s:e])
                 if direct and tn:
-                    _gr.accumulate_mm_into_main_grad(w, logits, h[s:e], a_t=ops.transpose2d(logits),
+                    _gr.accumulate_mm_into_main_grad(w, logits, h[s:e], a_t=ops.transpose2d(lp)[:V],
                                                      b_t=ops.transpose2d(h[s:e]))
                 elif direct:
                     _gr.accumulate_mm_into_main_grad(w, logits, h[s:e])

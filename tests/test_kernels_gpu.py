@@ -421,3 +421,34 @@ def test_flash_attn_varlen_key_ranges(cuda, D, hq, hkv, causal):
     for a, b, n in zip(got, ref, ("dq", "dk", "dv")):
         assert _rel(a, b) < 2e-2, f"{n} rel err {_rel(a, b)}"
     assert float(got[1][:ks[0]].float().abs().max()) == 0.0  # untouched keys: zero gradient
+
+
+@pytest.mark.parametrize("V", [1003, 50257, 1024])
+@pytest.mark.parametrize("direct", [False, True])
+def test_fused_linear_ce_odd_vocab(cuda, V, direct, monkeypatch):
+    """Loss head with a vocabulary that is not a multiple of 8 (GPT-2, rime): the zero-padded
+    weight / logits path gives the f32 loss, dH and dW (direct: dW written into main_grad in the
+    forward, the engine-owned-loss path)."""
+    from dtg.ops import functional as F_
+    from dtg.ops import grad_routing as gr
+
+    monkeypatch.setattr(F_, "_LINEAR_BWD", "tn")
+    torch.manual_seed(0)
+    T, H = 2048, 256
+    h = torch.randn(T, H).bfloat16()
+    w = (0.05 * torch.randn(V, H)).bfloat16()
+    lab = torch.randint(0, V, (T,))
+    lab[::7] = -100
+    hg = h.to(cuda).requires_grad_()
+    wg = w.to(cuda).requires_grad_()
+    if direct:
+        wg.main_grad = torch.zeros(V, H, dtype=torch.bfloat16, device=cuda)
+        monkeypatch.setattr(gr, "_DIRECT_LOSS_GRAD", True)
+    loss = F_.fused_linear_cross_entropy(hg, wg, lab.to(cuda), chunk=1024)
+    loss.backward()
+    hr, wr = h.float().requires_grad_(), w.float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(hr @ wr.t(), lab, ignore_index=-100)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 2e-3 * abs(ref.item())
+    assert _rel(hg.grad, hr.grad) < 2e-2
+    assert _rel(wg.main_grad if direct else wg.grad, wr.grad) < 2e-2

@@ -58,7 +58,9 @@ def _worker(shapes_file, results_file, max_tuning_ms):
     # without this TunableOp ranks on time alone, and one hipBLASLt solution for GPT-2's batched
     # attention-score GEMM (tn_1024_1024_64_B_96) returned values of order 1e33 -- NaN losses
     # (found by tools/check_tunableop.py, profiles/r2_s35/).
-    os.environ.setdefault("PYTORCH_TUNABLEOP_NUMERICAL_CHECK", "1")
+    # format "atol_rtol" (PyTorch 2.10): bf16 outputs of two correct kernels differ by rounding
+    # (a few ulps of values ~sqrt(K)); a broken one is off by orders of magnitude
+    os.environ.setdefault("PYTORCH_TUNABLEOP_NUMERICAL_CHECK", "1e-1_5e-2")
     import torch
 
     t = torch.cuda.tunable
