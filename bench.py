@@ -252,7 +252,7 @@ def collective_sweep(args, torch, dist, device, world, cuda):
         ops = {"reduce_scatter": (lambda: dist.reduce_scatter_tensor(shard, x), (world - 1) / world),
                "all_gather": (lambda: dist.all_gather_into_tensor(full, shard), (world - 1) / world),
                "all_reduce": (lambda: dist.all_reduce(x), 2 * (world - 1) / world)}
-        if not cuda:  # gloo (CPU rehearsal) has no reduce-scatter
+        if dist.get_backend() == "gloo":  # gloo (CPU / shared-GPU rehearsals) has no reduce-scatter
             ops.pop("reduce_scatter")
         for op, (fn, factor) in ops.items():
             iters = 5 if mib >= 256 else 10
