@@ -485,6 +485,13 @@ class CheckpointManager:
         else:
             meta = load_sharded(d / "checkpoint", self.engine)
         self.lr_scheduler.load_state_dict(torch.load(d / "lr_scheduler.pt", weights_only=True))
+        # The sharded / per-rank layouts restore the AdamW moments but not the optimizer's
+        # param_groups, and chainable schedulers (CosineAnnealingLR) compute the next lr FROM the
+        # group's current lr: without this the resumed run restarted the recursion from the
+        # initial lr (a TP=2 -> TP=1 resume on the GPU logged step 4 at step 3's lr, and the whole
+        # tail of the schedule scaled by lr0 / lr(resume step)).
+        for g, lr in zip(self.optimizer.param_groups, self.lr_scheduler.get_last_lr()):
+            g["lr"] = lr
         if (d / "rng.pt").exists():
             load_rng(d / "rng.pt", self.local_rank)
         with open(d / "state.json") as fp:

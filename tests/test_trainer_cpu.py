@@ -47,6 +47,18 @@ def test_fsdp_chapter_checkpoint_resume(tmp_path):
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "Resuming" in out, out[-3000:]
     assert json.loads((tmp_path / "fs" / "state.json").read_text())["global_step"] == 4
+    # the resumed steps continue the uninterrupted cosine schedule (the optimizer's lr is restored
+    # from the scheduler: chainable schedulers compute the next lr from the group's current one)
+    lrs = {json.loads(l)["global_step"]: json.loads(l)["lr"]
+           for l in (tmp_path / "fs" / "metrics-rank0.jsonl").read_text().splitlines()}
+    ref = tmp_path / "ref"
+    r = _torchrun("04-fully-sharded-data-parallel", [a if a != str(tmp_path) else str(ref) for a in base]
+                  + ["--max-steps", "4", "--ckpt-freq", "100"])
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    ref_lrs = {json.loads(l)["global_step"]: json.loads(l)["lr"]
+               for l in (ref / "fs" / "metrics-rank0.jsonl").read_text().splitlines()}
+    for step in (3, 4):
+        assert lrs[step] == pytest.approx(ref_lrs[step], rel=1e-9), (step, lrs, ref_lrs)
 
 
 @pytest.mark.slow
