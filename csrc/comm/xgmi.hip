@@ -24,6 +24,18 @@
 //     Kernel boundaries give the acquire/release of the data itself (caches are written back
 //     at the end of a kernel and invalidated at the start of the next).
 //   * Epochs increase monotonically per communicator, so signal rows never need resetting.
+//   * A timed-out barrier is sticky: the error word stays set and every later barrier kernel of
+//     the communicator returns at once, so one missing peer costs one timeout, not one per
+//     collective; the trainer polls it (`check()`) and exits non-zero.
+//   * Zero-copy: every collective takes the byte `offset` of its message in the workspace.  When
+//     the input already lives there (a producer GEMM wrote its output straight into
+//     `workspace()`, parallel/async_tp.py), the stage copy is skipped; peers pull from the same
+//     offset of their own workspace.
+//   * Copy-engine variants (`*_dma`): the stage and every peer pull are hipMemcpyAsync transfers
+//     issued on a pool of per-peer streams forked from / joined into the caller's stream with
+//     events, so the world-1 peer copies run concurrently on the copy engines (one xGMI link
+//     each) and take no CU time; the reduce-scatter's sum is one local kernel over the pulled
+//     slices.
 //
 // RCCL stays the path for the large DDP/ZeRO/FSDP buckets and for inter-node traffic.
 // All stores are vector-memory stores / atomics; nothing writes through the scalar cache.
@@ -63,6 +75,8 @@ struct Peers {
 __global__ void barrier_kernel(Peers peers, int me, int world, int row, uint32_t epoch, uint32_t* err,
                                uint64_t timeout_ticks) {
   const int t = threadIdx.x;
+  // a previous collective of this communicator timed out: peers are out of step, never wait again
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
   if (t < world) {
     uint32_t* dst = peers.sig[t] + row * kSigSlots + me;
     __hip_atomic_store(dst, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -161,9 +175,30 @@ struct Comm {
   Peers peers{};
   std::vector<void*> opened;
   uint32_t epoch = 0;
-  double timeout_s = 10.0;
+  double timeout_s = 60.0;
+  // copy-engine path: one stream per peer, fork/join events
+  hipStream_t peer_st[kMaxRanks] = {};
+  hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_join[kMaxRanks] = {};
+
+  void ensure_streams() {
+    if (ev_fork) return;
+    for (int r = 0; r < world; ++r) {
+      XGMI_CHECK(hipStreamCreateWithFlags(&peer_st[r], hipStreamNonBlocking));
+      XGMI_CHECK(hipEventCreateWithFlags(&ev_join[r], hipEventDisableTiming));
+    }
+    XGMI_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+  }
 
   ~Comm() {
+    if (ev_fork) {
+      (void)hipDeviceSynchronize();
+      for (int r = 0; r < world; ++r) {
+        (void)hipStreamDestroy(peer_st[r]);
+        (void)hipEventDestroy(ev_join[r]);
+      }
+      (void)hipEventDestroy(ev_fork);
+    }
     for (void* p : opened) (void)hipIpcCloseMemHandle(p);
     if (base) (void)hipFree(base);
     if (err) (void)hipHostFree(err);
@@ -248,6 +283,13 @@ void destroy(int64_t id) {
   g_comms[id].reset();
 }
 
+at::Tensor workspace(int64_t id) {
+  Comm& c = get(id);
+  // a view of the own data region (no deleter: the communicator owns the memory)
+  return at::from_blob(c.base, {c.capacity},
+                       at::TensorOptions().dtype(at::kByte).device(c10::Device(c10::DeviceType::CUDA, c.device)));
+}
+
 namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -264,13 +306,6 @@ int grid_for(int64_t n16, int cap = 2048) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
 }
 
-void stage(Comm& c, const at::Tensor& inp, hipStream_t st) {
-  const int64_t n16 = inp.numel() * inp.element_size() / 16;
-  copy16_kernel<<<grid_for(n16), 256, 0, st>>>(reinterpret_cast<const u32x4*>(inp.data_ptr()),
-                                               reinterpret_cast<u32x4*>(c.base), n16);
-  C10_HIP_KERNEL_LAUNCH_CHECK();
-}
-
 void check_io(const Comm& c, const at::Tensor& t, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.get_device() == c.device, "xgmi: ", what, " must be on cuda:", c.device);
   TORCH_CHECK(t.is_contiguous(), "xgmi: ", what, " must be contiguous");
@@ -279,90 +314,190 @@ void check_io(const Comm& c, const at::Tensor& t, const char* what) {
               "xgmi: ", what, " must be 16-byte aligned and a multiple of 16 bytes");
 }
 
+void check_msg(const Comm& c, int64_t offset, int64_t bytes) {
+  TORCH_CHECK(offset >= 0 && offset % 16 == 0, "xgmi: workspace offset must be a non-negative multiple of 16");
+  TORCH_CHECK(offset + bytes <= c.capacity, "xgmi: message of ", bytes, " B at offset ", offset,
+              " exceeds the workspace (", c.capacity, " B)");
+}
+
+// The output must not alias the message in the workspace: peers are still pulling from it while
+// this rank writes its result.
+void check_no_alias(const Comm& c, const at::Tensor& out, int64_t offset, int64_t bytes) {
+  const auto lo = reinterpret_cast<uintptr_t>(out.data_ptr());
+  const auto hi = lo + out.numel() * out.element_size();
+  const auto wlo = reinterpret_cast<uintptr_t>(c.base + offset);
+  TORCH_CHECK(hi <= wlo || lo >= wlo + bytes, "xgmi: the output overlaps the message in the workspace");
+}
+
+// The message's home in the own workspace; the stage copy is skipped when the producer already
+// wrote it there (zero-copy).
+uint8_t* stage(Comm& c, const at::Tensor& inp, int64_t offset, bool dma, hipStream_t st) {
+  uint8_t* dst = c.base + offset;
+  if (inp.data_ptr() == dst) return dst;
+  const int64_t bytes = inp.numel() * inp.element_size();
+  if (dma) {
+    XGMI_CHECK(hipMemcpyAsync(dst, inp.data_ptr(), bytes, hipMemcpyDeviceToDevice, st));
+  } else {
+    const int64_t n16 = bytes / 16;
+    copy16_kernel<<<grid_for(n16), 256, 0, st>>>(reinterpret_cast<const u32x4*>(inp.data_ptr()),
+                                                 reinterpret_cast<u32x4*>(dst), n16);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+  return dst;
+}
+
+// Copy-engine fan-out: the peer streams start after everything queued on `st` ...
+void fork(Comm& c, hipStream_t st) {
+  c.ensure_streams();
+  XGMI_CHECK(hipEventRecord(c.ev_fork, st));
+  for (int r = 0; r < c.world; ++r) XGMI_CHECK(hipStreamWaitEvent(c.peer_st[r], c.ev_fork, 0));
+}
+
+// ... and `st` continues once every peer copy has landed.
+void join(Comm& c, hipStream_t st) {
+  for (int r = 0; r < c.world; ++r) {
+    XGMI_CHECK(hipEventRecord(c.ev_join[r], c.peer_st[r]));
+    XGMI_CHECK(hipStreamWaitEvent(st, c.ev_join[r], 0));
+  }
+}
+
 }  // namespace
 
-void all_gather(int64_t id, const at::Tensor& out, const at::Tensor& inp) {
+void all_gather(int64_t id, const at::Tensor& out, const at::Tensor& inp, int64_t offset) {
   Comm& c = get(id);
   check_io(c, inp, "input");
   check_io(c, out, "output");
   TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == inp.numel() * c.world, "xgmi all_gather: shape");
   const int64_t bytes = inp.numel() * inp.element_size();
-  TORCH_CHECK(bytes <= c.capacity, "xgmi: message of ", bytes, " B exceeds the workspace (", c.capacity, " B)");
+  check_msg(c, offset, bytes);
+  check_no_alias(c, out, offset, bytes);
   c10::DeviceGuard g(inp.device());
   hipStream_t st = cur_stream();
   ++c.epoch;
-  stage(c, inp, st);
+  stage(c, inp, offset, false, st);
   barrier(c, 0, st);
+  Peers src = c.peers;
+  for (int r = 0; r < c.world; ++r) src.data[r] += offset;
   const int64_t shard16 = bytes / 16;
-  const int bpp = std::max(1, grid_for(shard16, 1024) / 1);
-  all_gather_kernel<<<bpp * c.world, 256, 0, st>>>(c.peers, c.rank, c.world, reinterpret_cast<u32x4*>(out.data_ptr()),
+  const int bpp = std::max(1, grid_for(shard16, 1024));
+  all_gather_kernel<<<bpp * c.world, 256, 0, st>>>(src, c.rank, c.world, reinterpret_cast<u32x4*>(out.data_ptr()),
                                                    shard16, bpp);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   barrier(c, 1, st);
 }
 
-// Copy-engine all-gather: the same stage -> barrier -> pull -> barrier protocol, but the stage
-// and the pulls are hipMemcpyAsync transfers (SDMA engines between GPUs) instead of kernels, so
-// an all-gather issued on a side stream while GEMMs run (parallel/async_tp.py) takes no CU time;
-// only the two one-wave barrier kernels touch the shader array.
-void all_gather_dma(int64_t id, const at::Tensor& out, const at::Tensor& inp) {
+// Copy-engine all-gather: stage -> barrier -> world concurrent pulls (one per peer stream) ->
+// barrier.  Only the two one-wave barrier kernels touch the shader array, so an all-gather on a
+// side stream overlaps GEMMs without taking CUs from them (parallel/async_tp.py).
+void all_gather_dma(int64_t id, const at::Tensor& out, const at::Tensor& inp, int64_t offset) {
   Comm& c = get(id);
   check_io(c, inp, "input");
   check_io(c, out, "output");
   TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == inp.numel() * c.world, "xgmi all_gather: shape");
   const int64_t bytes = inp.numel() * inp.element_size();
-  TORCH_CHECK(bytes <= c.capacity, "xgmi: message of ", bytes, " B exceeds the workspace (", c.capacity, " B)");
+  check_msg(c, offset, bytes);
+  check_no_alias(c, out, offset, bytes);
   c10::DeviceGuard g(inp.device());
   hipStream_t st = cur_stream();
   ++c.epoch;
-  XGMI_CHECK(hipMemcpyAsync(c.base, inp.data_ptr(), bytes, hipMemcpyDeviceToDevice, st));
+  stage(c, inp, offset, true, st);
   barrier(c, 0, st);
   auto* o = static_cast<uint8_t*>(out.data_ptr());
-  for (int k = 0; k < c.world; ++k) {  // own shard first, then the peers in ring order
+  fork(c, st);
+  for (int k = 0; k < c.world; ++k) {
     const int p = (c.rank + k) % c.world;
-    XGMI_CHECK(hipMemcpyAsync(o + (int64_t)p * bytes, c.peers.data[p], bytes, hipMemcpyDeviceToDevice, st));
+    const uint8_t* src = p == c.rank ? static_cast<const uint8_t*>(inp.data_ptr()) : c.peers.data[p] + offset;
+    XGMI_CHECK(hipMemcpyAsync(o + (int64_t)p * bytes, src, bytes, hipMemcpyDeviceToDevice, c.peer_st[p]));
   }
+  join(c, st);
   barrier(c, 1, st);
 }
 
-void reduce_scatter(int64_t id, const at::Tensor& out, const at::Tensor& inp) {
+void reduce_scatter(int64_t id, const at::Tensor& out, const at::Tensor& inp, int64_t offset) {
   Comm& c = get(id);
   check_io(c, inp, "input");
   check_io(c, out, "output");
   TORCH_CHECK(out.scalar_type() == inp.scalar_type() && inp.numel() == out.numel() * c.world, "xgmi reduce_scatter: shape");
   const int64_t bytes = inp.numel() * inp.element_size();
-  TORCH_CHECK(bytes <= c.capacity, "xgmi: message of ", bytes, " B exceeds the workspace (", c.capacity, " B)");
+  check_msg(c, offset, bytes);
+  check_no_alias(c, out, offset, bytes);
   c10::DeviceGuard g(inp.device());
   hipStream_t st = cur_stream();
   ++c.epoch;
-  stage(c, inp, st);
+  stage(c, inp, offset, false, st);
   barrier(c, 0, st);
   const int64_t n16 = out.numel() * out.element_size() / 16;
   auto* o = reinterpret_cast<u32x4*>(out.data_ptr());
+  Peers src = c.peers;
+  for (int r = 0; r < c.world; ++r) src.data[r] += offset;
   if (inp.scalar_type() == at::kBFloat16)
-    reduce_kernel<true><<<grid_for(n16), 256, 0, st>>>(c.peers, c.rank, c.world, o, (int64_t)c.rank * n16, n16);
+    reduce_kernel<true><<<grid_for(n16), 256, 0, st>>>(src, c.rank, c.world, o, (int64_t)c.rank * n16, n16);
   else
-    reduce_kernel<false><<<grid_for(n16), 256, 0, st>>>(c.peers, c.rank, c.world, o, (int64_t)c.rank * n16, n16);
+    reduce_kernel<false><<<grid_for(n16), 256, 0, st>>>(src, c.rank, c.world, o, (int64_t)c.rank * n16, n16);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   barrier(c, 1, st);
 }
 
-void all_reduce(int64_t id, const at::Tensor& inout) {
+// Copy-engine reduce-scatter: the world slices [me*shard, (me+1)*shard) of every peer's message
+// are pulled concurrently into a local [world, shard] scratch (one copy per peer stream), the
+// peers are released, and one local kernel sums the slices at HBM speed (f32 accumulation).
+void reduce_scatter_dma(int64_t id, const at::Tensor& out, const at::Tensor& inp, int64_t offset) {
+  Comm& c = get(id);
+  check_io(c, inp, "input");
+  check_io(c, out, "output");
+  TORCH_CHECK(out.scalar_type() == inp.scalar_type() && inp.numel() == out.numel() * c.world, "xgmi reduce_scatter: shape");
+  const int64_t bytes = inp.numel() * inp.element_size();
+  const int64_t shard = bytes / c.world;
+  check_msg(c, offset, bytes);
+  check_no_alias(c, out, offset, bytes);
+  c10::DeviceGuard g(inp.device());
+  hipStream_t st = cur_stream();
+  // allocated on `st`; every peer-stream access is joined back into `st` before it is freed
+  at::Tensor scratch = at::empty({bytes}, inp.options().dtype(at::kByte));
+  auto* sc = static_cast<uint8_t*>(scratch.data_ptr());
+  ++c.epoch;
+  stage(c, inp, offset, true, st);
+  barrier(c, 0, st);
+  fork(c, st);
+  for (int k = 0; k < c.world; ++k) {
+    const int p = (c.rank + k) % c.world;
+    const uint8_t* src = (p == c.rank ? static_cast<const uint8_t*>(inp.data_ptr()) : c.peers.data[p] + offset) +
+                         (int64_t)c.rank * shard;
+    XGMI_CHECK(hipMemcpyAsync(sc + (int64_t)p * shard, src, shard, hipMemcpyDeviceToDevice, c.peer_st[p]));
+  }
+  join(c, st);
+  barrier(c, 1, st);  // peers may restage: the slices are local now
+  Peers loc{};
+  for (int r = 0; r < c.world; ++r) loc.data[r] = sc + (int64_t)r * shard;
+  const int64_t n16 = shard / 16;
+  auto* o = reinterpret_cast<u32x4*>(out.data_ptr());
+  if (inp.scalar_type() == at::kBFloat16)
+    reduce_kernel<true><<<grid_for(n16), 256, 0, st>>>(loc, c.rank, c.world, o, 0, n16);
+  else
+    reduce_kernel<false><<<grid_for(n16), 256, 0, st>>>(loc, c.rank, c.world, o, 0, n16);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+void all_reduce(int64_t id, const at::Tensor& inout, int64_t offset) {
   Comm& c = get(id);
   check_io(c, inout, "tensor");
   const int64_t bytes = inout.numel() * inout.element_size();
-  TORCH_CHECK(bytes <= c.capacity, "xgmi: message of ", bytes, " B exceeds the workspace (", c.capacity, " B)");
+  check_msg(c, offset, bytes);
+  // in place: the result overwrites `inout`, so it must live outside the workspace message
+  check_no_alias(c, inout, offset, bytes);
   c10::DeviceGuard g(inout.device());
   hipStream_t st = cur_stream();
   ++c.epoch;
-  stage(c, inout, st);
+  stage(c, inout, offset, false, st);
   barrier(c, 0, st);
   const int64_t n16 = bytes / 16;
   auto* o = reinterpret_cast<u32x4*>(inout.data_ptr());
+  Peers src = c.peers;
+  for (int r = 0; r < c.world; ++r) src.data[r] += offset;
   if (inout.scalar_type() == at::kBFloat16)
-    reduce_kernel<true><<<grid_for(n16), 256, 0, st>>>(c.peers, c.rank, c.world, o, 0, n16);
+    reduce_kernel<true><<<grid_for(n16), 256, 0, st>>>(src, c.rank, c.world, o, 0, n16);
   else
-    reduce_kernel<false><<<grid_for(n16), 256, 0, st>>>(c.peers, c.rank, c.world, o, 0, n16);
+    reduce_kernel<false><<<grid_for(n16), 256, 0, st>>>(src, c.rank, c.world, o, 0, n16);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   barrier(c, 1, st);
 }
@@ -374,10 +509,12 @@ TORCH_LIBRARY(dtg_xgmi, m) {
   m.def("set_timeout(int id, float seconds) -> ()", &set_timeout);
   m.def("error(int id) -> int", &error);
   m.def("destroy(int id) -> ()", &destroy);
-  m.def("all_gather(int id, Tensor(a!) out, Tensor inp) -> ()", &all_gather);
-  m.def("all_gather_dma(int id, Tensor(a!) out, Tensor inp) -> ()", &all_gather_dma);
-  m.def("reduce_scatter(int id, Tensor(a!) out, Tensor inp) -> ()", &reduce_scatter);
-  m.def("all_reduce(int id, Tensor(a!) inout) -> ()", &all_reduce);
+  m.def("workspace(int id) -> Tensor", &workspace);
+  m.def("all_gather(int id, Tensor(a!) out, Tensor inp, int offset=0) -> ()", &all_gather);
+  m.def("all_gather_dma(int id, Tensor(a!) out, Tensor inp, int offset=0) -> ()", &all_gather_dma);
+  m.def("reduce_scatter(int id, Tensor(a!) out, Tensor inp, int offset=0) -> ()", &reduce_scatter);
+  m.def("reduce_scatter_dma(int id, Tensor(a!) out, Tensor inp, int offset=0) -> ()", &reduce_scatter_dma);
+  m.def("all_reduce(int id, Tensor(a!) inout, int offset=0) -> ()", &all_reduce);
 }
 
 }  // namespace xgmi

@@ -86,7 +86,7 @@ class LlamaAttention(nn.Module):
         self.o_proj = Weight(h, self.nq * self.d, device=device, dtype=dtype)
         self.window = int(cfg.sliding_window or 0)
 
-    def forward(self, x, rc: RunCtx):
+    def forward(self, x, rc: RunCtx, out=None):
         b = getattr(self.qkv_proj, "bias", None)
         qkv = ops.linear(x, self.qkv_proj.weight, None if b is None else b.view(-1))
         if rc.cp_group is not None:  # context parallel: zig-zag sequence shards
@@ -106,7 +106,7 @@ class LlamaAttention(nn.Module):
         else:
             o = ops.attention(qkv, self.nq, self.nkv, self.d, rc.cu_seqlens, rc.max_seqlen, rc.cos, rc.sin, rc.pos,
                               window=self.window)
-        return ops.linear(o, self.o_proj.weight)
+        return ops.linear(o, self.o_proj.weight, out=out)
 
 
 class LlamaMLP(nn.Module):
@@ -117,8 +117,8 @@ class LlamaMLP(nn.Module):
         self.gate_up_proj = Weight(2 * self.inter, cfg.hidden_size, device=device, dtype=dtype)
         self.down_proj = Weight(cfg.hidden_size, self.inter, device=device, dtype=dtype)
 
-    def forward(self, x):
-        return ops.swiglu_mlp(x, self.gate_up_proj.weight, self.down_proj.weight)
+    def forward(self, x, out=None):
+        return ops.swiglu_mlp(x, self.gate_up_proj.weight, self.down_proj.weight, out=out)
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -143,7 +143,7 @@ class LlamaDecoderLayer(nn.Module):
             n, res = ops.add_rms_norm(x, res, self.input_layernorm.weight, self.eps)
         ka, km = self._overlap_chunks(n.shape[0], rc) if g is not None else (1, 1)
         if ka > 1:
-            a = async_tp.sp_region(n, lambda xg, j: self.self_attn(xg, _chunk_ctx(rc, xg.shape[0])), g, ka,
+            a = async_tp.sp_region(n, lambda xg, j, out=None: self.self_attn(xg, _chunk_ctx(rc, xg.shape[0]), out=out), g, ka,
                                    tuple(p for p in self.self_attn.parameters()))
         else:
             if g is not None:
@@ -153,7 +153,7 @@ class LlamaDecoderLayer(nn.Module):
                 a = tp_comm.scatter_seq(a, g)
         n2, res = ops.add_rms_norm(a, res, self.post_attention_layernorm.weight, self.eps)
         if km > 1:
-            m = async_tp.sp_region(n2, lambda xg, j: self.mlp(xg), g, km,
+            m = async_tp.sp_region(n2, lambda xg, j, out=None: self.mlp(xg, out=out), g, km,
                                    (self.mlp.gate_up_proj.weight, self.mlp.down_proj.weight))
         else:
             if g is not None:

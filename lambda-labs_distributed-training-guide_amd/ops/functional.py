@@ -50,8 +50,10 @@ def _bwd_layout(x, w):
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, out=None):
         ctx.save_for_backward(x, w)
+        if out is not None:  # (buffer,): hidden from autograd, e.g. an xGMI workspace slot
+            return torch.mm(x, w.t(), out=out[0])
         return torch.mm(x, w.t())
 
     @staticmethod
@@ -66,13 +68,15 @@ class _Linear(torch.autograd.Function):
                 dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
             else:
                 dw = route_weight_grad_mm(w, dy, x)
-        return dx, dw
+        return dx, dw, None
 
 
-def linear(x, w, b=None):
-    """y = x @ w^T (+ b); x is [T, in]."""
+def linear(x, w, b=None, out=None):
+    """y = x @ w^T (+ b); x is [T, in].  `out`: preallocated [T, out_features] result buffer
+    (no bias) -- the zero-copy reduce-scatter input of a tensor-parallel region."""
     if b is None:
-        return _Linear.apply(x, w)
+        return _Linear.apply(x, w, None if out is None else (out,))
+    assert out is None, "linear: out= is for the bias-free projections"
     return _LinearBias.apply(x, w, b)
 
 
@@ -306,10 +310,12 @@ class _SwiGLUMLP(torch.autograd.Function):
     transpose pass; dX GEMMs use transposed weight copies (see _bwd_layout)."""
 
     @staticmethod
-    def forward(ctx, x, w_gu, w_down):
+    def forward(ctx, x, w_gu, w_down, out=None):
         gu = torch.mm(x, w_gu.t())
         h = ops.swiglu_fwd(gu)
         ctx.save_for_backward(x, w_gu, w_down, gu)
+        if out is not None:
+            return torch.mm(h, w_down.t(), out=out[0])
         return torch.mm(h, w_down.t())
 
     @staticmethod
@@ -335,12 +341,13 @@ class _SwiGLUMLP(torch.autograd.Function):
             dw_gu = route_weight_grad_mm(w_gu, dgu, x, a_t=dgu_t, b_t=ops.transpose2d(x))
         else:
             dw_gu = route_weight_grad_mm(w_gu, dgu, x)
-        return dx, dw_gu, dw_down
+        return dx, dw_gu, dw_down, None
 
 
-def swiglu_mlp(x, w_gu, w_down):
-    """Llama MLP: down_proj(silu(gate(x)) * up(x)) with the fused [gate; up] weight."""
-    return _SwiGLUMLP.apply(x, w_gu, w_down)
+def swiglu_mlp(x, w_gu, w_down, out=None):
+    """Llama MLP: down_proj(silu(gate(x)) * up(x)) with the fused [gate; up] weight.  `out`: see
+    `linear`."""
+    return _SwiGLUMLP.apply(x, w_gu, w_down, None if out is None else (out,))
 
 
 # --------------------------------------------------------------------------------------------

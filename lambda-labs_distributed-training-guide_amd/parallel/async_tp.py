@@ -21,6 +21,11 @@ side stream for the direct-peer xGMI library (utils/comm.py), and waited for onl
 before the GEMM that consumes them.  Only the first gather and the last scatter of a region
 stay exposed (2/k of the traffic instead of all of it).
 
+With the direct-peer xGMI library registered for the group, the forward's row-parallel GEMM of
+chunk j writes its partial output straight into one of two workspace slots
+(`XgmiCommunicator.rs_input_buffer`), so the reduce-scatter pulls from it without a stage copy.
+fn(x, j, out=None) must honour `out` for that (LlamaAttention / LlamaMLP do).
+
 Each chunk's f is recorded as its own small autograd graph inside the region's forward;
 the region's backward replays them chunk by chunk between the collectives.  Weight gradients
 from the k chunks accumulate in `main_grad` (first chunk writes, later chunks add), and the
@@ -64,9 +69,11 @@ class _Region(torch.autograd.Function):
             if j + 1 < k:  # prefetch the next chunk while this one computes
                 g = torch.empty((n * Tc, H), dtype=x.dtype, device=x.device)
                 work = comm.all_gather_dim0_into_async(g, xs[j + 1], group)
+            # zero-copy: the chunk's row-parallel GEMM writes straight into an xGMI workspace slot
+            buf = comm.rs_input_buffer(group, (n * Tc, H), x.dtype, stage_bytes=Tc * H * x.element_size())
             with torch.enable_grad():
                 leaf = cur.detach().requires_grad_(True)
-                y = fn(leaf, j)
+                y = fn(leaf, j) if buf is None else fn(leaf, j, out=buf)
             rs.append(comm.reduce_scatter_dim0_into_async(out[j], y.detach(), group))
             leaves.append(leaf)
             ys.append(y)
@@ -107,7 +114,8 @@ class _Region(torch.autograd.Function):
 def sp_region(x, fn, group, k, params):
     """reduce_scatter(fn(all_gather(x))) with k-chunk compute/communication overlap.
 
-    fn(x_chunk_gathered, j) -> partial output of the same row count; `params` are the weights
+    fn(x_chunk_gathered, j[, out=buffer]) -> partial output of the same row count (written into
+    `out` when one is passed); `params` are the weights
     fn uses (passed so the region is part of the autograd graph even when x needs no grad)."""
     return _Region.apply(x, fn, group, int(k), *params)
 

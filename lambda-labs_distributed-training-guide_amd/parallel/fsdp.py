@@ -137,8 +137,10 @@ class FullyShard:
         self.module = model
         self.group = group
         # HYBRID_SHARD (ZeRO++-style): shard inside `group` (one node's xGMI island), replicate
-        # across `replicate_group` (same local rank on every node); gradient shards are summed
-        # over the replicas once per optimizer step.
+        # across `replicate_group` (same local rank on every node); each unit's gradient shard is
+        # summed over the replicas right after its reduce-scatter, inside the backward (the
+        # all-reduce is stream-ordered behind the reduce-scatter and overlaps later units'
+        # backward compute), so step() has no exposed collective.
         self.replicate_group = replicate_group
         self.replicas = comm.world(replicate_group) if (replicate_group is not None and dist.is_initialized()) else 1
         self.tp_group = tp_group  # 2-D: sequence-parallel (replicated) grads are summed over TP first
@@ -434,6 +436,12 @@ class FullyShard:
     def _complete_rs(self, u, work, out, first, direct):
         if work is not None:
             work.wait()
+        if self.replicas > 1:
+            # HYBRID: this micro-batch's shard summed over the replicas (linear, so summing per
+            # micro-batch equals summing the accumulated shard).  RCCL: wait() only orders the
+            # current stream behind the all-reduce; the host keeps queueing backward kernels.
+            ar = dist.all_reduce(out, group=self.replicate_group, async_op=True)
+            ar.wait()
         ev = None
         if not direct:
             gs = self._shard_view(u, self.shard_grads)
@@ -535,8 +543,7 @@ class FullyShard:
                                "update (overlap_cpu_step); call step()/zero_grad() first, or mark earlier "
                                "micro-batches with no_sync() / last_microbatch=False")
         final = (not self._in_no_sync) if last_microbatch is None else bool(last_microbatch)
-        overlap = (self.cpu_offload and self.overlap_cpu_step and self._hparams is not None
-                   and self.replicas == 1 and final)
+        overlap = (self.cpu_offload and self.overlap_cpu_step and self._hparams is not None and final)
         if overlap:  # the last micro-batch: its per-unit gradient shards are final on arrival
             scale = 1.0 / (self.world * self.replicas * (self.accum_count + 1))
             self._bwd_step = (self.step_count + 1, scale, self._hparams())
@@ -595,14 +602,7 @@ class FullyShard:
         self._sync_d2h()
         if grad_scale is None:
             grad_scale = 1.0 / (self.world * self.replicas * max(1, self.accum_count))
-        if self.replicas > 1:
-            g = self.shard_grads
-            if g.device.type == "cpu" and comm.backend_of(self.replicate_group) != "gloo":
-                gd = g.to(self.device)
-                dist.all_reduce(gd, group=self.replicate_group)
-                g.copy_(gd)
-            else:
-                dist.all_reduce(g, group=self.replicate_group)
+        # (HYBRID: the gradient shards were already summed over the replicas during backward)
         if self.cpu_offload:
             from ..ops.adamw import adamw_step_cpu
 

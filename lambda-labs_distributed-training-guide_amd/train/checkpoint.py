@@ -41,6 +41,60 @@ def has_checkpoint(exp_dir) -> bool:
     return (Path(exp_dir) / "state.json").exists()
 
 
+# ------------------------------------------------------------------------------ journal
+# Every save is written whole into `{exp_dir}/.pending/` (state.json included) while the previous
+# checkpoint stays untouched.  Once every rank's files are on disk rank 0 drops a COMMIT marker
+# into .pending and rolls it forward: each item replaces its counterpart in exp_dir, state.json
+# last, then .pending is removed.  A crash before COMMIT leaves the old checkpoint intact (the
+# partial .pending is discarded on the next start); a crash after it is finished by
+# `recover_checkpoint` on the next start.  Either way a launch never sees new weights beside an
+# old state.json, and never loses the last complete checkpoint.
+PENDING = ".pending"
+COMMIT = "COMMIT"
+
+
+def _roll_forward(exp_dir: Path):
+    import shutil
+
+    pend = exp_dir / PENDING
+    items = [it for it in pend.iterdir() if it.name not in (COMMIT, "state.json")]
+    for item in items:
+        dst = exp_dir / item.name
+        if dst.is_dir():
+            shutil.rmtree(dst)
+        os.replace(item, dst)
+    if (pend / "state.json").exists():
+        os.replace(pend / "state.json", exp_dir / "state.json")
+    shutil.rmtree(pend, ignore_errors=True)
+
+
+def commit_pending(exp_dir):
+    """Rank 0, after every rank finished writing into .pending: publish it atomically."""
+    exp_dir = Path(exp_dir)
+    marker = exp_dir / PENDING / COMMIT
+    with open(marker, "w") as fp:
+        fp.write("ok\n")
+        fp.flush()
+        os.fsync(fp.fileno())
+    _roll_forward(exp_dir)
+
+
+def recover_checkpoint(exp_dir) -> str:
+    """Finish or discard an interrupted save (call on rank 0 before `has_checkpoint`, then
+    barrier).  Returns "rolled-forward", "discarded" or "clean"."""
+    import shutil
+
+    exp_dir = Path(exp_dir)
+    pend = exp_dir / PENDING
+    if not pend.exists():
+        return "clean"
+    if (pend / COMMIT).exists():
+        _roll_forward(exp_dir)
+        return "rolled-forward"
+    shutil.rmtree(pend, ignore_errors=True)
+    return "discarded"
+
+
 # ------------------------------------------------------------------------------ RNG (G7)
 def rng_state(device):
     st = {"python": random.getstate(), "numpy": np.random.get_state(), "torch": torch.get_rng_state()}
@@ -204,19 +258,31 @@ def _replicated_engine(engine) -> bool:
     return getattr(engine, "mode", "fsdp") in ("single", "ddp")
 
 
+def _writes_shards(engine) -> bool:
+    """Whether this rank writes its slices: replicated copies are written once -- by the first
+    data-parallel rank of a replicated engine, by replica 0 of a HYBRID_SHARD engine (every
+    replica holds the same shards)."""
+    if _replicated_engine(engine):
+        return getattr(engine, "rank", 0) == 0
+    rg = getattr(engine, "replicate_group", None)
+    if getattr(engine, "replicas", 1) > 1 and rg is not None and dist.is_initialized():
+        return dist.get_rank(rg) == 0
+    return True
+
+
 def snapshot_sharded(engine, global_step=None):
     """Collective: copy this rank's parameter + AdamW-moment slices to host memory and gather
     the slice index of every rank.  Returns (tensors, entry, metadata-or-None) for
     write_sharded; after it returns the device state may change (async checkpointing).
 
     Replicated copies are written once: with a replicated engine (DDP / single) only the first
-    data-parallel rank of each TP group writes, and TP-replicated parameters (norms) only by
-    TP rank 0."""
+    data-parallel rank of each TP group writes, with HYBRID_SHARD only replica 0, and
+    TP-replicated parameters (norms) only TP rank 0."""
     rank, world = get_rank(), get_world_size()
     geo = _TPGeom(engine)
     gname = _name_map(engine)
     shapes_local = {n: list(p.shape) for n, p in engine.module.named_parameters()}
-    write = not (_replicated_engine(engine) and getattr(engine, "rank", 0) != 0)
+    write = _writes_shards(engine)
     skip = getattr(engine.module, "_dtg_ckpt_skip", set())  # e.g. a pipeline's second tied-embedding copy
     pieces = engine.ckpt_pieces()
     tensors, index = {}, []
@@ -307,9 +373,14 @@ def load_sharded(ckpt_dir, engine, load_optimizer: bool = True):
         if list(gshapes[gname(name)]) != mine:
             raise ValueError(f"{gname(name)}: checkpoint global shape {gshapes[gname(name)]} != model's {mine}")
     stored = {}  # name -> [(file, key, rect)]
+    seen = set()  # identical rectangles stored twice (replicas of a pre-fix HYBRID save): read once
     for f in meta["files"]:
         for k, (name, n, rects) in enumerate(f["index"]):
             for rc in rects:
+                key = (name, tuple(rc[:4]))
+                if key in seen:
+                    continue
+                seen.add(key)
                 stored.setdefault(name, []).append((f["file"], k, rc))
     cache = {}
 
@@ -353,14 +424,14 @@ def load_sharded(ckpt_dir, engine, load_optimizer: bool = True):
 class CheckpointManager:
     """Save/resume in the reference's layout. `style` in {"full", "dp", "sharded"}.
 
-    `async_save=True`: `save()` only snapshots the state to host memory (device
-    -> host copies plus the small metadata collectives) and returns; a background thread
-    writes the files into `{exp_dir}/.pending/`.  The next `save()` or `finalize()` joins the
-    writer on every rank, meets at a barrier, and rank 0 moves the finished files into place and
-    writes `state.json` LAST -- resume keys on state.json, so an interrupted write is never
-    mistaken for a checkpoint."""
+    Every save goes through the `.pending/` journal (see `commit_pending`): the previous
+    checkpoint stays valid until the new one is complete.  `async_save=True`:
+    `save()` only snapshots the state to host memory (device -> host copies plus the small
+    metadata collectives) and returns; a background thread writes the files into .pending.  The
+    next `save()` or `finalize()` joins the writer on every rank, meets at a barrier, and rank 0
+    commits."""
 
-    PENDING = ".pending"
+    PENDING = PENDING
 
     def __init__(self, exp_dir, engine, optimizer, lr_scheduler, style: str, local_rank: int = 0,
                  async_save: bool = False):
@@ -373,9 +444,8 @@ class CheckpointManager:
         self._pending = None  # (state, lr_scheduler state, rng state) to publish on finalize
         self._error = None
 
-    # ------------------------------------------------------------------ async path
     def _snapshot_host(self, global_step=None):
-        """Collective part of a save: everything the writer thread needs, on the host."""
+        """Collective part of a save: everything the writer needs, on the host."""
         jobs = []  # (relative path, object) for torch.save; sharded handled separately
         shard = None
         if self.style == "full":
@@ -401,6 +471,19 @@ class CheckpointManager:
         except BaseException as e:  # surfaced by finalize() on the main thread
             self._error = e
 
+    def _publish(self, state, sched_sd, rng):
+        """Rank 0: the small files into .pending, then the atomic commit."""
+        pend = self.exp_dir / self.PENDING
+        pend.mkdir(parents=True, exist_ok=True)
+        torch.save(sched_sd, pend / "lr_scheduler.pt")
+        if isinstance(rng, _RngBox):
+            torch.save(rng.obj, pend / "rng.pt")
+        else:
+            torch.save(rng, pend / "rng.pt")
+        with open(pend / "state.json", "w") as fp:
+            json.dump(state, fp)
+        commit_pending(self.exp_dir)
+
     def finalize(self):
         """Publish the pending async save (collective: call on every rank)."""
         if self._writer is None:
@@ -412,25 +495,18 @@ class CheckpointManager:
             raise RuntimeError("async checkpoint write failed") from err
         barrier()
         if get_rank() == 0:
-            import shutil
-
-            pend, d = self.exp_dir / self.PENDING, self.exp_dir
-            state, sched_sd, rng = self._pending
-            # state.json goes first and comes back last: a crash anywhere in between leaves no
-            # state.json, i.e. no checkpoint, instead of an old state.json beside new weights
-            if (d / "state.json").exists():
-                os.remove(d / "state.json")
-            for item in pend.iterdir():
-                dst = d / item.name
-                if dst.is_dir():
-                    shutil.rmtree(dst)
-                os.replace(item, dst)
-            torch.save(sched_sd, d / "lr_scheduler.pt")
-            torch.save(rng, d / "rng.pt")
-            with open(d / "state.json", "w") as fp:
-                json.dump(state, fp)
-            shutil.rmtree(pend, ignore_errors=True)
+            self._publish(*self._pending)
         self._pending = None
+        barrier()
+
+    def _begin(self):
+        """Collective: a clean .pending (a stale one from a crashed save is discarded)."""
+        import shutil
+
+        barrier()
+        if get_rank() == 0:
+            shutil.rmtree(self.exp_dir / self.PENDING, ignore_errors=True)
+            (self.exp_dir / self.PENDING).mkdir(parents=True, exist_ok=True)
         barrier()
 
     def save(self, state: dict):
@@ -438,7 +514,7 @@ class CheckpointManager:
             import threading
 
             self.finalize()
-            barrier()
+            self._begin()
             jobs, shard = self._snapshot_host(state.get("global_step"))
             if get_rank() == 0:
                 box = _RngBox()
@@ -449,29 +525,17 @@ class CheckpointManager:
             self._writer = threading.Thread(target=self._write_pending, args=(jobs, shard), daemon=False)
             self._writer.start()
             return
-        rank = get_rank()
-        d = self.exp_dir
+        self._begin()
+        jobs, shard = self._snapshot_host(state.get("global_step"))
+        self._write_pending(jobs, shard)
+        err, self._error = self._error, None
+        if err is not None:
+            raise RuntimeError("checkpoint write failed") from err
         barrier()
-        if rank == 0 and (d / "state.json").exists():
-            os.remove(d / "state.json")  # re-written last: never an old state beside new weights
-        barrier()
-        gs = state.get("global_step")
-        if self.style == "full":
-            if rank == 0:
-                torch.save(self.engine.full_state_dict(), d / "model.pt")
-                torch.save(self.optimizer.state_dict(), d / "optimizer.pt")
-        elif self.style == "dp":
-            sd = self.engine.full_state_dict()
-            if rank == 0:
-                torch.save(sd, d / "model.pt")
-            save_sharded(d / "checkpoint", self.engine, gs)
-        else:
-            save_sharded(d / "checkpoint", self.engine, gs)
-        if rank == 0:
-            torch.save(self.lr_scheduler.state_dict(), d / "lr_scheduler.pt")
-            save_rng(d / "rng.pt")
-            with open(d / "state.json", "w") as fp:
-                json.dump(state, fp)
+        if get_rank() == 0:
+            box = _RngBox()
+            save_rng(box)
+            self._publish(dict(state), self.lr_scheduler.state_dict(), box.obj)
         barrier()
 
     def load(self) -> dict:

@@ -31,10 +31,11 @@ from .. import data as dtg_data
 from ..models import build_model, count_valid_labels, resolve_config
 from ..parallel.checkpointing import apply_activation_checkpointing
 from ..parallel.data_parallel import DataParallel, FlatAdamW
+from ..utils import comm as ucomm
 from ..utils import dist as udist
 from ..utils.metrics import MI355X_BF16_DENSE_FLOPS, MetricSink, get_mem_stats
 from ..utils.timers import make_timers
-from .checkpoint import CheckpointManager, has_checkpoint, new_state
+from .checkpoint import CheckpointManager, has_checkpoint, new_state, recover_checkpoint
 from .cli import get_parser
 
 LOGGER = logging.getLogger("dtg")
@@ -117,10 +118,11 @@ def _build(args, chapter, device, world):
             from ..utils import comm as _comm
 
             engine = "dma" if args.tp_comm == "xgmi-dma" else "kernel"
+            timeout = float(os.environ.get("DTG_XGMI_TIMEOUT", getattr(args, "tp_comm_timeout", 60.0)))
             _comm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=args.tp_comm_mb << 20, device=device,
-                                                           gather_engine=engine))
+                                                           gather_engine=engine, timeout_s=timeout))
             LOGGER.info(f"tp collectives: direct-peer xGMI ({args.tp_comm_mb} MiB workspace per rank, "
-                        f"all-gathers on {'copy engines' if engine == 'dma' else 'pull kernels'})")
+                        f"collectives on {'copy engines' if engine == 'dma' else 'pull kernels'}, barrier timeout {timeout:g} s)")
     seq = None  # (kind, group, rank, degree): Ulysses / context parallel over each row
     nseq = max(getattr(args, "sp", 1), getattr(args, "cp", 1))
     if nseq > 1:
@@ -267,6 +269,11 @@ def run(chapter: str, argv=None):
     resumed = False
     mgr = CheckpointManager(exp_dir, engine, opt, lr_scheduler, style, local_rank,
                             async_save=getattr(args, "async_ckpt", "off") == "on")
+    if rank == 0 and exp_dir.exists():  # finish (or discard) a save interrupted by a crash
+        how = recover_checkpoint(exp_dir)
+        if how != "clean":
+            LOGGER.warning(f"{exp_dir}: interrupted checkpoint save {how}")
+    udist.barrier()
     if has_checkpoint(exp_dir):
         LOGGER.info(f"Resuming from {exp_dir}")
         state = mgr.load()
@@ -396,6 +403,7 @@ def run(chapter: str, argv=None):
                 state["running_loss"] += float(run_loss.item())
                 run_loss = None
             if state["global_step"] % args.log_freq == 0:
+                ucomm.check_xgmi()  # a timed-out xGMI barrier ends the job here (non-zero exit)
                 ms_per_step = sum(t.avg_elapsed_ms() for t in timers.values())
                 tps = 1000 * tok_per_step / ms_per_step if ms_per_step > 0 else 0.0
                 info = {
@@ -421,6 +429,7 @@ def run(chapter: str, argv=None):
                     t.reset()
 
             if state["global_step"] % args.ckpt_freq == 0:
+                ucomm.check_xgmi()  # never checkpoint state computed from stale peer data
                 LOGGER.info("Saving checkpoint.")
                 mgr.save(state)
             if args.max_steps and state["global_step"] >= args.max_steps:
@@ -429,12 +438,14 @@ def run(chapter: str, argv=None):
                 LOGGER.info(f"Reached --max-steps {args.max_steps}")
                 progress.close()
                 mgr.finalize()
+                ucomm.check_xgmi()
                 return state
         progress.close()
         state["epoch_step"] = 0
     if run_loss is not None:
         state["running_loss"] += float(run_loss.item())
     mgr.finalize()
+    ucomm.check_xgmi()
     return state
 
 

@@ -37,6 +37,23 @@ def unregister_xgmi(group):
     return _XGMI.pop(group, None)
 
 
+def check_xgmi():
+    """Raise XgmiError if any registered direct-peer communicator saw a barrier time out (a
+    peer died or fell out of step).  Synchronises the device.  Called by the trainer at every
+    log step, checkpoint and exit."""
+    for c in list(_XGMI.values()):
+        c.check()
+
+
+def rs_input_buffer(group, shape, dtype, stage_bytes: int = 0):
+    """Zero-copy reduce-scatter input: a workspace slot of the group's xGMI communicator for a
+    producer to write into, or None (no communicator / does not fit)."""
+    c = _XGMI.get(group)
+    if c is None or world(group) == 1:
+        return None
+    return c.rs_input_buffer(shape, dtype, stage_bytes)
+
+
 def _xgmi_for(group, x: torch.Tensor, nbytes: int):
     c = _XGMI.get(group)
     if c is not None and x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and c.fits(nbytes):
@@ -81,7 +98,9 @@ def reduce_scatter_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
     out = torch.empty((chunk,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     c = _xgmi_for(group, x, x.numel() * x.element_size())
     if c is not None:
-        return c.reduce_scatter_into(out, x)
+        c.reduce_scatter_into(out, x)
+        c.release_slot(x, None)  # stream-ordered: the slot is free for the next producer
+        return out
     dist.reduce_scatter_tensor(out, x, group=group)
     return out
 
@@ -196,7 +215,9 @@ def reduce_scatter_dim0_into_async(out: torch.Tensor, x: torch.Tensor, group=Non
         return _DoneWork()
     c = _xgmi_for(group, x, x.numel() * x.element_size())
     if c is not None:
-        return _on_side_stream(lambda: c.reduce_scatter_into(out, x), out, x)
+        w = _on_side_stream(lambda: c.reduce_scatter_into(out, x), out, x)
+        c.release_slot(x, w.event)
+        return w
     if backend_of(group) == "gloo":
         y = x.clone()
         dist.all_reduce(y, group=group)

@@ -190,3 +190,101 @@ def test_sharded_checkpoint_rejects_incomplete():
         os.remove(os.path.join(ck, "shard_r00000.pt"))
         with pytest.raises(FileNotFoundError):
             load_sharded(ck, eng2)
+
+
+def _hybrid_make():
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+    from dtg.parallel.tensor_parallel import make_mesh
+
+    torch.manual_seed(0)
+    replicate, shard_group, _, _, _ = make_mesh(2)
+    m = build_model("llama-tiny", device="cpu", dtype=torch.float32)
+    eng = FullyShard(m, group=shard_group, replicate_group=replicate, device="cpu")
+    return m, eng, FlatAdamW(eng, lr=1e-2, eps=1e-3)
+
+
+def _hybrid_save_worker(rank, world, batches, d):
+    from dtg.train.checkpoint import save_sharded
+
+    m, eng, opt = _hybrid_make()
+    _steps(m, eng, opt, batches[:2], rank, world)
+    save_sharded(os.path.join(d, "checkpoint"), eng)
+    _steps(m, eng, opt, batches[2:], rank, world)
+    return eng.full_state_dict(rank0_only=False)
+
+
+def _hybrid_load_worker(rank, world, batches, d):
+    from dtg.train.checkpoint import load_sharded
+
+    m, eng, opt = _hybrid_make()
+    load_sharded(os.path.join(d, "checkpoint"), eng)
+    assert eng.step_count == 2
+    _steps(m, eng, opt, batches[2:], rank, world)
+    return eng.full_state_dict(rank0_only=False)
+
+
+def test_hybrid_checkpoint_written_once_and_reshards():
+    """HYBRID_SHARD (2 replicas x 2-way shards): only replica 0 writes, every slice is indexed
+    once, and the checkpoint resumes both as HYBRID (world 4) and as FULL_SHARD (world 2)."""
+    import json
+
+    batches = _batches(512, 4, 32, n=3)
+    with tempfile.TemporaryDirectory() as d:
+        cont = run_distributed(_hybrid_save_worker, 4, batches, d)[0]
+        meta = json.load(open(os.path.join(d, "checkpoint", "index.json")))
+        assert sorted(f["rank"] for f in meta["files"]) == [0, 1], [f["rank"] for f in meta["files"]]
+        for r in (2, 3):
+            assert not os.path.exists(os.path.join(d, "checkpoint", f"shard_r{r:05d}.pt"))
+        again = run_distributed(_hybrid_load_worker, 4, batches, d)
+        for n in cont:
+            torch.testing.assert_close(again[3][n], cont[n], **TOL, msg=n)
+        full = run_distributed(_load_worker, 2, "fsdp", batches, d)[0]
+        for n in cont:
+            torch.testing.assert_close(full[n], cont[n], **TOL, msg=n)
+
+
+def test_interrupted_save_keeps_previous_checkpoint(tmp_path):
+    """A crash before the commit marker leaves the previous checkpoint loadable (the partial
+    .pending is discarded); a crash after it is rolled forward on the next start."""
+    import json
+    import shutil
+
+    from dtg.train.checkpoint import (COMMIT, CheckpointManager, has_checkpoint, new_state,
+                                      recover_checkpoint)
+
+    m, eng, opt = _make("single")
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10)
+    mgr = CheckpointManager(tmp_path, eng, opt, sched, "full")
+    st = new_state()
+    st["global_step"] = 5
+    mgr.save(st)
+    assert has_checkpoint(tmp_path) and not (tmp_path / ".pending").exists()
+    before = torch.load(tmp_path / "model.pt", weights_only=True)
+    # crash in the middle of writing the next save: a .pending without COMMIT
+    pend = tmp_path / ".pending"
+    pend.mkdir()
+    (pend / "model.pt").write_bytes(b"partial")
+    assert recover_checkpoint(tmp_path) == "discarded"
+    assert not pend.exists() and json.loads((tmp_path / "state.json").read_text())["global_step"] == 5
+    after = torch.load(tmp_path / "model.pt", weights_only=True)
+    assert all(torch.equal(before[k], after[k]) for k in before)
+    # crash after COMMIT, half-way through the roll-forward: state.json still old, new model.pt
+    # already moved, the rest still pending -> the next start finishes the move
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(1.0)
+    st["global_step"] = 9
+    staging = tmp_path / "staging"
+    mgr2 = CheckpointManager(staging, eng, opt, sched, "full")
+    mgr2.save(st)
+    pend.mkdir()
+    for name in ("optimizer.pt", "lr_scheduler.pt", "rng.pt", "state.json"):
+        shutil.copy(staging / name, pend / name)
+    (pend / COMMIT).write_text("ok\n")
+    shutil.copy(staging / "model.pt", tmp_path / "model.pt")  # moved before the crash
+    assert json.loads((tmp_path / "state.json").read_text())["global_step"] == 5
+    assert recover_checkpoint(tmp_path) == "rolled-forward"
+    assert json.loads((tmp_path / "state.json").read_text())["global_step"] == 9 and not pend.exists()
+    assert CheckpointManager(tmp_path, eng, opt, sched, "full").load()["global_step"] == 9

@@ -30,7 +30,7 @@ def _run(model, eng, ids):
     return out.loss.item()
 
 
-def _worker(rank, world, rows=2, chunks=1):
+def _worker(rank, world, rows=2, chunks=1, engine="kernel"):
     import torch.distributed as dist
 
     from dtg.models import build_model, resolve_config
@@ -42,7 +42,8 @@ def _worker(rank, world, rows=2, chunks=1):
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
     _, tp_group, _, tp_rank, _ = make_mesh(2)
-    dcomm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=16 << 20, device=dev, timeout_s=5.0))
+    dcomm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=16 << 20, device=dev, timeout_s=5.0,
+                                                    gather_engine=engine))
     cfg = resolve_config(MODEL)
     torch.manual_seed(0)
     full = build_model(cfg, device="cpu", dtype=torch.bfloat16)
@@ -58,8 +59,10 @@ def _worker(rank, world, rows=2, chunks=1):
     return res
 
 
-@pytest.mark.parametrize("rows,chunks", [(2, 1), (4, 2)])
-def test_tp2_xgmi_matches_single_device(cuda, rows, chunks):
+@pytest.mark.parametrize("rows,chunks,engine", [(2, 1, "kernel"), (4, 2, "kernel"), (4, 2, "dma")])
+def test_tp2_xgmi_matches_single_device(cuda, rows, chunks, engine):
+    """chunks=2: overlapped regions whose row-parallel GEMMs write into the workspace slots
+    (zero-copy reduce-scatter); engine="dma": copy-engine pulls on per-peer streams."""
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel
     from dtg.parallel.tensor_parallel import unshard_state_dicts
@@ -70,7 +73,7 @@ def test_tp2_xgmi_matches_single_device(cuda, rows, chunks):
     eng = DataParallel(ref, mode="single")
     ref_loss = _run(ref, eng, _ids(cfg.vocab_size, rows).to(cuda))
     ref_g = _grads(ref)
-    res = run_distributed(_worker, 2, rows, chunks)
+    res = run_distributed(_worker, 2, rows, chunks, engine)
     assert abs(res[0][0] - ref_loss) < 2e-2 * abs(ref_loss) and res[0][0] == res[1][0]
     shards = [r[1] for r in sorted(res, key=lambda r: r[2])]
     full = unshard_state_dicts(shards, cfg)

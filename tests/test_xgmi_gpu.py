@@ -63,25 +63,80 @@ def _worker(rank, world, engine="kernel"):
     z = dcomm.reduce_scatter_dim0(torch.ones(32, 64, device=dev), None)
     torch.cuda.synchronize()
     out["routed"] = (y[:16].float().mean().item(), y[16:].float().mean().item(), z.mean().item(), tuple(z.shape))
+    # zero-copy: the input is written straight into a workspace slot (no stage copy), twice per
+    # slot so the slot-reuse wait is exercised; rows [r*8, (r+1)*8) of every rank's input sum up
+    zc = []
+    for i in range(4):
+        buf = c.rs_input_buffer((8 * world, 64), torch.bfloat16, stage_bytes=8 * 64 * 2)
+        assert buf is not None and c.ws.data_ptr() <= buf.data_ptr() < c.ws.data_ptr() + c.capacity
+        buf.copy_(torch.full((8 * world, 64), float(rank + i), device=dev, dtype=torch.bfloat16))
+        o = torch.empty(8, 64, device=dev, dtype=torch.bfloat16)
+        w = dcomm.reduce_scatter_dim0_into_async(o, buf, None)
+        w.wait()
+        zc.append(o.float().mean().item())
+    torch.cuda.synchronize()
+    out["zero_copy"] = zc
     dcomm.unregister_xgmi(None)
     dist.barrier()
     c.close()
     return out
 
 
-@pytest.mark.parametrize("engine", ["kernel", "dma"])
-def test_xgmi_collectives_two_ranks(cuda, engine):
-    """engine="dma": the all-gather's stage and pulls are copy-engine transfers (hipMemcpyAsync)."""
-    res = run_distributed(_worker, 2, engine)
-    for r in range(2):
+@pytest.mark.parametrize("engine,world", [("kernel", 2), ("dma", 2), ("kernel", 4), ("dma", 4)])
+def test_xgmi_collectives(cuda, engine, world):
+    """engine="dma": stage and pulls are copy-engine transfers (hipMemcpyAsync, one stream per
+    peer); the reduce-scatter sums the pulled slices locally."""
+    res = run_distributed(_worker, world, engine)
+    for r in range(world):
         for k, v in res[r].items():
             if k == "repeat":
                 assert v == 0, v
                 continue
+            if k == "zero_copy":
+                exp = [sum(q + i for q in range(world)) for i in range(4)]
+                assert v == exp, (r, v, exp)
+                continue
             if k == "routed":
-                assert v[0] == 0.0 and v[1] == 1.0 and v[2] == 2.0 and v[3] == (16, 64), v
+                assert v[0] == 0.0 and v[1] == 1.0 and v[2] == float(world) and v[3] == (16, 64), v
                 continue
             ag_ok, rs_err, ar_err = v
             assert ag_ok, (r, k)
             tol = 0.05 if "bfloat16" in k[0] else 1e-5
             assert rs_err <= tol and ar_err <= tol, (r, k, rs_err, ar_err)
+
+
+def _fault_worker(rank, world):
+    import os
+    import time
+
+    import torch.distributed as dist
+
+    from dtg.parallel.xgmi import XgmiCommunicator, XgmiError
+
+    os.environ["DTG_XGMI_FAULT"] = "1:2"  # group rank 1 skips its third collective
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    c = XgmiCommunicator(None, capacity_bytes=1 << 20, device=dev, timeout_s=0.5)
+    x = torch.ones(1024, device=dev)
+    t0 = time.time()
+    for _ in range(20):  # after the first timeout every barrier returns at once (sticky error)
+        c.all_reduce_(x)
+    torch.cuda.synchronize()
+    took = time.time() - t0
+    err = None
+    try:
+        c.check()
+    except XgmiError as e:
+        err = str(e)
+    dist.barrier()
+    c.close()
+    return err, took
+
+
+def test_xgmi_barrier_timeout_is_sticky_and_raises(cuda):
+    """A peer that skips a collective: the waiting rank's barrier times out once (not once per
+    later collective), check() raises XgmiError naming the peer, nothing hangs."""
+    res = run_distributed(_fault_worker, 2)
+    err0, took0 = res[0]
+    assert err0 is not None and "peer 1" in err0, res
+    assert took0 < 10.0, took0  # one 0.5 s timeout, not 20 of them

@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--marker", default="adamw_kernel")
+    ap.add_argument("--sequence", default=None, help="write the last step's ordered kernel list (us, name) here")
     a = ap.parse_args()
     rows = []
     for f in glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True):
@@ -67,6 +68,10 @@ def main():
         print("|---|---:|---:|---:|")
         for k, (t, c) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
             print(f"| `{k[:70]}` | {c} | {t / 1e6:.2f} | {100 * t / tot:.1f} |")
+        if a.sequence:
+            with open(a.sequence, "w") as fp:
+                for s, e, n in sorted(last):
+                    fp.write(f"{(e - s) / 1e3:10.1f}  {n.split('(')[0][:150]}\n")
 
 
 if __name__ == "__main__":
