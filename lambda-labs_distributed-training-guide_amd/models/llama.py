@@ -330,13 +330,12 @@ class LlamaForCausalLM(nn.Module):
         cp_ranges = None
         if self.cp_group is not None:  # attention over zig-zag chunks; cu_seqlens (if given) are the
             # FULL rows' document boundaries of a packed batch (cp_batch keeps the collator's)
-            if cu_seqlens is not None:
-                from ..parallel.context_parallel import cp_ranges as _cp_ranges, row_doc_starts
+            if cu_seqlens is not None:  # built on the device: no host sync per forward
+                from ..parallel.context_parallel import cp_ranges as _cp_ranges
                 from ..utils import comm
 
                 n = comm.world(self.cp_group)
-                docs = row_doc_starts(cu_seqlens, B, S * n)
-                cp_ranges = _cp_ranges(comm.rank(self.cp_group), n, B, S // 2, dev, docs)
+                cp_ranges = _cp_ranges(comm.rank(self.cp_group), n, B, S // 2, dev, cu_seqlens=cu_seqlens)
             pos, cu, max_seqlen = position_ids.reshape(-1).to(torch.long), None, 0
         elif position_ids is None:
             pos, cu = self._dense_meta(B, S, dev)

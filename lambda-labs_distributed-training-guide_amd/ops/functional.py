@@ -473,49 +473,84 @@ def fused_linear_cross_entropy(h, w, labels, ignore_index=-100, num_valid=None, 
 class _VocabParallelFusedLinearCE(torch.autograd.Function):
     """lm_head sharded over the vocabulary across `group` (tensor parallel); h is replicated.
 
-    Per chunk: local logits -> (max, sum-exp, target logit) -> all-reduces over the TP group
-    -> global log-sum-exp -> local softmax gradient in place.  The returned
-    dh is this rank's vocab-shard PARTIAL; the caller's TP-region entry (sequence all-gather,
-    whose backward is a reduce-scatter) sums it across ranks."""
+    Per chunk: local logits -> per-row (max, sum-exp, target logit) -> ONE all-gather of those
+    [3, rows] stats over the TP group -> global log-sum-exp -> local softmax gradient in place
+    (SURVEY C12/K13).  The chunk loop is software-pipelined: chunk j's stats all-gather is in
+    flight (async, RCCL's stream) while chunk j+1's logits GEMM and stats kernel run, and only
+    then does chunk j's gradient pass wait for it -- no collective sits between the GEMMs.  The
+    weight gradient uses K-contiguous (TN) operands and, with an engine-owned loss, accumulates
+    straight into `main_grad` (no [V/tp, H] temporary).  The returned dh is this rank's
+    vocab-shard PARTIAL; the caller's TP-region entry (sequence all-gather, whose backward is a
+    reduce-scatter) sums it across ranks."""
 
     @staticmethod
     def forward(ctx, h, w, labels, ignore_index, num_valid, chunk, vocab_start, group):
+        from ..utils import comm as _comm
+
         T = h.shape[0]
         need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         scale = 1.0 / max(num_valid, 1)
         loss_sum = torch.zeros((), dtype=torch.float32, device=h.device)
         dh = torch.empty_like(h) if need else None
-        dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if need else None
-        w_t = ops.transpose2d(w) if (need and _ce_tn(h, w)) else None
-        for s in range(0, T, chunk):
-            e = min(T, s + chunk)
-            lab = labels[s:e]
+        want_dw = need and ctx.needs_input_grad[1]
+        direct = want_dw and _gr.direct_loss_grad() and getattr(w, "main_grad", None) is not None
+        dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if (want_dw and not direct) else None
+        tn = need and _ce_tn(h, w) and chunk % 8 == 0 and w.shape[0] % 8 == 0
+        w_t = ops.transpose2d(w) if (tn and ctx.needs_input_grad[0]) else None
+
+        def issue(s, e):
             logits = torch.mm(h[s:e], w.t())
-            m, sx, xl = ops.ce_stats(logits, lab, vocab_start)
-            gm = m.clone()
-            dist.all_reduce(gm, op=dist.ReduceOp.MAX, group=group)
-            sx = sx * torch.exp(m - gm)
-            stats = torch.stack([sx, xl])
-            dist.all_reduce(stats, group=group)
-            lse = gm + torch.log(stats[0])
+            m, sx, xl = ops.ce_stats(logits, labels[s:e], vocab_start)
+            stats, work = _comm.all_gather_stack_async(torch.stack([m, sx, xl]), group)
+            return s, e, logits, stats, work
+
+        def finish(s, e, logits, stats, work):
+            nonlocal loss_sum
+            work.wait()
+            gm = stats[:, 0].amax(0)
+            sx = (stats[:, 1] * torch.exp(stats[:, 0] - gm)).sum(0)
+            lse = gm + torch.log(sx)
+            lab = labels[s:e]
             valid = lab != ignore_index
-            loss_sum += torch.where(valid, lse - stats[1], torch.zeros_like(lse)).sum()
-            if need:
-                ops.ce_grad_(logits, lab, lse.contiguous(), vocab_start, ignore_index, scale)
-                _ce_dx(logits, w, w_t, dh[s:e])
-                if s == 0:
-                    torch.mm(logits.t(), h[s:e], out=dw)
+            loss_sum += torch.where(valid, lse - stats[:, 2].sum(0), torch.zeros_like(lse)).sum()
+            if not need:
+                return
+            ops.ce_grad_(logits, lab, lse.contiguous(), vocab_start, ignore_index, scale)
+            _ce_dx(logits, w, w_t, dh[s:e])
+            if not want_dw:
+                return
+            a_t = ops.transpose2d(logits) if tn else None
+            b_t = ops.transpose2d(h[s:e]) if tn else None
+            if direct:
+                _gr.accumulate_mm_into_main_grad(w, logits, h[s:e], a_t=a_t, b_t=b_t)
+            else:
+                lhs, rhs = (a_t, b_t.t()) if tn else (logits.t(), h[s:e])
+                if s == 0:  # f32 accumulate inside the GEMM, one bf16 rounding per chunk
+                    torch.mm(lhs, rhs, out=dw)
                 else:
-                    dw.addmm_(logits.t(), h[s:e])
+                    dw.addmm_(lhs, rhs)
+
+        pend = None
+        for s in range(0, T, chunk):
+            cur = issue(s, min(T, s + chunk))  # GEMM j+1 overlaps the stats gather of chunk j
+            if pend is not None:
+                finish(*pend)
+            pend = cur
+        if pend is not None:
+            finish(*pend)
         ctx.save_for_backward(dh, dw)
         ctx.w = w
+        ctx.direct = direct
         return loss_sum * scale
 
     @staticmethod
     def backward(ctx, go):
         dh, dw = ctx.saved_tensors
-        gdh = dh * go.to(dh.dtype)
-        gdw = route_param_grad(ctx.w, dw * go.to(dw.dtype))
+        if ctx.direct:
+            _gr.notify_param(ctx.w)
+            return dh, None, None, None, None, None, None, None
+        gdh = dh * go.to(dh.dtype) if ctx.needs_input_grad[0] else None
+        gdw = route_param_grad(ctx.w, dw * go.to(dw.dtype)) if dw is not None else None
         return gdh, gdw, None, None, None, None, None, None
 
 

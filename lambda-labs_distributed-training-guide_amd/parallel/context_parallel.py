@@ -6,22 +6,29 @@ c = S / (2*cp) tokens and rank r keeps chunks r and 2*cp-1-r.  Norms, projection
 and the loss are token-local and run on the local shard unchanged; only attention needs the
 other ranks' keys and values:
 
-  forward   all-gather K|V over the group (one RCCL all-gather per layer -- the 8 GPUs of an
-            MI355X node are fully connected, so the gather needs no ring of point-to-point
-            steps) and put the rows in global order (one index_select); then ONE varlen flash
-            call in which every local query chunk g is a sequence whose keys are its row's
-            prefix 0 .. (g+1)c, causal mask bottom-right aligned (the kernels' per-sequence key
-            ranges).  No per-block launches and no log-sum-exp merge.
-  backward  one varlen backward per local chunk slot (the two slots' key prefixes overlap),
-            dK / dV of the two added, one index_select back to rank order and one
-            reduce-scatter to the owners: O(1) launches per layer in both passes.
+  forward   start the all-gather of K|V over the group (one asynchronous RCCL all-gather per
+            layer -- the 8 GPUs of an MI355X node are fully connected, so the gather needs no
+            ring of point-to-point steps) and, while it is in flight, run the DIAGONAL blocks:
+            every local query chunk against its own keys (causal), from the local K/V.  Then put
+            the gathered rows in global order (one index_select) and run the OFF-DIAGONAL part:
+            every local chunk g against its row's strict prefix 0 .. g*c (no mask).  The two
+            partial softmaxes are merged by their log-sum-exps (one elementwise pass).
+  backward  off-diagonal: one varlen backward per local chunk slot (the two slots' key
+            prefixes overlap), dK / dV of the two added in f32, one index_select back to rank
+            order and one f32 reduce-scatter to the owners -- issued asynchronously, and the
+            diagonal blocks' backward runs while it is in flight.  O(1) launches per layer in
+            both passes; both parts use the MERGED out / lse, so each gets the gradient of the
+            full softmax.
 
 Work per rank: the causal work of chunks r and 2cp-1-r, equal on every rank.
 
 Packed rows (several documents per row, 00-rime): a local chunk is cut at the document
-boundaries into pieces, and each piece is a varlen "sequence" whose keys are its document's
-prefix up to the piece's end (bottom-right causal alignment again) -- attention never crosses a
-document, RoPE uses the per-document positions, and the launch count stays O(1) per layer.
+boundaries into pieces; a piece's diagonal keys are the piece itself and its off-diagonal keys
+its document's part before the chunk (empty if the document starts inside the chunk) --
+attention never crosses a document, RoPE uses the per-document positions, and the launch count
+stays O(1) per layer.  The varlen descriptions are built ON THE DEVICE from the collator's
+cu_seqlens (`cp_ranges`): one entry per (document, local chunk) -- zero-length where they do not
+meet -- so nothing is copied to the host and no forward synchronises.
 """
 from __future__ import annotations
 
@@ -84,21 +91,9 @@ def _chunk_perm(cp: int, device) -> torch.Tensor:
     return torch.tensor(idx, dtype=torch.long, device=device)
 
 
-def _gather_kv(k, v, group, cp, B, c):
-    """Local K|V [B*2c, H, D] -> full rows [B*S, H, D] (K and V) in global token order: one
-    all-gather and one index_select, no per-chunk copies."""
-    kv = torch.cat([k, v], dim=1).contiguous()                      # [B*2c, 2H, D]
-    out = comm.all_gather_dim0(kv, group) if cp > 1 else kv          # [cp*B*2c, 2H, D]
-    H2, D = kv.shape[1], kv.shape[2]
-    rs = out.view(cp, B, 2, c, H2, D).transpose(0, 1).reshape(B, 2 * cp, c, H2, D)  # (rank, slot) order
-    full = rs.index_select(1, _chunk_perm(cp, kv.device)).reshape(B * 2 * cp * c, H2, D)
-    H = H2 // 2
-    return full[:, :H].contiguous(), full[:, H:].contiguous()
-
-
 def row_doc_starts(cu_seqlens, B: int, S: int):
     """Per-row document start offsets (row coordinates, 0 included) from the flattened [B*S]
-    document boundaries of a packed batch (`PackedCollator`'s cu_seqlens)."""
+    document boundaries of a packed batch (host lists; diagnostics and tests)."""
     cu = [int(x) for x in torch.as_tensor(cu_seqlens).tolist()]
     rows = [[0] for _ in range(B)]
     for x in cu:
@@ -109,10 +104,9 @@ def row_doc_starts(cu_seqlens, B: int, S: int):
 
 
 def packed_ranges(rank, cp, B, c, row_docs, device, slots=(0, 1)):
-    """Varlen description of the local query chunks of `slots` for packed rows: every (row, slot)
-    chunk is cut at document boundaries; a piece is one sequence whose keys are its document's
-    prefix in the gathered full rows, up to the piece's last token.  Returns (cu_seqlens_q,
-    k_start, k_len, max_q, max_k)."""
+    """Host reference of the single-call layout (query piece -> its document's prefix up to the
+    piece's end, bottom-right causal): (cu_seqlens_q, k_start, k_len, max_q, max_k) without
+    empty pieces.  Kept for tests and diagnostics; training uses `cp_ranges`."""
     S = 2 * cp * c
     g = zigzag_chunks(rank, cp)
     qlens, starts, lens = [], [], []
@@ -133,80 +127,151 @@ def packed_ranges(rank, cp, B, c, row_docs, device, slots=(0, 1)):
     return mk(cu), mk(starts), mk(lens), max(qlens), max(lens)
 
 
-def cp_ranges(rank, cp, B, c, device, row_docs=None):
-    """{"all": ranges of both local slots, 0: slot 0, 1: slot 1} for the forward and the two
-    per-slot backward calls (dense rows: one sequence per chunk)."""
-    if row_docs is None:
-        f = lambda sl: _ranges(rank, cp, B, c, device, sl)
-        return {k: (*f(sl)[:3], c, f(sl)[3]) for k, sl in (("all", (0, 1)), (0, (0,)), (1, (1,)))}
-    return {k: packed_ranges(rank, cp, B, c, row_docs, device, sl) for k, sl in (("all", (0, 1)), (0, (0,)), (1, (1,)))}
+_RANGE_CACHE = {}
 
 
-def _ranges(rank, cp, B, c, device, slots=(0, 1)):
-    """cu_seqlens over the local query chunks of `slots` (one sequence per (row, slot)) and
-    each chunk's key range: the prefix of its row up to and including its own chunk."""
+def cp_ranges(rank, cp, B, c, device, row_docs=None, cu_seqlens=None):
+    """Device-side varlen descriptions of this rank's local query chunks (no host sync).
+
+    Documents come from `cu_seqlens` (the collator's flattened [B*S] boundaries, row starts
+    included), or host `row_docs` (per-row document starts), or -- both None -- one document
+    per row (dense).  Every (document, local chunk) pair is one entry (zero-length when they do
+    not meet).  Returns a dict of (cu_seqlens_q, k_start, k_len, max_q, max_k) int32 tuples:
+      "diag"     both slots, rows in local (row, slot) order; keys = the piece itself in the LOCAL
+                 K/V (causal);
+      "off"      same queries; keys = the document's part before the chunk in the GATHERED full
+                 rows (no mask; length 0 when the document starts inside the chunk);
+      "off0/1"   the off-diagonal part of one slot, rows in that slot's (row) order (backward)."""
     S = 2 * cp * c
+    dense = cu_seqlens is None and row_docs is None
+    key = (rank, cp, B, c, str(device)) if dense else None
+    if key is not None and key in _RANGE_CACHE:
+        return _RANGE_CACHE[key]
+    if cu_seqlens is not None:
+        cu = cu_seqlens.to(device=device, dtype=torch.long)
+    elif row_docs is not None:
+        cu = torch.tensor([b * S + d for b in range(B) for d in row_docs[b]] + [B * S], dtype=torch.long, device=device)
+    else:
+        cu = torch.arange(0, (B + 1) * S, S, dtype=torch.long, device=device)
+    b = cu[:-1] // S
+    ds, de = cu[:-1] - b * S, cu[1:] - b * S  # row-local document spans (documents never cross rows)
     g = zigzag_chunks(rank, cp)
-    starts, lens = [], []
-    for b in range(B):
-        for s in slots:
-            starts.append(b * S)
-            lens.append((g[s] + 1) * c)
-    n = len(starts)
-    cu = torch.arange(0, (n + 1) * c, c, dtype=torch.int32, device=device)
-    mk = lambda xs: torch.tensor(xs, dtype=torch.int32, device=device)
-    return cu, mk(starts), mk(lens), max(lens)
+    per = []
+    for s in (0, 1):
+        lo = g[s] * c
+        a = torch.clamp(ds, min=lo)
+        qlen = torch.clamp(torch.clamp(de, max=lo + c) - a, min=0)
+        ks_diag = (2 * b + s) * c + torch.clamp(a - lo, 0, c)
+        kl_off = torch.where(qlen > 0, torch.clamp(lo - ds, min=0), torch.zeros_like(qlen))
+        per.append((qlen, ks_diag, b * S + ds, kl_off))
+    i32 = lambda t: t.to(torch.int32).contiguous()
+
+    def cu_of(qlen):
+        return i32(torch.cat([torch.zeros(1, dtype=torch.long, device=device), torch.cumsum(qlen, 0)]))
+
+    # both slots in local (row, slot, document) order: a stable sort by 2*row + slot
+    order = torch.sort(torch.cat([2 * b, 2 * b + 1]), stable=True).indices
+    cat = lambda j: torch.cat([per[0][j], per[1][j]])[order]
+    qlen_all = cat(0)
+    out = {
+        "diag": (cu_of(qlen_all), i32(cat(1)), i32(qlen_all), c, c),
+        "off": (cu_of(qlen_all), i32(cat(2)), i32(cat(3)), c, S),
+    }
+    for s in (0, 1):
+        qlen, _, ks_off, kl_off = per[s]
+        out[f"off{s}"] = (cu_of(qlen), i32(ks_off), i32(kl_off), c, S)
+    if key is not None:
+        _RANGE_CACHE[key] = out
+    return out
+
+
+def _merge(o_a, lse_a, o_b, lse_b):
+    """Two partial softmax attentions over disjoint key sets -> the attention over their union."""
+    lse = torch.logaddexp(lse_a, lse_b)                       # [Hq, T]
+    wa = torch.exp(lse_a - lse).t().unsqueeze(-1)             # [T, Hq, 1]
+    wb = torch.exp(lse_b - lse).t().unsqueeze(-1)
+    o = (o_a.float() * wa + o_b.float() * wb).to(o_a.dtype)
+    return o.contiguous(), lse.contiguous()
+
+
+def _order_full(gathered, cp, B, c):
+    """Gathered K|V [cp*B*2c, 2H, D] in (rank, slot) order -> full rows [B*S, 2H, D]."""
+    H2, D = gathered.shape[1], gathered.shape[2]
+    rs = gathered.view(cp, B, 2, c, H2, D).transpose(0, 1).reshape(B, 2 * cp, c, H2, D)
+    return rs.index_select(1, _chunk_perm(cp, gathered.device)).reshape(B * 2 * cp * c, H2, D)
 
 
 class _CPAttention(torch.autograd.Function):
-    """Each local query chunk attends to the causal prefix of its row in ONE varlen flash call
-    (per-sequence key ranges, bottom-right causal alignment): no per-block launches, no
-    log-sum-exp merge.  Backward: one varlen call per local chunk slot (their key prefixes
-    overlap, so dK / dV of the two slots are computed separately and added), then one
-    reduce-scatter of the full-row dK|dV to the owners."""
+    """Diagonal blocks (local K/V, overlapped with the K/V all-gather) + off-diagonal prefixes
+    (gathered K/V) in two varlen flash calls, merged by log-sum-exp; see the module docstring."""
 
     @staticmethod
     def forward(ctx, q, k, v, group, cp, rank, B, scale, ranges):
         # q [B*2c, Hq, D], k / v [B*2c, Hkv, D] (local zig-zag shard, row-major over rows)
         T, Hq, D = q.shape
+        Hkv = k.shape[1]
         c = T // (2 * B)
-        kf, vf = _gather_kv(k, v, group, cp, B, c)
+        kv = torch.cat([k, v], dim=1).contiguous()  # [B*2c, 2Hkv, D]
+        if cp > 1:
+            gathered = torch.empty((cp * T,) + tuple(kv.shape[1:]), dtype=kv.dtype, device=kv.device)
+            work = comm.all_gather_dim0_into_async(gathered, kv, group)
         q = q.contiguous()
         if ranges is None:
             ranges = cp_ranges(rank, cp, B, c, q.device)
-        cu, ks, kl, maxq, maxk = ranges["all"]
-        out, lse = torch.ops.dtg.flash_attn_varlen_fwd(q, kf, vf, cu, ks, kl, maxq, maxk, scale, True)
-        ctx.save_for_backward(q, kf, vf, out, lse)
-        ctx.meta = (group, cp, rank, B, c, scale, k.shape[1], ranges)
+        kl_, vl_ = kv[:, :Hkv], kv[:, Hkv:]
+        o_a, lse_a = torch.ops.dtg.flash_attn_varlen_fwd(q, kl_, vl_, *ranges["diag"], scale, True)
+        if cp > 1:
+            work.wait()
+            full = _order_full(gathered, cp, B, c)
+            del gathered
+        else:
+            full = kv
+        kf, vf = full[:, :Hkv], full[:, Hkv:]
+        o_b, lse_b = torch.ops.dtg.flash_attn_varlen_fwd(q, kf, vf, *ranges["off"], scale, False)
+        out, lse = _merge(o_a, lse_a, o_b, lse_b)
+        ctx.save_for_backward(q, kv, full, out, lse)
+        ctx.meta = (group, cp, rank, B, c, scale, Hkv, ranges)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, kf, vf, out, lse = ctx.saved_tensors
+        q, kv, full, out, lse = ctx.saved_tensors
         group, cp, rank, B, c, scale, Hkv, ranges = ctx.meta
         T, Hq, D = q.shape
+        dout = dout.contiguous()
+        kf, vf = full[:, :Hkv], full[:, Hkv:]
         sl = lambda t: t.view(B, 2, c, *t.shape[1:])
-        q5, o5, do5 = sl(q), sl(out), sl(dout.contiguous())
+        q5, o5, do5 = sl(q), sl(out), sl(dout)
         lse4 = lse.view(Hq, B, 2, c)
-        dq = torch.empty_like(q5)
+        dq_b = torch.empty((B, 2, c, Hq, D), dtype=torch.float32, device=q.device)
         dk = dv = None
-        for s in (0, 1):
-            cu, ks, kl, maxq, maxk = ranges[s]
+        for s in (0, 1):  # off-diagonal: the two slots' key prefixes overlap -> one call each
             flat = lambda t: t[:, s].reshape(B * c, *t.shape[3:])
             dqs, dks, dvs = torch.ops.dtg.flash_attn_varlen_bwd(
-                flat(do5), flat(q5), kf, vf, flat(o5), lse4[:, :, s].reshape(Hq, B * c).contiguous(), cu, ks, kl, maxq, maxk,
-                scale, True)
-            dq[:, s] = dqs.view(B, c, Hq, D)
+                flat(do5), flat(q5), kf, vf, flat(o5), lse4[:, :, s].reshape(Hq, B * c).contiguous(),
+                *ranges[f"off{s}"], scale, False)
+            dq_b[:, s] = dqs.view(B, c, Hq, D).float()
             dk = dks.float() if dk is None else dk + dks.float()
             dv = dvs.float() if dv is None else dv + dvs.float()
-        # full-row dK|dV -> (rank, slot) order -> reduce-scatter to the owners
-        S = 2 * cp * c
-        dkv = torch.cat([dk, dv], dim=1).to(q.dtype).view(B, 2 * cp, c, 2 * Hkv, D)
+        # full-row dK|dV (f32) -> (rank, slot) order -> reduce-scatter to the owners, in flight
+        # while the diagonal blocks' backward runs
+        dkv = torch.cat([dk, dv], dim=1).view(B, 2 * cp, c, 2 * Hkv, D)
+        del dk, dv
         inv = torch.argsort(_chunk_perm(cp, q.device))
-        send = dkv.index_select(1, inv).view(B, cp, 2, c, 2 * Hkv, D).transpose(0, 1).reshape(cp * B * 2 * c, 2 * Hkv, D)
-        mine = comm.reduce_scatter_dim0(send.contiguous(), group) if cp > 1 else send  # [B*2c, 2Hkv, D]
-        return (dq.view(T, Hq, D), mine[:, :Hkv].contiguous(), mine[:, Hkv:].contiguous(),
-                None, None, None, None, None, None)
+        send = dkv.index_select(1, inv).view(B, cp, 2, c, 2 * Hkv, D).transpose(0, 1).reshape(cp * T, 2 * Hkv, D)
+        if cp > 1:
+            mine = torch.empty((T, 2 * Hkv, D), dtype=torch.float32, device=q.device)
+            work = comm.reduce_scatter_dim0_into_async(mine, send.contiguous(), group)
+        else:
+            mine, work = send, None
+        dq_a, dk_a, dv_a = torch.ops.dtg.flash_attn_varlen_bwd(dout, q, kv[:, :Hkv], kv[:, Hkv:], out, lse,
+                                                               *ranges["diag"], scale, True)
+        if work is not None:
+            work.wait()
+        dq = (dq_a.float() + dq_b.view(T, Hq, D)).to(q.dtype)
+        dk = (dk_a.float() + mine[:, :Hkv]).to(q.dtype)
+        dv = (dv_a.float() + mine[:, Hkv:]).to(q.dtype)
+        return dq, dk, dv, None, None, None, None, None, None
 
 
 def cp_attention(q, k, v, group, batch_rows: int, scale: float | None = None, ranges=None):

@@ -104,6 +104,9 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     g.add_argument("--max-steps", default=0, type=int, help="stop after this many optimizer steps (0 = no limit)")
     g.add_argument("--fault-inject-prob", default=0.0, type=float, help="raise on a step with this probability (elastic tests)")
     g.add_argument("--wandb", default="auto", choices=["auto", "off"])
+    g.add_argument("--wandb-mode", default="rank0", choices=["rank0", "local_rank0", "every_rank"],
+                   help="wandb run layout: one run from rank 0; one per node grouped by experiment; one per rank "
+                        "grouped (related-topics/wandb-configurations)")
     g.add_argument("--determinism", default="off", choices=["on", "off"])
     g.add_argument("--init-from", default=None, help="HF safetensors directory to load pretrained weights from")
     g.add_argument("--tunableop", default="use", choices=["off", "use", "tune"])

@@ -33,7 +33,7 @@ from ..parallel.checkpointing import apply_activation_checkpointing
 from ..parallel.data_parallel import DataParallel, FlatAdamW
 from ..utils import comm as ucomm
 from ..utils import dist as udist
-from ..utils.metrics import MI355X_BF16_DENSE_FLOPS, MetricSink, get_mem_stats
+from ..utils.metrics import MI355X_BF16_DENSE_FLOPS, MetricSink, get_mem_stats, wandb_init_kwargs
 from ..utils.timers import make_timers
 from .checkpoint import CheckpointManager, has_checkpoint, new_state, recover_checkpoint
 from .cli import get_parser
@@ -280,10 +280,10 @@ def run(chapter: str, argv=None):
         resumed = True
     LOGGER.info(f"Resumed={resumed} | {state}")
     udist.make_exp_dir(exp_dir, per_rank_dirs=chapter in ("04", "deepspeed"))
-    sink = MetricSink(exp_dir, rank, use_wandb=args.wandb != "off", wandb_kwargs=dict(
-        project="distributed-training-guide", dir=str(exp_dir), name=args.experiment_name, id=args.experiment_name,
-        resume="must" if resumed else None, config={"args": vars(args), "training_data_size": len(train_data),
-                                                     "num_batches": len(dataloader), "world_size": world}))
+    wb_kw = wandb_init_kwargs(getattr(args, "wandb_mode", "rank0"), exp_dir, args.experiment_name, rank, local_rank,
+                              resumed, config={"args": vars(args), "training_data_size": len(train_data),
+                                               "num_batches": len(dataloader), "world_size": world})
+    sink = MetricSink(exp_dir, rank, use_wandb=args.wandb != "off", wandb_kwargs=wb_kw)
 
     waiting = getattr(args, "waiting_timers", "off") == "on" and world > 1
     names = ("data", "forward", "backward", "update") + (("waiting",) if waiting else ())

@@ -126,6 +126,21 @@ def all_to_all_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
     return out
 
 
+def all_gather_stack_async(x: torch.Tensor, group=None):
+    """(out [n, *x.shape], work): every rank's x stacked rank-major, issued asynchronously on
+    RCCL (work.wait() orders the current stream behind it); gloo runs it synchronously."""
+    n = world(group)
+    out = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    if n == 1:
+        out[0].copy_(x)
+        return out, _DoneWork()
+    x = x.contiguous()
+    if backend_of(group) == "gloo":
+        dist.all_gather(list(out.unbind(0)), x, group=group)
+        return out, _DoneWork()
+    return out, dist.all_gather_into_tensor(out, x, group=group, async_op=True)
+
+
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group=None, async_op=False):
     """Flat all-gather: out.numel() == shard.numel() * world."""
     return dist.all_gather_into_tensor(out, shard, group=group, async_op=async_op)

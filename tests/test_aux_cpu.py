@@ -143,3 +143,62 @@ def test_collectives_bench_gloo_rehearsal():
     for x in recs:
         factor = 1.0 if x["op"] == "all_reduce" else 0.5  # 2(n-1)/n and (n-1)/n at n = 2
         assert x["busbw_GBps"] == pytest.approx(x["algbw_GBps"] * factor, rel=0.02, abs=0.02)
+
+
+@pytest.mark.parametrize("mode", ["rank0", "local_rank0", "every_rank"])
+def test_wandb_init_kwargs_per_mode(tmp_path, mode):
+    """The reference's three wandb layouts (related-topics/wandb-configurations): which ranks log,
+    and the id / name / group / dir / save_code / resume of their runs.  4 ranks, 2 per node."""
+    from dtg.utils.metrics import wandb_init_kwargs
+
+    got = {r: wandb_init_kwargs(mode, tmp_path, "exp", r, r % 2, resumed=(r == 1), config={"a": 1}) for r in range(4)}
+    logging_ranks = [r for r, kw in got.items() if kw is not None]
+    assert logging_ranks == {"rank0": [0], "local_rank0": [0, 2], "every_rank": [0, 1, 2, 3]}[mode]
+    for r in logging_ranks:
+        kw = got[r]
+        assert kw["project"] == "distributed-training-guide" and kw["save_code"] is True and kw["config"] == {"a": 1}
+        assert kw["resume"] == ("must" if r == 1 else None)
+        if mode == "rank0":
+            assert (kw["id"], kw["name"], kw["dir"]) == ("exp", "exp", str(tmp_path)) and "group" not in kw
+        else:
+            assert (kw["id"], kw["name"], kw["group"]) == (f"exp-{r}", f"rank-{r}", "exp")
+            assert kw["dir"] == str(tmp_path / f"rank-{r}") and (tmp_path / f"rank-{r}").is_dir()
+
+
+def test_trainer_wandb_every_rank_with_stub_module(tmp_path):
+    """Chapter 02 on 2 gloo ranks with a stub `wandb` module on the path: every rank opens its own
+    grouped run with the reference's kwargs and logs its metric records to it."""
+    import subprocess
+    import sys
+
+    from _dist import free_port
+
+    stub = tmp_path / "stub"
+    stub.mkdir()
+    (stub / "wandb.py").write_text(
+        "import json, os\n"
+        "_out = os.environ['WANDB_STUB_OUT']\n"
+        "def init(**kw):\n"
+        "    global _id\n"
+        "    _id = kw['id']\n"
+        "    kw = {k: v for k, v in kw.items() if k != 'config'}\n"
+        "    json.dump(kw, open(os.path.join(_out, 'init-' + _id + '.json'), 'w'))\n"
+        "def log(info, step=None):\n"
+        "    open(os.path.join(_out, 'log-' + _id + '.txt'), 'a').write(str(step) + '\\n')\n")
+    out = tmp_path / "out"
+    out.mkdir()
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=f"{stub}:{os.environ.get('PYTHONPATH', '')}",
+               WANDB_STUB_OUT=str(out))
+    env.pop("DTG_NO_WANDB", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "02-distributed-data-parallel", "train_llm.py"),
+           "-e", "wb", "-m", "llama-tiny", "-d", "synthetic", "-b", "2", "-s", "64", "--max-steps", "2",
+           "--log-freq", "1", "--save-dir", str(tmp_path / "runs"), "--wandb-mode", "every_rank"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for rank in (0, 1):
+        kw = json.loads((out / f"init-wb-{rank}.json").read_text())
+        assert (kw["group"], kw["name"], kw["save_code"]) == ("wb", f"rank-{rank}", True)
+        assert kw["dir"].endswith(f"wb/rank-{rank}")
+        assert (out / f"log-wb-{rank}.txt").read_text().split() == ["1", "2"]
