@@ -198,6 +198,17 @@ class _TPGeom:
             lo += sz
         return out
 
+    def full_shape(self, kind, local_shape):
+        """The parameter's real (un-tensor-parallel) shape."""
+        sh = list(local_shape)
+        if self.size == 1 or kind == "rep":
+            return sh
+        if kind == "col":
+            sh[1] *= self.size
+        else:
+            sh[0] *= self.size
+        return sh
+
     def global_shape(self, kind, local_shape):
         R, C = (local_shape[0], int(np.prod(local_shape[1:]))) if len(local_shape) > 1 else (1, local_shape[0])
         if self.size == 1 or kind == "rep":
@@ -301,24 +312,23 @@ def snapshot_sharded(engine, global_step=None):
     else:
         gathered = [entry]
     meta = None
+    kind_of = lambda n: param_kind(n) if geo.size > 1 else "rep"
+    mine = {gname(n): (geo.global_shape(kind_of(n), sh), geo.full_shape(kind_of(n), sh)) for n, sh in shapes_local.items()}
     if rank == 0:
         files = [f for f in gathered if f["index"]]
-        gshapes = {}  # from every rank: a pipeline stage knows only its own layers
+        shapes = {}  # from every rank: a pipeline stage knows only its own layers
         if dist.is_initialized() and world > 1:
-            mine = {gname(n): geo.global_shape(param_kind(n) if geo.size > 1 else "rep", sh)
-                    for n, sh in shapes_local.items()}
             allshapes = [None] * world
             dist.gather_object(mine, allshapes, dst=0)
             for d in allshapes:
-                gshapes.update(d)
+                shapes.update(d)
         else:
-            gshapes = {gname(n): geo.global_shape(param_kind(n) if geo.size > 1 else "rep", sh)
-                       for n, sh in shapes_local.items()}
+            shapes = mine
         meta = {"format": FORMAT, "world_size": world, "tp_size": geo.size, "step": int(engine.step_count),
-                "global_step": global_step, "param_shapes_global": gshapes, "files": files}
+                "global_step": global_step, "param_shapes_global": {n: v[0] for n, v in shapes.items()},
+                "param_shapes_full": {n: v[1] for n, v in shapes.items()}, "files": files}
     elif dist.is_initialized() and world > 1:
-        dist.gather_object({gname(n): geo.global_shape(param_kind(n) if geo.size > 1 else "rep", sh)
-                            for n, sh in shapes_local.items()}, None, dst=0)
+        dist.gather_object(mine, None, dst=0)
     return tensors, entry, meta
 
 
@@ -417,6 +427,88 @@ def load_sharded(ckpt_dir, engine, load_optimizer: bool = True):
     if sync is not None:
         sync()
     barrier()
+    return meta
+
+
+# ------------------------------------------------------------------------------ export / import
+def _stored_rects(meta):
+    stored, seen = {}, set()
+    for f in meta["files"]:
+        for k, (name, n, rects) in enumerate(f["index"]):
+            for rc in rects:
+                key = (name, tuple(rc[:4]))
+                if key not in seen:
+                    seen.add(key)
+                    stored.setdefault(name, []).append((f["file"], k, rc))
+    return stored
+
+
+def iter_full_params(ckpt_dir, what=("p",)):
+    """Yield (name, {"p": param[, "m": exp_avg, "v": exp_avg_sq]}) of a dtg-sharded-v2
+    checkpoint, one parameter at a time in its real (un-sharded, un-tensor-parallel) shape,
+    assembled on the host from the memory-mapped shard files -- peak memory is one parameter,
+    not the model.  Raises if any element of a parameter is not stored."""
+    ckpt_dir = Path(ckpt_dir)
+    meta = read_index(ckpt_dir)
+    stored = _stored_rects(meta)
+    files = {}
+
+    def get(fname):
+        if fname not in files:
+            files[fname] = torch.load(ckpt_dir / fname, weights_only=True, mmap=True)
+        return files[fname]
+
+    full_shapes = meta.get("param_shapes_full", {})
+    for name, (R, C) in meta["param_shapes_global"].items():
+        outs, covered = {}, 0
+        for fname, k, (r0, nr, c0, nc, off) in stored.get(name, []):
+            t = get(fname)
+            for key in what:
+                src = t[f"{key}{k}"]
+                if key not in outs:
+                    outs[key] = torch.empty((R, C), dtype=src.dtype)
+                outs[key][r0:r0 + nr, c0:c0 + nc].copy_(src[off:off + nr * nc].view(nr, nc))
+            covered += nr * nc
+        if covered != R * C:
+            raise RuntimeError(f"{ckpt_dir}: parameter {name!r} is only {covered} of {R * C} elements covered")
+        shape = full_shapes.get(name) or ([C] if R == 1 else [R, C])  # pre-`param_shapes_full` indexes
+        yield name, {key: v.view(*shape) for key, v in outs.items()}
+
+
+def consolidate_sharded(ckpt_dir, with_optimizer: bool = False):
+    """Full host state dict {name: param} (and, with_optimizer, {name: (exp_avg, exp_avg_sq)})."""
+    what = ("p", "m", "v") if with_optimizer else ("p",)
+    params, moments = {}, {}
+    for name, d in iter_full_params(ckpt_dir, what):
+        params[name] = d["p"]
+        if with_optimizer:
+            moments[name] = (d["m"], d["v"])
+    return (params, moments) if with_optimizer else params
+
+
+def write_single_shard(ckpt_dir, params: dict, moments: dict = None, step: int = 0, global_step=None):
+    """Write full parameters (real shapes, this framework's names) as a one-shard
+    dtg-sharded-v2 checkpoint: world 1, no TP.  `load_sharded` reshards it onto any
+    (data-parallel x tensor-parallel) layout, so this is the import path for weights trained
+    elsewhere (HF safetensors -> hf_compat -> here).  Missing moments are written as zeros."""
+    ckpt_dir = Path(ckpt_dir)
+    ckpt_dir.mkdir(parents=True, exist_ok=True)
+    tensors, index, gsh, fsh = {}, [], {}, {}
+    for k, (name, p) in enumerate(params.items()):
+        p = p.detach().contiguous()
+        R, C = (p.shape[0], int(np.prod(p.shape[1:]))) if p.dim() > 1 else (1, p.shape[0])
+        m, v = (moments or {}).get(name, (None, None))
+        tensors[f"p{k}"] = p.reshape(-1).cpu()
+        tensors[f"m{k}"] = (m.reshape(-1).to(p.dtype) if m is not None else torch.zeros(p.numel(), dtype=p.dtype)).cpu()
+        tensors[f"v{k}"] = (v.reshape(-1).to(p.dtype) if v is not None else torch.zeros(p.numel(), dtype=p.dtype)).cpu()
+        index.append([name, int(p.numel()), [[0, R, 0, C, 0]]])
+        gsh[name], fsh[name] = [R, C], list(p.shape)
+    torch.save(tensors, ckpt_dir / _shard_file(0))
+    meta = {"format": FORMAT, "world_size": 1, "tp_size": 1, "step": int(step), "global_step": global_step,
+            "param_shapes_global": gsh, "param_shapes_full": fsh,
+            "files": [{"file": _shard_file(0), "rank": 0, "tp_rank": 0, "index": index}]}
+    with open(ckpt_dir / INDEX, "w") as fp:
+        json.dump(meta, fp)
     return meta
 
 

@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""Get a trained model out of (or into) this framework's sharded checkpoints.
+
+A `dtg-sharded-v2` checkpoint (`{exp_dir}/checkpoint/`: index.json + shard_rNNNNN.pt, written
+by FSDP / ZeRO / TP / 2-D / PP runs on any world size) is consolidated on ONE CPU process, one
+parameter at a time from the memory-mapped shards (peak host memory: one parameter plus one
+output file), into
+
+  * model.pt           this framework's full state dict (what chapter 01's `model.pt` holds; load
+                       it with `model.load_state_dict` or `--init-from`-style tooling), and/or
+  * HF safetensors     model-0000k-of-0000n.safetensors + model.safetensors.index.json +
+                       config.json, via `dtg.models.hf_compat` (fused qkv / gate_up split back into
+                       q/k/v and gate/up), loadable by `transformers.AutoModelForCausalLM`;
+  * --with-optimizer   the AdamW moments as exp_avg.pt / exp_avg_sq.pt (full shapes).
+
+The reverse direction, `import`, turns HF safetensors (or a model.pt) into a one-shard
+dtg-sharded-v2 checkpoint; the sharded loader reshards it onto any (data-parallel x tensor-
+parallel) layout on resume.
+
+    python tools/ckpt_export.py export outputs/llama-fsdp/checkpoint --model llama-3-8b --out export/ --format both
+    python tools/ckpt_export.py import /weights/Meta-Llama-3-8B --model llama-3-8b --out outputs/ft/checkpoint
+
+Reference: the reference converts DCP checkpoints with torch's format utilities
+(/root/reference/04-fully-sharded-data-parallel/README.md:244-248); this is the equivalent for
+this framework's own format.
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import json
+import os
+import sys
+from pathlib import Path
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import dtg  # noqa: E402,F401
+from dtg.models import resolve_config  # noqa: E402
+from dtg.models.config import LlamaConfig  # noqa: E402
+from dtg.train.checkpoint import iter_full_params, read_index, write_single_shard  # noqa: E402
+
+
+def _hf_items(name, t, cfg):
+    """This framework's (name, tensor) -> HF (name, tensor) pairs (one parameter at a time)."""
+    from dtg.models.hf_compat import llama_to_hf
+
+    if not isinstance(cfg, LlamaConfig):
+        raise SystemExit("HF export supports the Llama family (llama / qwen2 / mistral) configs")
+    untied = dataclasses.replace(cfg, tie_word_embeddings=False)
+    return list(llama_to_hf({name: t}, untied).items())
+
+
+def export(ckpt_dir, out, model=None, fmt="both", with_optimizer=False, max_shard_gb=5.0, dtype=None):
+    out = Path(out)
+    out.mkdir(parents=True, exist_ok=True)
+    meta = read_index(ckpt_dir)
+    cfg = resolve_config(model) if model else None
+    if fmt in ("hf", "both") and cfg is None:
+        raise SystemExit("--model is needed for the HF export (the config names the fused splits)")
+    what = ("p", "m", "v") if with_optimizer else ("p",)
+    cast = (lambda t: t.to(dtype)) if dtype is not None else (lambda t: t)
+    model_sd, m_sd, v_sd = {}, {}, {}
+    hf_files, hf_cur, hf_bytes, weight_map = [], {}, 0, {}
+    limit = int(max_shard_gb * (1 << 30))
+
+    def flush():
+        nonlocal hf_cur, hf_bytes
+        if hf_cur:
+            from safetensors.torch import save_file
+
+            fname = f"model-{len(hf_files) + 1:05d}.safetensors"
+            save_file({k: v.contiguous() for k, v in hf_cur.items()}, str(out / fname), metadata={"format": "pt"})
+            hf_files.append((fname, list(hf_cur)))
+            hf_cur, hf_bytes = {}, 0
+
+    for name, d in iter_full_params(ckpt_dir, what):
+        p = cast(d["p"])
+        if fmt in ("pt", "both"):
+            model_sd[name] = p
+        if with_optimizer:
+            m_sd[name], v_sd[name] = d["m"], d["v"]
+        if fmt in ("hf", "both"):
+            for hn, ht in _hf_items(name, p, cfg):
+                if hn == "lm_head.weight" and cfg.tie_word_embeddings:
+                    continue
+                nb = ht.numel() * ht.element_size()
+                if hf_bytes and hf_bytes + nb > limit:
+                    flush()
+                hf_cur[hn] = ht.clone()
+                hf_bytes += nb
+    if fmt in ("hf", "both"):
+        flush()
+        n = len(hf_files)
+        total = 0
+        for i, (fname, keys) in enumerate(hf_files):
+            new = f"model-{i + 1:05d}-of-{n:05d}.safetensors"
+            os.replace(out / fname, out / new)
+            for k in keys:
+                weight_map[k] = new
+        for f in out.glob("model-*-of-*.safetensors"):
+            total += f.stat().st_size
+        with open(out / "model.safetensors.index.json", "w") as fp:
+            json.dump({"metadata": {"total_size": total}, "weight_map": weight_map}, fp, indent=1)
+        from dtg.models.hf_compat import hf_llama_config
+
+        hf_llama_config(cfg).to_json_file(str(out / "config.json"))
+    if fmt in ("pt", "both"):
+        torch.save(model_sd, out / "model.pt")
+    if with_optimizer:
+        torch.save(m_sd, out / "exp_avg.pt")
+        torch.save(v_sd, out / "exp_avg_sq.pt")
+    summary = {"source": str(ckpt_dir), "world_size": meta["world_size"], "tp_size": meta["tp_size"],
+               "step": meta["step"], "global_step": meta.get("global_step"), "params": len(meta["param_shapes_global"]),
+               "hf_files": len(hf_files)}
+    with open(out / "export.json", "w") as fp:
+        json.dump(summary, fp, indent=1)
+    return summary
+
+
+def import_(src, out, model, step=0):
+    """HF safetensors directory / file, or a model.pt of this framework -> one-shard checkpoint."""
+    from dtg.models.hf_compat import llama_from_hf
+
+    src = Path(src)
+    cfg = resolve_config(model)
+    if src.suffix == ".pt":
+        sd = torch.load(src, map_location="cpu", weights_only=True)
+    else:
+        from safetensors.torch import load_file
+
+        files = sorted(src.glob("*.safetensors")) if src.is_dir() else [src]
+        hf = {}
+        for f in files:
+            hf.update(load_file(str(f)))
+        if cfg.tie_word_embeddings:
+            hf.pop("lm_head.weight", None)
+        sd = llama_from_hf(hf, cfg)
+    return write_single_shard(out, sd, step=step)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    e = sub.add_parser("export")
+    e.add_argument("ckpt_dir", help="a dtg-sharded-v2 checkpoint/ directory")
+    e.add_argument("--out", required=True)
+    e.add_argument("--model", default=None, help="bundled config name or HF config dir (needed for --format hf)")
+    e.add_argument("--format", default="both", choices=["pt", "hf", "both"])
+    e.add_argument("--with-optimizer", action="store_true")
+    e.add_argument("--max-shard-gb", type=float, default=5.0)
+    e.add_argument("--dtype", default=None, choices=[None, "bf16", "fp32"])
+    i = sub.add_parser("import")
+    i.add_argument("src", help="HF safetensors dir/file, or a model.pt")
+    i.add_argument("--model", required=True)
+    i.add_argument("--out", required=True, help="checkpoint/ directory to create")
+    a = ap.parse_args(argv)
+    if a.cmd == "export":
+        dt = {"bf16": torch.bfloat16, "fp32": torch.float32}.get(a.dtype)
+        print(json.dumps(export(a.ckpt_dir, a.out, a.model, a.format, a.with_optimizer, a.max_shard_gb, dt)))
+    else:
+        meta = import_(a.src, a.out, a.model)
+        print(json.dumps({"out": a.out, "params": len(meta["param_shapes_global"])}))
+
+
+if __name__ == "__main__":
+    main()
