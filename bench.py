@@ -264,7 +264,7 @@ def collective_sweep(args, torch, dist, device, world, cuda):
             _sync(dist, world, cuda)
             dt = (time.perf_counter() - t0) / iters
             out.append({"op": op, "mib": mib, "us": round(dt * 1e6, 1),
-                        "busbw_gbs": round((n * esz) / dt / 1e9 * factor, 1)})
+                        "busbw_gbs": round((n * esz) / dt / 1e9 * factor, 4)})
         del x, shard, full
     return out
 

@@ -195,6 +195,155 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   DTG_LAUNCH_CHECK();
 }
 
-TORCH_LIBRARY_IMPL(dtg, CUDA, m) { m.impl("adamw_", &adamw_); }
+// ------------------------------------------------------------------------------------------
+// AdamW that also refreshes the transposed copy of every weight matrix (single / DDP engines).
+//
+// hipBLASLt's backward dX = dY W runs at TN speed only with W^T (K-contiguous); weights change
+// once per step, so instead of transposing every weight in every backward (one read + one write
+// of W per step), this kernel writes W^T while the updated W is still in registers: the read is
+// saved, the write moves here.  The flat buffer is described as a list of matrices (2-D params;
+// 1-D params as [1, n] rows with no transposed copy); the grid walks 64 x 64 tiles of all of
+// them: phase 1 updates the tile row-wise with 16-byte vectors and parks the new bf16 values in
+// LDS, phase 2 writes the tile's columns as rows of W^T (16-byte vectors again).
+// ------------------------------------------------------------------------------------------
+struct MatDesc {
+  int64_t off, rows, cols, toff, tile0;  // toff < 0: no transposed copy
+};
+
+constexpr int kAtTile = 64;
+constexpr int kAtPitch = kAtTile + 2;  // halfwords; odd dword pitch spreads the column gathers
+
+template <typename ST, bool MASTER>
+__global__ __launch_bounds__(256) void adamw_t_kernel(uint16_t* __restrict__ p, float* __restrict__ master,
+                                                      const uint16_t* __restrict__ g, ST* __restrict__ m,
+                                                      ST* __restrict__ v, uint16_t* __restrict__ pt,
+                                                      const MatDesc* __restrict__ mats, int nmats, int64_t ntiles,
+                                                      AdamHyper h, const float* __restrict__ dev_hyper) {
+  __shared__ uint16_t tile[kAtTile * kAtPitch];
+  if (dev_hyper != nullptr) {
+    h.lr = dev_hyper[0];
+    h.bc1 = dev_hyper[1];
+    h.bc2_sqrt = dev_hyper[2];
+  }
+  const float step_size = h.lr / h.bc1;
+  const float decay = 1.f - h.lr * h.wd;
+  const int tid = threadIdx.x;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    int lo = 0, hi = nmats - 1;  // last matrix whose first tile is <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (mats[mid].tile0 <= t) lo = mid; else hi = mid - 1;
+    }
+    const MatDesc md = mats[lo];
+    const int64_t lt = t - md.tile0;
+    const int64_t ntc = (md.cols + kAtTile - 1) / kAtTile;
+    const int64_t r0 = (lt / ntc) * kAtTile, c0 = (lt % ntc) * kAtTile;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // 512 16-byte vectors per tile
+      const int id = tid + 256 * i;
+      const int lr = id >> 3, lc = (id & 7) * 8;
+      const int64_t r = r0 + lr, c = c0 + lc;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(tile + lr * kAtPitch + lc);
+      if (r < md.rows && c < md.cols) {
+        const int64_t k = md.off + r * md.cols + c;
+        float pv[8], gv[8], mv[8], vv[8];
+        if (MASTER) ld8<float>(master + k, pv); else load8(p + k, pv);
+        load8(g + k, gv);
+        ld8<ST>(m + k, mv);
+        ld8<ST>(v + k, vv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) adam_elem(pv[j], gv[j] * h.grad_scale, mv[j], vv[j], h, step_size, decay);
+        st8<ST>(m + k, mv);
+        st8<ST>(v + k, vv);
+        if (MASTER) st8<float>(master + k, pv);
+        u16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = f2bf(pv[j]);
+        *reinterpret_cast<u16x8*>(p + k) = pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[j] = (uint32_t)pb[2 * j] | ((uint32_t)pb[2 * j + 1] << 16);
+      }
+    }
+    if (md.toff >= 0) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int id = tid + 256 * i;
+        const int oc = id >> 3, orr = (id & 7) * 8;  // input column -> output row; first input row
+        const int64_t c = c0 + oc, r = r0 + orr;
+        if (c < md.cols && r < md.rows) {
+          u16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = tile[(orr + j) * kAtPitch + oc];
+          *reinterpret_cast<u16x8*>(pt + md.toff + c * md.rows + r) = o;
+        }
+      }
+    }
+    __syncthreads();  // the tile buffer is reused by this block's next tile
+  }
+}
+
+void adamw_t_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g, const at::Tensor& m,
+              const at::Tensor& v, const at::Tensor& pt, const at::Tensor& mats, int64_t ntiles, double lr,
+              double beta1, double beta2, double eps, double wd, int64_t step, double grad_scale,
+              const c10::optional<at::Tensor>& hyper) {
+  DTG_CHECK_CUDA_BF16(p);
+  DTG_CHECK_CUDA_BF16(pt);
+  DTG_CHECK(g.scalar_type() == at::kBFloat16, "adamw_t_: grads must be bf16");
+  DTG_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous() && pt.is_contiguous(),
+            "adamw_t_: buffers must be contiguous");
+  const int64_t n = p.numel();
+  DTG_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adamw_t_: size mismatch");
+  DTG_CHECK(m.scalar_type() == v.scalar_type(), "adamw_t_: exp_avg/exp_avg_sq dtype mismatch");
+  DTG_CHECK(step >= 1, "adamw_t_: step must be >= 1");
+  DTG_CHECK(mats.is_cuda() && mats.scalar_type() == at::kLong && mats.dim() == 2 && mats.size(1) == 5 &&
+                mats.is_contiguous(), "adamw_t_: mats must be int64 [n, 5] on the GPU");
+  auto aligned = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
+  DTG_CHECK(aligned(p) && aligned(g) && aligned(m) && aligned(v) && aligned(pt), "adamw_t_: 16-byte aligned buffers");
+  const bool has_master = master.has_value() && master->defined();
+  if (has_master)
+    DTG_CHECK(master->scalar_type() == at::kFloat && master->numel() == n && master->is_contiguous() &&
+              aligned(*master), "adamw_t_: master must be contiguous f32");
+  const float* hp = nullptr;
+  if (hyper.has_value() && hyper->defined()) {
+    DTG_CHECK(hyper->is_cuda() && hyper->scalar_type() == at::kFloat && hyper->numel() >= 3 && hyper->is_contiguous(),
+              "adamw_t_: hyper must be a contiguous f32 GPU tensor");
+    hp = hyper->data_ptr<float>();
+  }
+  const int nm = (int)mats.size(0);
+  if (nm == 0 || ntiles == 0) return;
+  const c10::DeviceGuard gd(p.device());
+  AdamHyper h;
+  h.lr = lr;
+  h.beta1 = beta1;
+  h.beta2 = beta2;
+  h.eps = eps;
+  h.wd = wd;
+  h.bc1 = 1.0 - std::pow(beta1, (double)step);
+  h.bc2_sqrt = std::sqrt(1.0 - std::pow(beta2, (double)step));
+  h.grad_scale = grad_scale;
+  const int blocks = (int)std::min<int64_t>(ntiles, 256 * 32);
+  float* mp = has_master ? master->data_ptr<float>() : nullptr;
+  const auto* md = reinterpret_cast<const MatDesc*>(mats.data_ptr<int64_t>());
+  const auto* gp = reinterpret_cast<const uint16_t*>(g.data_ptr());
+  uint16_t* ptp = bf16_mut(pt);
+#define DTG_ADAMT_LAUNCH(ST, MASTER)                                                                   \
+  adamw_t_kernel<ST, MASTER><<<blocks, 256, 0, stream()>>>(bf16_mut(p), mp, gp, reinterpret_cast<ST*>(m.data_ptr()), \
+                                                           reinterpret_cast<ST*>(v.data_ptr()), ptp, md, nm, ntiles, h, hp)
+  const bool sb = m.scalar_type() == at::kBFloat16;
+  DTG_CHECK(sb || m.scalar_type() == at::kFloat, "adamw_t_: states must be bf16 or f32");
+  if (has_master) {
+    if (sb) DTG_ADAMT_LAUNCH(uint16_t, true); else DTG_ADAMT_LAUNCH(float, true);
+  } else {
+    if (sb) DTG_ADAMT_LAUNCH(uint16_t, false); else DTG_ADAMT_LAUNCH(float, false);
+  }
+#undef DTG_ADAMT_LAUNCH
+  DTG_LAUNCH_CHECK();
+}
+
+TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
+  m.impl("adamw_", &adamw_);
+  m.impl("adamw_t_", &adamw_t_);
+}
 
 }  // namespace dtg

@@ -473,9 +473,33 @@ constexpr int kDqBK = 64;   // keys per K/V tile
 constexpr int kKvBK = 128;  // keys per workgroup (4 waves x 32)
 constexpr int kKvBQ = 32;   // query rows per item
 
+// delta[h, t] = rowsum(dO[t, h, :] * O[t, h, :]) in f32, for the concurrent backward (the dQ
+// and dK/dV kernels both read it, so neither has to run first).  A 256-thread block handles 16
+// consecutive tokens of one head: D/8 lanes per row, 16-byte loads, a D/8-lane shuffle sum and
+// one 64-byte store of the 16 results.
+template <int D>
+__global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ o,
+                                                        float* __restrict__ delta, int64_t T, int hq) {
+  constexpr int NCH = D / 8, ROWS = 256 / NCH;
+  const int head = blockIdx.y;
+  const int r = threadIdx.x / NCH, ch = threadIdx.x % NCH;
+  const int64_t t = (int64_t)blockIdx.x * ROWS + r;
+  float part = 0.f;
+  if (t < T) {
+    const int64_t base = (t * hq + head) * D + ch * 8;
+    const u16x8 a = *reinterpret_cast<const u16x8*>(dout + base);
+    const u16x8 b = *reinterpret_cast<const u16x8*>(o + base);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part += bf2f(a[j]) * bf2f(b[j]);
+  }
+#pragma unroll
+  for (int x = 1; x < NCH; x <<= 1) part += __shfl_xor(part, x, 64);
+  if (ch == 0 && t < T) delta[(int64_t)head * T + t] = part;
+}
+
 // dQ = scale * sum_keys dS K, query-stationary (the forward's structure).  Also writes
 // delta = rowsum(dO * O) for its rows, which bwd_dkdv_kernel (launched after it) reads.
-template <int D, bool CAUSAL, int OCC, bool WIN = false>
+template <int D, bool CAUSAL, int OCC, bool WIN = false, bool PRE_DELTA = false>
 __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int TILE = kDqBK * RB;
@@ -526,19 +550,21 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     const int64_t srow = (int64_t)(s0 + q0);
     sq.load(P.q + srow * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
     sdo.load(P.dout + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
-    so.load(P.o + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
+    if constexpr (!PRE_DELTA) so.load(P.o + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
     sk.load(kbase + (int64_t)t_begin * kDqBK * P.sk, P.sk, klen - t_begin * kDqBK);
     sv.load(vbase + (int64_t)t_begin * kDqBK * P.sv, P.sv, klen - t_begin * kDqBK);
-    constexpr int NCH = D / 8, RSTEP = 256 / NCH, PER = kDqBQ / RSTEP;
-    const int row0 = threadIdx.x / NCH, ch = threadIdx.x % NCH;
+    if constexpr (!PRE_DELTA) {
+      constexpr int NCH = D / 8, RSTEP = 256 / NCH, PER = kDqBQ / RSTEP;
+      const int row0 = threadIdx.x / NCH, ch = threadIdx.x % NCH;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      float part = 0.f;
+      for (int i = 0; i < PER; ++i) {
+        float part = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) part += bf2f(sdo.regs[i][j]) * bf2f(so.regs[i][j]);
+        for (int j = 0; j < 8; ++j) part += bf2f(sdo.regs[i][j]) * bf2f(so.regs[i][j]);
 #pragma unroll
-      for (int x = 1; x < NCH; x <<= 1) part += __shfl_xor(part, x, 64);  // the row's NCH lanes
-      if (ch == 0) rowd[row0 + i * RSTEP] = part;
+        for (int x = 1; x < NCH; x <<= 1) part += __shfl_xor(part, x, 64);  // the row's NCH lanes
+        if (ch == 0) rowd[row0 + i * RSTEP] = part;
+      }
     }
     sq.store(smem);
     sdo.store(smem + QIMG);
@@ -548,10 +574,13 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
       qf[c] = lds_frag(smem + 32 * w * RB + koff[c]);
       dof[c] = lds_frag(smem + QIMG + 32 * w * RB + koff[c]);
     }
-    delta = rowd[32 * w + r];
+    if constexpr (PRE_DELTA) delta = qok ? P.delta[(int64_t)head * P.T + s0 + qrow] : 0.f;
+    else delta = rowd[32 * w + r];
     __syncthreads();  // every wave holds its fragments before tile 0 overwrites the images
   }
-  if (qok && h == 0) P.delta[(int64_t)head * P.T + s0 + qrow] = delta;
+  if constexpr (!PRE_DELTA) {
+    if (qok && h == 0) P.delta[(int64_t)head * P.T + s0 + qrow] = delta;
+  }
   const float lse2 = qok ? P.lse[(int64_t)head * P.T + s0 + qrow] * kLog2e : 0.f;
 
   f32x16 acc[ND];
@@ -942,6 +971,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_fwd_stamped(const at::
   return {o, lse, st};
 }
 
+static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen, int64_t hq, int nseq,
+                          hipStream_t st, bool pre_delta);
+static void launch_bwd_dkdv(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
+                            int nseq, hipStream_t st);
+
 // Shared backward driver: outputs are [T, H, D] views (contiguous heads, any token stride).
 static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, const at::Tensor& k,
                                 const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
@@ -986,11 +1020,68 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   DTG_CHECK(window >= 0 && window < (1ll << 30), "flash_attn: window must be >= 0 (0 = full causal)");
   P.window = causal ? (int)window : 0;
   if (max_seqlen_k < 0) max_seqlen_k = max_seqlen;
-  // Waves per SIMD of the dq kernel at head_dim 128 (DTG_FA_OCC=1|2; measured in profiles/).
-  static const int occ = [] {
+  // Concurrent backward (DTG_FA_BWD_CONC=1, default; not for sliding windows): delta comes
+  // from its own small kernel, then the dQ kernel runs on a side stream WHILE the dK/dV kernel
+  // runs on the caller's stream.  Each alone keeps one wave per SIMD (256 VGPRs) with its MFMA
+  // pipe busy a quarter to a third of the time; co-resident on every CU (99 KB of LDS for the
+  // pair) one kernel's softmax / address work issues under the other's MFMAs.
+  static const bool conc = [] {
+    const char* e = std::getenv("DTG_FA_BWD_CONC");
+    return e == nullptr || e[0] != '0';
+  }();
+  const bool concurrent = conc && P.window == 0;
+  hipStream_t main_st = stream(), dq_st = main_st;
+  if (concurrent) {
+    dim3 dgrid((T + 256 / (D / 8) - 1) / (256 / (D / 8)), hq);
+    if (D == 128) fa::bwd_delta_kernel<128><<<dgrid, 256, 0, main_st>>>(bf16_ptr(dout), bf16_ptr(o), P.delta, T, (int)hq);
+    else fa::bwd_delta_kernel<64><<<dgrid, 256, 0, main_st>>>(bf16_ptr(dout), bf16_ptr(o), P.delta, T, (int)hq);
+    DTG_LAUNCH_CHECK();
+    static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    if (ev_fork == nullptr) {
+      DTG_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess, "flash_attn: event");
+      DTG_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess, "flash_attn: event");
+    }
+    dq_st = c10::hip::getStreamFromPool(false, q.device().index()).stream();
+    DTG_CHECK(hipEventRecord(ev_fork, main_st) == hipSuccess, "flash_attn: event record");
+    DTG_CHECK(hipStreamWaitEvent(dq_st, ev_fork, 0) == hipSuccess, "flash_attn: stream wait");
+    launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, dq_st, true);
+    launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, main_st);
+    DTG_CHECK(hipEventRecord(ev_join, dq_st) == hipSuccess, "flash_attn: event record");
+    DTG_CHECK(hipStreamWaitEvent(main_st, ev_join, 0) == hipSuccess, "flash_attn: stream wait");
+    return;
+  }
+  launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, main_st, false);
+  launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, main_st);
+}
+
+static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen, int64_t hq, int nseq,
+                          hipStream_t st, bool pre_delta) {
+  static const int occ = [] {  // waves per SIMD of the dq kernel at head_dim 128 (DTG_FA_OCC=1|2)
     const char* e = std::getenv("DTG_FA_OCC");
     return (e != nullptr && e[0] == '2') ? 2 : 1;
   }();
+  {
+    dim3 grid(hq, nseq, (max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ);
+    const size_t lds = 4 * fa::kDqBK * D * 2 + fa::kDqBQ * 4;  // + the per-row delta
+#define DTG_BWD_DQ(DD, C, O, ...)                                                         \
+  do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>, lds);         \
+       hipLaunchKernelGGL((fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>), grid, dim3(256), lds, st, P); } while (0)
+    if (P.window > 0) {  // sliding window (causal only)
+      if (D == 128) DTG_BWD_DQ(128, true, 1, true); else DTG_BWD_DQ(64, true, 2, true);
+    } else if (pre_delta) {
+      if (D == 128) { if (causal) DTG_BWD_DQ(128, true, 1, false, true); else DTG_BWD_DQ(128, false, 1, false, true); }
+      else { if (causal) DTG_BWD_DQ(64, true, 2, false, true); else DTG_BWD_DQ(64, false, 2, false, true); }
+    } else if (D == 128) {
+      if (occ == 2) { if (causal) DTG_BWD_DQ(128, true, 2); else DTG_BWD_DQ(128, false, 2); }
+      else { if (causal) DTG_BWD_DQ(128, true, 1); else DTG_BWD_DQ(128, false, 1); }
+    } else { if (causal) DTG_BWD_DQ(64, true, 2); else DTG_BWD_DQ(64, false, 2); }
+#undef DTG_BWD_DQ
+    DTG_LAUNCH_CHECK();
+  }
+}
+
+static void launch_bwd_dkdv(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
+                            int nseq, hipStream_t st) {
   // Items the dK/dV kernel stages ahead (DTG_FA_KV_PF=1|2).  Equal on MI355X once the kernel's
   // false vmcnt waits were gone (bwd 0.767 vs 0.768 ms at the 8B shape, profiles/r1_s51_*), so
   // the single-set form with fewer registers is the default.
@@ -999,26 +1090,11 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
     return (e != nullptr && e[0] == '2') ? 2 : 1;
   }();
   {
-    dim3 grid(hq, nseq, (max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ);
-    const size_t lds = 4 * fa::kDqBK * D * 2 + fa::kDqBQ * 4;  // + the per-row delta
-#define DTG_BWD_DQ(DD, C, O, ...)                                                         \
-  do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>, lds);         \
-       hipLaunchKernelGGL((fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>), grid, dim3(256), lds, stream(), P); } while (0)
-    if (P.window > 0) {  // sliding window (causal only)
-      if (D == 128) DTG_BWD_DQ(128, true, 1, true); else DTG_BWD_DQ(64, true, 2, true);
-    } else if (D == 128) {
-      if (occ == 2) { if (causal) DTG_BWD_DQ(128, true, 2); else DTG_BWD_DQ(128, false, 2); }
-      else { if (causal) DTG_BWD_DQ(128, true, 1); else DTG_BWD_DQ(128, false, 1); }
-    } else { if (causal) DTG_BWD_DQ(64, true, 2); else DTG_BWD_DQ(64, false, 2); }
-#undef DTG_BWD_DQ
-    DTG_LAUNCH_CHECK();
-  }
-  {
     dim3 grid(hkv, nseq, (max_seqlen_k + fa::kKvBK - 1) / fa::kKvBK);
     const size_t lds = 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
 #define DTG_BWD_KV(DD, C, PF, ...)                                                        \
   do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>, lds);      \
-       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>), grid, dim3(256), lds, stream(), P); } while (0)
+       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>), grid, dim3(256), lds, st, P); } while (0)
     if (P.window > 0) {  // sliding window (causal only)
       if (D == 128) DTG_BWD_KV(128, true, 1, true); else DTG_BWD_KV(64, true, 1, true);
     } else if (kv_pf == 2) {

@@ -109,6 +109,18 @@ def ce_grad_(logits, labels, lse, vocab_start, ignore_index, grad_scale):
     logits.copy_(g.to(logits.dtype))
 
 
+def adamw_t_(p, master, g, m, v, pt, mats, ntiles, lr, beta1, beta2, eps, wd, step, grad_scale, hyper=None):
+    """The HIP kernel's semantics: only the elements of the listed matrices are updated; each
+    matrix with a transposed slot gets its new values transposed into `pt`."""
+    for off, rows, cols, toff, _ in mats.tolist():
+        n = rows * cols
+        sl = slice(off, off + n)
+        adamw_(p[sl], None if master is None else master[sl], g[sl], m[sl], v[sl], lr, beta1, beta2, eps, wd,
+               step, grad_scale, hyper)
+        if toff >= 0:
+            pt[toff:toff + n].copy_(p[sl].view(rows, cols).t().reshape(-1))
+
+
 def adamw_(p, master, g, m, v, lr, beta1, beta2, eps, wd, step, grad_scale, hyper=None):
     bc1 = 1 - beta1**step
     bc2 = math.sqrt(1 - beta2**step)
@@ -279,7 +291,7 @@ def embedding_bwd_(out, ids, dy):
 for _name, _fn in list(globals().items()):
     if _name in (
         "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
-        "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "flash_attn_fwd", "flash_attn_bwd",
+        "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "adamw_t_", "flash_attn_fwd", "flash_attn_bwd",
         "flash_attn_bwd_qkv", "transpose2d", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
         "flash_attn_varlen_bwd",
     ):

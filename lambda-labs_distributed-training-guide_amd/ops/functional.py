@@ -38,6 +38,17 @@ def _tn_ok(*ts):
                and t.stride(1) == 1 for t in ts)
 
 
+def _wt(w):
+    """K-contiguous W^T for dX = dY W: the engine's persistent copy (refreshed by the optimizer
+    kernel, parallel/data_parallel.py) when it is current, else a transpose now."""
+    ref = getattr(w, "_dtg_wt", None)
+    if ref is not None:
+        t = ref[0].weight_t(ref[1])
+        if t is not None:
+            return t
+    return ops.transpose2d(w)
+
+
 def _bwd_layout(x, w):
     """(dx_tn, dw_tn) for this Linear's backward."""
     mode = _LINEAR_BWD
@@ -62,7 +73,7 @@ class _Linear(torch.autograd.Function):
         dx_tn, dw_tn = _bwd_layout(x, w)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy, ops.transpose2d(w).t()) if dx_tn else torch.mm(dy, w)
+            dx = torch.mm(dy, _wt(w).t()) if dx_tn else torch.mm(dy, w)
         if ctx.needs_input_grad[1]:
             if dw_tn and _tn_ok(dy):
                 dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
@@ -92,7 +103,7 @@ class _LinearBias(torch.autograd.Function):
         dx_tn, dw_tn = _bwd_layout(x, w)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy, ops.transpose2d(w).t()) if dx_tn else torch.mm(dy, w)
+            dx = torch.mm(dy, _wt(w).t()) if dx_tn else torch.mm(dy, w)
         if ctx.needs_input_grad[1]:
             if dw_tn and _tn_ok(dy):
                 dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
@@ -324,7 +335,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         dy = dy.contiguous()
         dx_tn, dw_tn = _bwd_layout(x, w_gu)
         fused = dw_tn and _tn_ok(dy, gu) and gu.stride(0) == gu.shape[1]
-        dh = torch.mm(dy, ops.transpose2d(w_down).t()) if dx_tn else torch.mm(dy, w_down)
+        dh = torch.mm(dy, _wt(w_down).t()) if dx_tn else torch.mm(dy, w_down)
         if fused:
             dgu, dgu_t, h_t = ops.swiglu_bwd_t(dh, gu)
             del dh
@@ -336,7 +347,7 @@ class _SwiGLUMLP(torch.autograd.Function):
             del dh
             dw_down = route_weight_grad_mm(w_down, dy, h)
             del h
-        dx = torch.mm(dgu, ops.transpose2d(w_gu).t()) if dx_tn else torch.mm(dgu, w_gu)
+        dx = torch.mm(dgu, _wt(w_gu).t()) if dx_tn else torch.mm(dgu, w_gu)
         if fused:
             dw_gu = route_weight_grad_mm(w_gu, dgu, x, a_t=dgu_t, b_t=ops.transpose2d(x))
         else:
@@ -421,7 +432,7 @@ class _FusedLinearCE(torch.autograd.Function):
             wp = torch.zeros((V + pad, w.shape[1]), dtype=w.dtype, device=w.device)
             wp[:V].copy_(w.detach())
         tn = need and _ce_tn(h, wp) and chunk % 8 == 0
-        w_t = ops.transpose2d(wp) if (tn and ctx.needs_input_grad[0]) else None
+        w_t = (_wt(w) if wp is w else ops.transpose2d(wp)) if (tn and ctx.needs_input_grad[0]) else None
         for s in range(0, T, chunk):
             e = min(T, s + chunk)
             lp = torch.mm(h[s:e], wp.t())
@@ -496,7 +507,7 @@ class _VocabParallelFusedLinearCE(torch.autograd.Function):
         direct = want_dw and _gr.direct_loss_grad() and getattr(w, "main_grad", None) is not None
         dw = torch.empty(w.shape, dtype=w.dtype, device=h.device) if (want_dw and not direct) else None
         tn = need and _ce_tn(h, w) and chunk % 8 == 0 and w.shape[0] % 8 == 0
-        w_t = ops.transpose2d(w) if (tn and ctx.needs_input_grad[0]) else None
+        w_t = _wt(w) if (tn and ctx.needs_input_grad[0]) else None
 
         def issue(s, e):
             logits = torch.mm(h[s:e], w.t())

@@ -11,6 +11,16 @@
                  not checkpointable) is strictly more traffic; this engine's state is
                  checkpointable (§2.11 #1).
 
+Transposed weights (single / DDP, bf16 on the GPU; `weight_t=True`): hipBLASLt runs the
+backward's dX = dY W at TN speed only with a K-contiguous W^T.  Weights change once per step,
+so the optimizer kernel (`adamw_t_`) writes W^T of every weight matrix while the updated values
+are in registers, into a persistent buffer the Linear backward reads (`ops.functional._wt`),
+instead of every backward transposing every weight (one read + one write of W per step: the
+read is saved, the write moves into the optimizer).  Staleness is impossible by construction:
+the copy is used only while the flat parameter buffer's version counter still equals the value
+recorded after the last refresh, so any other write to the weights (a checkpoint or pretrained
+load, a manual edit) makes the backward fall back to transposing until the next step.
+
 `overlap_optimizer=True` moves the AdamW update into backward: the moment a bucket's gradients
 are final (and, with DDP/ZeRO, its all-reduce / reduce-scatter has landed) its update runs on a
 side HIP stream while backward keeps the matrix cores busy with the remaining layers; under
@@ -42,7 +52,7 @@ class DataParallel:
                  bucket_mb: int = 256, broadcast_from_rank0: bool = True, state_dtype=torch.bfloat16,
                  master_weights: bool = False, overlap_param_gather: bool = True,
                  overlap_optimizer: bool = False, grad_divisor: Optional[int] = None,
-                 force_collectives: bool = False):
+                 force_collectives: bool = False, weight_t: Optional[bool] = None):
         assert mode in ("single", "ddp", "zero")
         self.module = model
         self.group = group
@@ -111,6 +121,77 @@ class DataParallel:
         # The engine owns the loss: backward(loss) uses an implicit gradient of 1 and any
         # scaling goes into AdamW's grad_scale, which lets the loss head write dW in place.
         set_direct_loss_grad(True)
+        # persistent W^T copies refreshed by the optimizer kernel (see the module docstring)
+        if weight_t is None:
+            import os
+
+            weight_t = os.environ.get("DTG_WEIGHT_T", "1") == "1" and dev.type == "cuda"
+        self._wt_buf = None
+        self._wt_version = -1
+        if (weight_t and self.mode in ("single", "ddp") and not overlap_optimizer
+                and self.space.dtype == torch.bfloat16 and self.space.grad_dtype == torch.bfloat16) or \
+                (weight_t and dev.type == "cpu" and self.mode in ("single", "ddp") and not overlap_optimizer):
+            self._build_weight_t()
+
+    # ------------------------------------------------------------------ transposed weights
+    def _build_weight_t(self):
+        import math
+
+        sp = self.space
+        rows_desc, slots, toff, tile0 = [], {}, 0, 0
+        for i in range(len(sp.names)):
+            shape, off = sp.shapes[i], sp.offsets[i]
+            n = math.prod(shape)
+            if n == 0:
+                continue
+            if len(shape) == 2 and shape[0] % 8 == 0 and shape[1] % 8 == 0 and min(shape) >= 64:
+                rows, cols, t = shape[0], shape[1], toff
+                slots[i] = (toff, rows, cols)
+                toff += n
+            else:  # updated as one row (within the flat buffer's 16-element padding), no W^T
+                rows, cols, t = 1, (n + 7) // 8 * 8, -1
+            rows_desc.append([off, rows, cols, t, tile0])
+            tile0 += -(-rows // 64) * -(-cols // 64)
+        if not slots:
+            return
+        dev = sp.param_buf.device
+        self._wt_mats = torch.tensor(rows_desc, dtype=torch.long, device=dev)
+        self._wt_tiles = tile0
+        self._wt_buf = torch.empty(toff, dtype=sp.dtype, device=dev)
+        self._wt_views = {}
+        for i, (o, rows, cols) in slots.items():
+            self._wt_views[i] = self._wt_buf[o:o + rows * cols].view(cols, rows)
+        index = {id(p): i for i, p in enumerate(self._space_params())}
+        for p in self.params:
+            i = index.get(id(p))
+            if i is not None and i in self._wt_views:
+                p._dtg_wt = (self, i)
+        self.refresh_weight_t()
+
+    def _space_params(self):
+        """Parameters in FlatSpace order (names -> this engine's rebound parameters)."""
+        by_name = {getattr(p, "_dtg_name", None): p for p in self.params}
+        return [by_name.get(n) for n in self.space.names]
+
+    @torch.no_grad()
+    def refresh_weight_t(self):
+        """Recompute every W^T from the current weights (init; any load)."""
+        if self._wt_buf is None:
+            return
+        from ..ops import functional as _F
+
+        ps = self._space_params()
+        for i, view in self._wt_views.items():
+            w = ps[i]
+            view.copy_(_F.ops.transpose2d(w) if w.is_cuda else w.t())
+        self._wt_version = self.space.param_buf._version
+
+    def weight_t(self, i):
+        """The current W^T of flat parameter i, or None if the weights changed since the last
+        refresh (the caller then transposes)."""
+        if self._wt_buf is None or self.space.param_buf._version != self._wt_version:
+            return None
+        return self._wt_views.get(i)
 
     # ------------------------------------------------------------------ grad sync
     @contextlib.contextmanager
@@ -253,6 +334,12 @@ class DataParallel:
                            eps=eps, weight_decay=weight_decay, grad_scale=grad_scale,
                            master=None if self.master is None else self.master[o:o + n], hyper=self.graph_hyper)
             self._allgather_params(wait=not self.overlap_param_gather)
+        elif self._wt_buf is not None:  # same update + every weight's W^T for the next backward
+            torch.ops.dtg.adamw_t_(self.space.param_buf, self.master, self.space.grad_buf, self.exp_avg,
+                                   self.exp_avg_sq, self._wt_buf, self._wt_mats, int(self._wt_tiles), float(lr),
+                                   float(beta1), float(beta2), float(eps), float(weight_decay), int(self.step_count),
+                                   float(grad_scale), self.graph_hyper)
+            self._wt_version = self.space.param_buf._version
         else:
             adamw_step(self.space.param_buf, self.space.grad_buf, self.exp_avg, self.exp_avg_sq, lr=lr,
                        step=self.step_count, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,

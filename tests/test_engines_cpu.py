@@ -116,3 +116,47 @@ def test_optimizer_in_backward_distributed(mode, accum):
     for r in range(2):
         for n in ref:
             torch.testing.assert_close(res[r][0][n], ref[n], atol=3e-4, rtol=1e-3, msg=f"rank {r} {n}")
+
+
+def test_weight_t_copies_refreshed_by_optimizer_match_plain_training(monkeypatch):
+    """Single-device engine with persistent W^T (written by the adamw_t_ optimizer kernel):
+    the same parameters after 3 steps as the plain engine, every copy equal to its weight's
+    transpose after each step, the backward reads the copies (no per-weight transposes), and a
+    weight edited outside the optimizer is never paired with its stale copy."""
+    import dtg.ops.functional as F_
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    batches = _batches(512, 2, 32, n=3)
+    res = {}
+    for wt in (False, True):
+        torch.manual_seed(0)
+        m = build_model("llama-tiny", device="cpu", dtype=torch.float32)
+        eng = DataParallel(m, mode="single", weight_t=wt)
+        opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
+        calls = []
+        real = F_.ops.transpose2d
+        monkeypatch.setattr(F_, "ops", type("O", (), {"__getattr__": lambda s, k: getattr(torch.ops.dtg, k),
+                                                      "transpose2d": staticmethod(lambda x: calls.append(x.shape) or real(x))})())
+        for ids in batches:
+            opt.zero_grad()
+            out = m(input_ids=ids, labels=ids)
+            eng.backward(out.loss)
+            opt.step()
+            if wt:
+                ps = eng._space_params()
+                for i, view in eng._wt_views.items():
+                    assert torch.equal(view, ps[i].detach().t()), eng.space.names[i]
+        monkeypatch.undo()
+        res[wt] = ({n: p.detach().clone() for n, p in m.named_parameters()}, len(calls))
+        if wt:
+            assert eng._wt_buf is not None and len(eng._wt_views) > 0
+            i = next(iter(eng._wt_views))
+            with torch.no_grad():
+                eng._space_params()[i].add_(1.0)  # an edit outside the optimizer
+            assert eng.weight_t(i) is None  # -> the backward transposes instead of using the copy
+    for n, v in res[False][0].items():
+        assert torch.equal(res[True][0][n], v), n
+    # the plain engine transposes every weight (and activations) per backward; with W^T only
+    # activations (tokens < 4096 here: the TN path is off on CPU, so both counts may be 0)
+    assert res[True][1] <= res[False][1]

@@ -216,6 +216,90 @@ def test_adamw(cuda, state_dtype, master, n):
         assert (tp.detach().float() - pm.float()).abs().max().item() <= 2 * 2**-7 * tp.detach().float().abs().max().item()
 
 
+@pytest.mark.parametrize("state_dtype,master", [(torch.bfloat16, False), (torch.float32, True)])
+def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master):
+    """adamw_t_ (update + W^T of every listed matrix, 64 x 64 LDS tiles, edge tiles, [1, n]
+    rows without a copy) == adamw_ on the same elements, bitwise; copies == W^T exactly;
+    elements outside the listed matrices untouched."""
+    torch.manual_seed(0)
+    shapes = [(192, 320), (1, 136), (72, 200), (1024, 64)]  # 72 x 200: partial edge tiles
+    offs, o = [], 0
+    for r, c in shapes:
+        offs.append(o)
+        o += (r * c + 15) // 16 * 16 + 16  # 16 gap elements that must stay untouched
+    n = o
+    p = torch.randn(n, device=cuda).bfloat16()
+    g = torch.randn(n, device=cuda).bfloat16()
+    m = (0.1 * torch.randn(n, device=cuda)).to(state_dtype)
+    v = (0.01 * torch.rand(n, device=cuda)).to(state_dtype)
+    mw = p.float() if master else None
+    ref = [t.clone() if t is not None else None for t in (p, g, m, v, mw)]
+    desc, toff, tile0 = [], 0, 0
+    for (r, c), off in zip(shapes, offs):
+        t = toff if r > 1 else -1
+        desc.append([off, r, c, t, tile0])
+        tile0 += -(-r // 64) * -(-c // 64)
+        if r > 1:
+            toff += r * c
+    pt = torch.zeros(toff, dtype=torch.bfloat16, device=cuda)
+    mats = torch.tensor(desc, dtype=torch.long, device=cuda)
+    for step in (1, 2):
+        dops.adamw_t_(p, mw, g, m, v, pt, mats, tile0, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, 0.5)
+        for (r, c), off in zip(shapes, offs):
+            sl = slice(off, off + r * c)
+            dops.adamw_(ref[0][sl], None if ref[4] is None else ref[4][sl], ref[1][sl], ref[2][sl], ref[3][sl],
+                        1e-3, 0.9, 0.999, 1e-8, 0.01, step, 0.5)
+    assert torch.equal(p, ref[0]) and torch.equal(m, ref[2]) and torch.equal(v, ref[3])
+    for (r, c), off, d in zip(shapes, offs, desc):
+        if d[3] >= 0:
+            assert torch.equal(pt[d[3]:d[3] + r * c].view(c, r), p[off:off + r * c].view(r, c).t())
+
+
+@pytest.mark.parametrize("engine_mode", ["single"])
+def test_engine_weight_t_bitwise_and_fewer_transposes(cuda, engine_mode, monkeypatch):
+    """Llama on the GPU with the TN backward (T = 4096 tokens): persistent W^T written by the
+    optimizer gives bitwise the same training as per-backward weight transposes, with 4 fewer
+    transpose launches per layer (+1 for the tied/untied loss-head weight)."""
+    import dtg.ops.functional as F_
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    cfg = resolve_config("llama-tiny-d128")
+    g = torch.Generator().manual_seed(0)
+    batches = [torch.randint(0, cfg.vocab_size, (4, 1024), generator=g).to(cuda) for _ in range(3)]
+    res = {}
+    for wt in (False, True):
+        torch.manual_seed(0)
+        m = build_model(cfg, device=cuda)
+        eng = DataParallel(m, mode=engine_mode, weight_t=wt)
+        opt = FlatAdamW(eng, lr=1e-3)
+        calls = [0]
+        real = torch.ops.dtg.transpose2d
+
+        class _Ops:
+            def __getattr__(self, k):
+                return getattr(torch.ops.dtg, k)
+
+            @staticmethod
+            def transpose2d(x):
+                calls[0] += 1
+                return real(x)
+
+        monkeypatch.setattr(F_, "ops", _Ops())
+        for ids in batches:
+            opt.zero_grad()
+            out = m(input_ids=ids, labels=ids)
+            eng.backward(out.loss)
+            opt.step()
+        monkeypatch.undo()
+        torch.cuda.synchronize()
+        res[wt] = ({n: p.detach().clone() for n, p in m.named_parameters()}, calls[0])
+    for n, v in res[False][0].items():
+        assert torch.equal(res[True][0][n], v), n
+    per_step = (res[False][1] - res[True][1]) / len(batches)
+    assert per_step == 4 * cfg.num_hidden_layers + 1, (res[False][1], res[True][1])
+
+
 def _attn_case(cuda, seqlens, hq, hkv, D, causal, stride_extra=0, qscale=1.0, window=0):
     torch.manual_seed(0)
     T = sum(seqlens)
