@@ -108,6 +108,9 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                    help="wandb run layout: one run from rank 0; one per node grouped by experiment; one per rank "
                         "grouped (related-topics/wandb-configurations)")
     g.add_argument("--determinism", default="off", choices=["on", "off"])
+    g.add_argument("--pin-numa", default="off", choices=["on", "off"],
+                   help="restrict each rank's CPU affinity to its GPU's NUMA node (host AdamW / D2H locality); "
+                        "the placement is logged at startup either way")
     g.add_argument("--init-from", default=None, help="HF safetensors directory to load pretrained weights from")
     g.add_argument("--tunableop", default="use", choices=["off", "use", "tune"])
     g.add_argument("--async-ckpt", default="off", choices=["on", "off"],

@@ -237,6 +237,8 @@ def run(chapter: str, argv=None):
     LOGGER.info(os.environ)
     LOGGER.info(args)
     LOGGER.info(f"local_rank={local_rank} rank={rank} world size={world}")
+    # host CPU share and NUMA placement of this rank (chapter 05's offload is host-bound)
+    LOGGER.info(f"host placement: {udist.host_placement(device, pin=getattr(args, 'pin_numa', 'off') == 'on')}")
     if args.tunableop != "off" and device.type == "cuda":
         from ..utils.gemm_tuning import enable_tunableop
 

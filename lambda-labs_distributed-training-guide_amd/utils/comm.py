@@ -135,6 +135,9 @@ def all_gather_stack_async(x: torch.Tensor, group=None):
         out[0].copy_(x)
         return out, _DoneWork()
     x = x.contiguous()
+    c = _xgmi_for(group, x, x.numel() * x.element_size())
+    if c is not None:  # direct-peer library on a side stream (latency-bound message)
+        return out, _on_side_stream(lambda: c.all_gather_into(out.view(-1), x.view(-1)), out, x)
     if backend_of(group) == "gloo":
         dist.all_gather(list(out.unbind(0)), x, group=group)
         return out, _DoneWork()

@@ -133,6 +133,64 @@ def make_exp_dir(exp_dir, per_rank_dirs: bool = False):
     return exp_dir
 
 
+def _parse_cpulist(text: str):
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        else:
+            cpus.add(int(part))
+    return cpus
+
+
+def host_placement(device, pin: bool = False) -> dict:
+    """Where this rank's host work runs relative to its GPU: the CPUs it may use
+    (`os.sched_getaffinity`), the GPU's NUMA node and that node's CPUs (sysfs, from the PCI bus
+    id), and OMP_NUM_THREADS.  Chapter 05's backward is bound by gradient D2H and the host AdamW
+    runs on these CPUs, so the numbers are logged at startup; `pin=True` restricts the process
+    to the GPU-local NUMA node's CPUs (within its current affinity) so pinned buffers, the DMA
+    engine and the optimizer threads share one memory controller."""
+    info = {"affinity_cpus": None, "gpu_numa_node": None, "numa_cpus": None, "omp_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        aff = os.sched_getaffinity(0)
+        info["affinity_cpus"] = len(aff)
+    except (AttributeError, OSError):
+        aff = None
+    if getattr(device, "type", "cpu") == "cuda":
+        try:
+            bus = torch.cuda.get_device_properties(device).pci_bus_id  # bus number, e.g. 93 = 0000:5d:..
+
+            def _is_gpu(d):  # display / processing-accelerator class on that bus
+                c = d / "class"
+                return c.exists() and c.read_text().strip()[:4] in ("0x03", "0x12")
+
+            dev_dirs = [d for d in Path("/sys/bus/pci/devices").iterdir()
+                        if int(d.name.split(":")[1], 16) == int(bus) and _is_gpu(d)]
+            for d in dev_dirs:
+                node_file = d / "numa_node"
+                if node_file.exists():
+                    node = int(node_file.read_text().strip())
+                    if node >= 0:
+                        info["gpu_numa_node"] = node
+                        cl = Path(f"/sys/devices/system/node/node{node}/cpulist")
+                        if cl.exists():
+                            cpus = _parse_cpulist(cl.read_text())
+                            info["numa_cpus"] = len(cpus)
+                            if aff is not None:
+                                info["affinity_cpus_on_gpu_node"] = len(cpus & aff)
+                                if pin and cpus & aff:
+                                    os.sched_setaffinity(0, cpus & aff)
+                                    info["pinned_to_gpu_node"] = True
+                                    info["affinity_cpus"] = len(cpus & aff)
+                    break
+        except Exception as e:  # informational only: never fail a run over sysfs layout
+            info["error"] = repr(e)[:120]
+    return info
+
+
 def setup_logging(rank: Optional[int] = None, with_rank: bool = True):
     """Reference log format: `[rank=R] [time] LEVEL:message` (B8)."""
     rank = get_rank() if rank is None else rank
