@@ -290,6 +290,20 @@ at::Tensor workspace(int64_t id) {
                        at::TensorOptions().dtype(at::kByte).device(c10::Device(c10::DeviceType::CUDA, c.device)));
 }
 
+// A fresh tensor (its own TensorImpl and version counter, not a view) over `sizes` elements of
+// `dtype` at byte `offset` of the own data region: a zero-copy producer output.  Autograd forbids
+// in-place changes to the base of a view a custom Function returned, and every hand-out of a
+// slot rewrites the same memory, so each hand-out must be a distinct base.
+at::Tensor workspace_view(int64_t id, int64_t offset, at::IntArrayRef sizes, at::ScalarType dtype) {
+  Comm& c = get(id);
+  int64_t n = 1;
+  for (auto v : sizes) n *= v;
+  const int64_t bytes = n * (int64_t)c10::elementSize(dtype);
+  TORCH_CHECK(offset >= 0 && offset % 16 == 0 && offset + bytes <= c.capacity, "xgmi: workspace_view out of range");
+  return at::from_blob(c.base + offset, sizes,
+                       at::TensorOptions().dtype(dtype).device(c10::Device(c10::DeviceType::CUDA, c.device)));
+}
+
 namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -510,6 +524,7 @@ TORCH_LIBRARY(dtg_xgmi, m) {
   m.def("error(int id) -> int", &error);
   m.def("destroy(int id) -> ()", &destroy);
   m.def("workspace(int id) -> Tensor", &workspace);
+  m.def("workspace_view(int id, int offset, int[] sizes, ScalarType dtype) -> Tensor", &workspace_view);
   m.def("all_gather(int id, Tensor(a!) out, Tensor inp, int offset=0) -> ()", &all_gather);
   m.def("all_gather_dma(int id, Tensor(a!) out, Tensor inp, int offset=0) -> ()", &all_gather_dma);
   m.def("reduce_scatter(int id, Tensor(a!) out, Tensor inp, int offset=0) -> ()", &reduce_scatter);

@@ -147,7 +147,7 @@ class DataParallel:
             if len(shape) == 2 and shape[0] % 8 == 0 and shape[1] % 8 == 0 and min(shape) >= 64:
                 rows, cols, t = shape[0], shape[1], toff
                 slots[i] = (toff, rows, cols)
-                toff += n
+                toff += (n + 127) // 128 * 128  # 256-byte aligned copies, like the allocator's
             else:  # updated as one row (within the flat buffer's 16-element padding), no W^T
                 rows, cols, t = 1, (n + 7) // 8 * 8, -1
             rows_desc.append([off, rows, cols, t, tile0])

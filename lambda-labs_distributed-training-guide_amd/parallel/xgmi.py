@@ -149,7 +149,8 @@ class XgmiCommunicator:
             self._slot_free[k] = None
         off = self.capacity - (2 - k) * slot
         self._slot_of[self._ws_ptr + off] = k
-        return self.ws[off:off + nbytes].view(dtype).view(*shape)
+        # a distinct base per hand-out (not a view of self.ws): see workspace_view in xgmi.hip
+        return torch.ops.dtg_xgmi.workspace_view(self.id, off, [int(x) for x in shape], dtype)
 
     def release_slot(self, t: torch.Tensor, event):
         """`event` completes once the reduce-scatter reading slot-resident `t` has closed."""
