@@ -53,6 +53,9 @@ __device__ __forceinline__ void st8<float>(float* p, const float* v) {
 
 __device__ __forceinline__ void adam_elem(float& pv, float gv, float& mv, float& vv, const AdamHyper& h,
                                           float step_size, float decay) {
+  // No FMA contraction: every kernel that inlines this (adamw_, adamw_t_) must round the same
+  // way, so the optimizer choice never changes a bit of the trained weights.
+#pragma clang fp contract(off)
   pv *= decay;
   mv = mv + (gv - mv) * (1.f - h.beta1);
   vv = vv * h.beta2 + (1.f - h.beta2) * gv * gv;
@@ -228,12 +231,17 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(uint16_t* __restrict__ p, 
   const float step_size = h.lr / h.bc1;
   const float decay = 1.f - h.lr * h.wd;
   const int tid = threadIdx.x;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    int lo = 0, hi = nmats - 1;  // last matrix whose first tile is <= t
+  int lo = 0;  // the matrix of tile t: tiles are walked in increasing order, so it only advances
+  {
+    int hi = nmats - 1;  // binary search for this block's first tile
+    const int64_t t0 = blockIdx.x;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (mats[mid].tile0 <= t) lo = mid; else hi = mid - 1;
+      if (mats[mid].tile0 <= t0) lo = mid; else hi = mid - 1;
     }
+  }
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    while (lo + 1 < nmats && mats[lo + 1].tile0 <= t) ++lo;
     const MatDesc md = mats[lo];
     const int64_t lt = t - md.tile0;
     const int64_t ntc = (md.cols + kAtTile - 1) / kAtTile;

@@ -1020,14 +1020,17 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   DTG_CHECK(window >= 0 && window < (1ll << 30), "flash_attn: window must be >= 0 (0 = full causal)");
   P.window = causal ? (int)window : 0;
   if (max_seqlen_k < 0) max_seqlen_k = max_seqlen;
-  // Concurrent backward (DTG_FA_BWD_CONC=1, default; not for sliding windows): delta comes
-  // from its own small kernel, then the dQ kernel runs on a side stream WHILE the dK/dV kernel
-  // runs on the caller's stream.  Each alone keeps one wave per SIMD (256 VGPRs) with its MFMA
-  // pipe busy a quarter to a third of the time; co-resident on every CU (99 KB of LDS for the
-  // pair) one kernel's softmax / address work issues under the other's MFMAs.
+  // Concurrent backward (DTG_FA_BWD_CONC=1; off by default): delta comes from its own small
+  // kernel, then the dQ kernel runs on a side stream WHILE the dK/dV kernel runs on the
+  // caller's stream, co-resident on every CU (99 KB of LDS for the pair).  The idea: each alone
+  // keeps one wave per SIMD with its MFMA pipe busy a quarter to a third of the time, so one
+  // kernel's softmax work could issue under the other's MFMAs.  Measured on MI355X
+  // (profiles/r3_s04): SLOWER -- 8B shape 0.737 -> 0.803 ms, rime 0.320 -> 0.342, 2 x 8192
+  // 4.22 -> 4.40 -- the pair contends for LDS bandwidth and L2 more than it gains in issue
+  // overlap; kept as an option, not the default.
   static const bool conc = [] {
     const char* e = std::getenv("DTG_FA_BWD_CONC");
-    return e == nullptr || e[0] != '0';
+    return e != nullptr && e[0] == '1';
   }();
   const bool concurrent = conc && P.window == 0;
   hipStream_t main_st = stream(), dq_st = main_st;
