@@ -38,44 +38,6 @@ def _tn_ok(*ts):
                and t.stride(1) == 1 for t in ts)
 
 
-# The K-contiguous activation copies of the weight-gradient GEMMs (dY^T, X^T) do not depend on
-# the input-gradient GEMM issued right before them, and they are pure HBM streaming work while
-# the GEMM is matrix-core bound: issue them on a side stream so they run in the GEMM's shadow
-# (co-resident workgroups, otherwise idle HBM bandwidth), and make the main stream wait only
-# right before the weight-gradient GEMM.  DTG_OVERLAP_T=0 restores the serial order.
-_OVERLAP_T = os.environ.get("DTG_OVERLAP_T", "1") == "1"
-_T_STREAMS = {}
-
-
-class _SideT:
-    """transpose2d of `xs` issued on a side stream; `.get()` joins and returns them."""
-
-    def __init__(self, *xs):
-        self.side = None
-        if not (_OVERLAP_T and xs[0].is_cuda and not torch.cuda.is_current_stream_capturing()):
-            self.out = [ops.transpose2d(x) for x in xs]
-            return
-        dev = xs[0].device
-        side = _T_STREAMS.get(dev.index)
-        if side is None:
-            side = _T_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
-        main = torch.cuda.current_stream(dev)
-        side.wait_stream(main)  # the inputs are written
-        with torch.cuda.stream(side):
-            self.out = [ops.transpose2d(x) for x in xs]
-        for x in xs:
-            x.record_stream(side)  # read on the side stream: not reused before that finishes
-        self.side, self.main = side, main
-
-    def get(self):
-        if self.side is not None:
-            self.main.wait_stream(self.side)
-            for o in self.out:
-                o.record_stream(self.main)
-            self.side = None
-        return self.out
-
-
 def _wt(w):
     """K-contiguous W^T for dX = dY W: the engine's persistent copy (refreshed by the optimizer
     kernel, parallel/data_parallel.py) when it is current, else a transpose now."""
@@ -110,14 +72,11 @@ class _Linear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx_tn, dw_tn = _bwd_layout(x, w)
         dx = dw = None
-        tn_w = ctx.needs_input_grad[1] and dw_tn and _tn_ok(dy)
-        side = _SideT(dy, x) if tn_w else None  # under the dX GEMM
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy, _wt(w).t()) if dx_tn else torch.mm(dy, w)
         if ctx.needs_input_grad[1]:
-            if tn_w:
-                dy_t, x_t = side.get()
-                dw = route_weight_grad_mm(w, dy, x, a_t=dy_t, b_t=x_t)
+            if dw_tn and _tn_ok(dy):
+                dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
             else:
                 dw = route_weight_grad_mm(w, dy, x)
         return dx, dw, None
@@ -143,14 +102,11 @@ class _LinearBias(torch.autograd.Function):
         x, w, b = ctx.saved_tensors
         dx_tn, dw_tn = _bwd_layout(x, w)
         dx = dw = db = None
-        tn_w = ctx.needs_input_grad[1] and dw_tn and _tn_ok(dy)
-        side = _SideT(dy, x) if tn_w else None  # under the dX GEMM
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy, _wt(w).t()) if dx_tn else torch.mm(dy, w)
         if ctx.needs_input_grad[1]:
-            if tn_w:
-                dy_t, x_t = side.get()
-                dw = route_weight_grad_mm(w, dy, x, a_t=dy_t, b_t=x_t)
+            if dw_tn and _tn_ok(dy):
+                dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
             else:
                 dw = route_weight_grad_mm(w, dy, x)
         if ctx.needs_input_grad[2]:
@@ -379,14 +335,12 @@ class _SwiGLUMLP(torch.autograd.Function):
         dy = dy.contiguous()
         dx_tn, dw_tn = _bwd_layout(x, w_gu)
         fused = dw_tn and _tn_ok(dy, gu) and gu.stride(0) == gu.shape[1]
-        side = _SideT(dy, x) if fused else None  # dY^T and X^T under the dH GEMM
         dh = torch.mm(dy, _wt(w_down).t()) if dx_tn else torch.mm(dy, w_down)
         if fused:
             dgu, dgu_t, h_t = ops.swiglu_bwd_t(dh, gu)
             del dh
-            dy_t, x_t = side.get()
-            dw_down = route_weight_grad_mm(w_down, dy, None, a_t=dy_t, b_t=h_t)
-            del h_t, dy_t
+            dw_down = route_weight_grad_mm(w_down, dy, None, a_t=ops.transpose2d(dy), b_t=h_t)
+            del h_t
         else:
             h = ops.swiglu_fwd(gu)
             dgu = ops.swiglu_bwd(dh, gu)
@@ -395,7 +349,7 @@ class _SwiGLUMLP(torch.autograd.Function):
             del h
         dx = torch.mm(dgu, _wt(w_gu).t()) if dx_tn else torch.mm(dgu, w_gu)
         if fused:
-            dw_gu = route_weight_grad_mm(w_gu, dgu, x, a_t=dgu_t, b_t=x_t)
+            dw_gu = route_weight_grad_mm(w_gu, dgu, x, a_t=dgu_t, b_t=ops.transpose2d(x))
         else:
             dw_gu = route_weight_grad_mm(w_gu, dgu, x)
         return dx, dw_gu, dw_down, None
@@ -486,12 +440,10 @@ class _FusedLinearCE(torch.autograd.Function):
             rows = ops.ce_fwd_bwd_(logits, labels[s:e], ignore_index, scale, need)
             loss_sum += rows.sum()
             if need:
-                side = _SideT(lp, h[s:e]) if (direct and tn) else None  # under the dh GEMM
                 _ce_dx(lp, wp, w_t, dh[s:e])
                 if direct and tn:
-                    lp_t, h_t = side.get()
-                    _gr.accumulate_mm_into_main_grad(w, logits, h[s:e], a_t=lp_t[:V], b_t=h_t)
-                    del lp_t, h_t
+                    _gr.accumulate_mm_into_main_grad(w, logits, h[s:e], a_t=ops.transpose2d(lp)[:V],
+                                                     b_t=ops.transpose2d(h[s:e]))
                 elif direct:
                     _gr.accumulate_mm_into_main_grad(w, logits, h[s:e])
                 elif dw is not None:
