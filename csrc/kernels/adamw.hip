@@ -240,50 +240,77 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(uint16_t* __restrict__ p, 
       if (mats[mid].tile0 <= t0) lo = mid; else hi = mid - 1;
     }
   }
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  // Software pipeline: tile t+G's four operand vectors per lane are loaded before tile t's
+  // transposed store phase (and its two barriers), so their HBM latency overlaps it.
+  float pv[2][8], gv[2][8], mv[2][8], vv[2][8];
+  int64_t kk[2];
+  MatDesc md;
+  int64_t r0 = 0, c0 = 0;
+  auto locate = [&](int64_t t) {
     while (lo + 1 < nmats && mats[lo + 1].tile0 <= t) ++lo;
-    const MatDesc md = mats[lo];
+    md = mats[lo];
     const int64_t lt = t - md.tile0;
     const int64_t ntc = (md.cols + kAtTile - 1) / kAtTile;
-    const int64_t r0 = (lt / ntc) * kAtTile, c0 = (lt % ntc) * kAtTile;
+    r0 = (lt / ntc) * kAtTile;
+    c0 = (lt % ntc) * kAtTile;
+  };
+  auto fetch = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {  // 512 16-byte vectors per tile
+    for (int i = 0; i < 2; ++i) {
       const int id = tid + 256 * i;
-      const int lr = id >> 3, lc = (id & 7) * 8;
-      const int64_t r = r0 + lr, c = c0 + lc;
-      uint32_t* dst = reinterpret_cast<uint32_t*>(tile + lr * kAtPitch + lc);
-      if (r < md.rows && c < md.cols) {
-        const int64_t k = md.off + r * md.cols + c;
-        float pv[8], gv[8], mv[8], vv[8];
-        if (MASTER) ld8<float>(master + k, pv); else load8(p + k, pv);
-        load8(g + k, gv);
-        ld8<ST>(m + k, mv);
-        ld8<ST>(v + k, vv);
+      const int64_t r = r0 + (id >> 3), c = c0 + (id & 7) * 8;
+      kk[i] = (r < md.rows && c < md.cols) ? md.off + r * md.cols + c : -1;
+      if (kk[i] >= 0) {
+        if (MASTER) ld8<float>(master + kk[i], pv[i]); else load8(p + kk[i], pv[i]);
+        load8(g + kk[i], gv[i]);
+        ld8<ST>(m + kk[i], mv[i]);
+        ld8<ST>(v + kk[i], vv[i]);
+      }
+    }
+  };
+  int64_t t = blockIdx.x;
+  if (t < ntiles) {
+    locate(t);
+    fetch();
+  }
+  for (; t < ntiles; t += gridDim.x) {
+    const MatDesc cur = md;
+    const int64_t cr0 = r0, cc0 = c0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) adam_elem(pv[j], gv[j] * h.grad_scale, mv[j], vv[j], h, step_size, decay);
-        st8<ST>(m + k, mv);
-        st8<ST>(v + k, vv);
-        if (MASTER) st8<float>(master + k, pv);
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 256 * i;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(tile + (id >> 3) * kAtPitch + (id & 7) * 8);
+      if (kk[i] >= 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) adam_elem(pv[i][j], gv[i][j] * h.grad_scale, mv[i][j], vv[i][j], h, step_size, decay);
+        st8<ST>(m + kk[i], mv[i]);
+        st8<ST>(v + kk[i], vv[i]);
+        if (MASTER) st8<float>(master + kk[i], pv[i]);
         u16x8 pb;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = f2bf(pv[j]);
-        *reinterpret_cast<u16x8*>(p + k) = pb;
+        for (int j = 0; j < 8; ++j) pb[j] = f2bf(pv[i][j]);
+        *reinterpret_cast<u16x8*>(p + kk[i]) = pb;
 #pragma unroll
         for (int j = 0; j < 4; ++j) dst[j] = (uint32_t)pb[2 * j] | ((uint32_t)pb[2 * j + 1] << 16);
       }
     }
-    if (md.toff >= 0) {
+    const int64_t tn = t + gridDim.x;
+    if (tn < ntiles) {  // next tile's loads in flight under this tile's transposed store
+      locate(tn);
+      fetch();
+    }
+    if (cur.toff >= 0) {
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int id = tid + 256 * i;
         const int oc = id >> 3, orr = (id & 7) * 8;  // input column -> output row; first input row
-        const int64_t c = c0 + oc, r = r0 + orr;
-        if (c < md.cols && r < md.rows) {
+        const int64_t c = cc0 + oc, r = cr0 + orr;
+        if (c < cur.cols && r < cur.rows) {
           u16x8 o;
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = tile[(orr + j) * kAtPitch + oc];
-          *reinterpret_cast<u16x8*>(pt + md.toff + c * md.rows + r) = o;
+          *reinterpret_cast<u16x8*>(pt + cur.toff + c * cur.rows + r) = o;
         }
       }
     }
