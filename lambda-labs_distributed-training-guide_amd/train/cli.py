@@ -111,6 +111,8 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     g.add_argument("--pin-numa", default="off", choices=["on", "off"],
                    help="restrict each rank's CPU affinity to its GPU's NUMA node (host AdamW / D2H locality); "
                         "the placement is logged at startup either way")
+    g.add_argument("--num-layers", default=None, type=int,
+                   help="override the model's num_hidden_layers (exact-width, reduced-depth runs)")
     g.add_argument("--init-from", default=None, help="HF safetensors directory to load pretrained weights from")
     g.add_argument("--tunableop", default="use", choices=["off", "use", "tune"])
     g.add_argument("--async-ckpt", default="off", choices=["on", "off"],

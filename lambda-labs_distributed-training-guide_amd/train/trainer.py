@@ -101,7 +101,8 @@ def _scheduler(args, opt):
 
 def _build(args, chapter, device, world):
     """Model + engine + optimizer for a chapter.  Returns (model, engine, dp_size, dp_rank, ckpt_style)."""
-    cfg = resolve_config(args.model_name)
+    depth = getattr(args, "num_layers", None)
+    cfg = resolve_config(args.model_name, **({} if depth is None else {"num_hidden_layers": depth}))
     if chapter == "rime" and cfg.vocab_size != 156939:
         LOGGER.warning("rime chapter expects the +28,683-token vocabulary (llama-3.2-3b-rime)")
     tp_group = dp_group = None
