@@ -11,6 +11,8 @@
 //   p   -= (lr / (1 - beta1^t)) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
 // computed in f32 from whatever storage dtype the buffers use (bf16 "pure bf16" training as
 // in the reference, or f32 states / an f32 master copy).
+#include <type_traits>
+
 #include "common.h"
 
 namespace dtg {
@@ -205,24 +207,54 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
 // once per step, so instead of transposing every weight in every backward (one read + one write
 // of W per step), this kernel writes W^T while the updated W is still in registers: the read is
 // saved, the write moves here.  The flat buffer is described as a list of matrices (2-D params;
-// 1-D params as [1, n] rows with no transposed copy); the grid walks 64 x 64 tiles of all of
+// 1-D params as [1, n] rows with no transposed copy); the grid walks 64 x TC tiles of all of
 // them: phase 1 updates the tile row-wise with 16-byte vectors and parks the new bf16 values in
 // LDS, phase 2 writes the tile's columns as rows of W^T (16-byte vectors again).
+//
+// TC (tile columns) sets the access pattern: every phase-1 row segment is TC x 2 bytes of each
+// of the six streams (p, g, m, v in; p, m, v out), every W^T segment 128 bytes.  64-column tiles
+// read 128-byte segments of 64 different rows per array; 128 / 256 columns read 256 / 512-byte
+// segments (NT = 256 / 512 threads keep four vectors per lane).
 // ------------------------------------------------------------------------------------------
 struct MatDesc {
   int64_t off, rows, cols, toff, tile0;  // toff < 0: no transposed copy
 };
 
-constexpr int kAtTile = 64;
-constexpr int kAtPitch = kAtTile + 2;  // halfwords; odd dword pitch spreads the column gathers
+constexpr int kAtRows = 64;
 
-template <typename ST, bool MASTER>
-__global__ __launch_bounds__(256) void adamw_t_kernel(uint16_t* __restrict__ p, float* __restrict__ master,
-                                                      const uint16_t* __restrict__ g, ST* __restrict__ m,
-                                                      ST* __restrict__ v, uint16_t* __restrict__ pt,
-                                                      const MatDesc* __restrict__ mats, int nmats, int64_t ntiles,
-                                                      AdamHyper h, const float* __restrict__ dev_hyper) {
-  __shared__ uint16_t tile[kAtTile * kAtPitch];
+// Eight raw elements of a buffer, converted to f32 only when the update runs (bf16 vectors stay
+// packed in 4 VGPRs while their loads are in flight under the previous tile's store phase).
+template <typename T>
+struct Raw8;
+template <>
+struct Raw8<uint16_t> {
+  u16x8 v;
+  __device__ __forceinline__ void load(const uint16_t* p) { v = *reinterpret_cast<const u16x8*>(p); }
+  __device__ __forceinline__ float operator[](int j) const { return bf2f(v[j]); }
+};
+template <>
+struct Raw8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = reinterpret_cast<const f32x4*>(p)[0];
+    b = reinterpret_cast<const f32x4*>(p)[1];
+  }
+  __device__ __forceinline__ float operator[](int j) const { return j < 4 ? a[j] : b[j - 4]; }
+};
+
+template <typename ST, bool MASTER, int TC, int NT>
+__global__ __launch_bounds__(NT) void adamw_t_kernel(uint16_t* __restrict__ p, float* __restrict__ master,
+                                                     const uint16_t* __restrict__ g, ST* __restrict__ m,
+                                                     ST* __restrict__ v, uint16_t* __restrict__ pt,
+                                                     const MatDesc* __restrict__ mats, int nmats, int64_t ntiles,
+                                                     AdamHyper h, const float* __restrict__ dev_hyper) {
+  constexpr int kPitch = TC + 2;          // halfwords; odd dword pitch spreads the column gathers
+  constexpr int kVR = TC / 8;             // 16-byte vectors per tile row
+  constexpr int kNP = kAtRows * kVR / NT; // phase-1 vectors per lane
+  constexpr int kOutPerPass = NT / 8;     // W^T rows written per phase-2 pass (8 vectors each)
+  static_assert(kAtRows * kVR % NT == 0 && TC % kOutPerPass == 0, "tile shape");
+  using PT = typename std::conditional<MASTER, float, uint16_t>::type;
+  __shared__ uint16_t tile[kAtRows * kPitch];
   if (dev_hyper != nullptr) {
     h.lr = dev_hyper[0];
     h.bc1 = dev_hyper[1];
@@ -240,31 +272,33 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(uint16_t* __restrict__ p, 
       if (mats[mid].tile0 <= t0) lo = mid; else hi = mid - 1;
     }
   }
-  // Software pipeline: tile t+G's four operand vectors per lane are loaded before tile t's
-  // transposed store phase (and its two barriers), so their HBM latency overlaps it.
-  float pv[2][8], gv[2][8], mv[2][8], vv[2][8];
-  int64_t kk[2];
+  // Software pipeline: tile t+G's operand vectors are loaded before tile t's transposed store
+  // phase (and its two barriers), so their HBM latency overlaps it.
+  Raw8<PT> pr[kNP];
+  Raw8<uint16_t> gr[kNP];
+  Raw8<ST> mr[kNP], vr[kNP];
+  int64_t kk[kNP];
   MatDesc md;
   int64_t r0 = 0, c0 = 0;
   auto locate = [&](int64_t t) {
     while (lo + 1 < nmats && mats[lo + 1].tile0 <= t) ++lo;
     md = mats[lo];
     const int64_t lt = t - md.tile0;
-    const int64_t ntc = (md.cols + kAtTile - 1) / kAtTile;
-    r0 = (lt / ntc) * kAtTile;
-    c0 = (lt % ntc) * kAtTile;
+    const int64_t ntc = (md.cols + TC - 1) / TC;
+    r0 = (lt / ntc) * kAtRows;
+    c0 = (lt % ntc) * TC;
   };
   auto fetch = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + 256 * i;
-      const int64_t r = r0 + (id >> 3), c = c0 + (id & 7) * 8;
+    for (int i = 0; i < kNP; ++i) {
+      const int id = tid + NT * i;
+      const int64_t r = r0 + id / kVR, c = c0 + (id % kVR) * 8;
       kk[i] = (r < md.rows && c < md.cols) ? md.off + r * md.cols + c : -1;
       if (kk[i] >= 0) {
-        if (MASTER) ld8<float>(master + kk[i], pv[i]); else load8(p + kk[i], pv[i]);
-        load8(g + kk[i], gv[i]);
-        ld8<ST>(m + kk[i], mv[i]);
-        ld8<ST>(v + kk[i], vv[i]);
+        if constexpr (MASTER) pr[i].load(master + kk[i]); else pr[i].load(p + kk[i]);
+        gr[i].load(g + kk[i]);
+        mr[i].load(m + kk[i]);
+        vr[i].load(v + kk[i]);
       }
     }
   };
@@ -277,18 +311,24 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(uint16_t* __restrict__ p, 
     const MatDesc cur = md;
     const int64_t cr0 = r0, cc0 = c0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + 256 * i;
-      uint32_t* dst = reinterpret_cast<uint32_t*>(tile + (id >> 3) * kAtPitch + (id & 7) * 8);
+    for (int i = 0; i < kNP; ++i) {
+      const int id = tid + NT * i;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(tile + (id / kVR) * kPitch + (id % kVR) * 8);
       if (kk[i] >= 0) {
+        float pv[8], mv[8], vv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) adam_elem(pv[i][j], gv[i][j] * h.grad_scale, mv[i][j], vv[i][j], h, step_size, decay);
-        st8<ST>(m + kk[i], mv[i]);
-        st8<ST>(v + kk[i], vv[i]);
-        if (MASTER) st8<float>(master + kk[i], pv[i]);
+        for (int j = 0; j < 8; ++j) {
+          pv[j] = pr[i][j];
+          mv[j] = mr[i][j];
+          vv[j] = vr[i][j];
+          adam_elem(pv[j], gr[i][j] * h.grad_scale, mv[j], vv[j], h, step_size, decay);
+        }
+        st8<ST>(m + kk[i], mv);
+        st8<ST>(v + kk[i], vv);
+        if (MASTER) st8<float>(master + kk[i], pv);
         u16x8 pb;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = f2bf(pv[i][j]);
+        for (int j = 0; j < 8; ++j) pb[j] = f2bf(pv[j]);
         *reinterpret_cast<u16x8*>(p + kk[i]) = pb;
 #pragma unroll
         for (int j = 0; j < 4; ++j) dst[j] = (uint32_t)pb[2 * j] | ((uint32_t)pb[2 * j + 1] << 16);
@@ -302,14 +342,13 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(uint16_t* __restrict__ p, 
     if (cur.toff >= 0) {
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int id = tid + 256 * i;
-        const int oc = id >> 3, orr = (id & 7) * 8;  // input column -> output row; first input row
+      for (int i = 0; i < TC / kOutPerPass; ++i) {
+        const int oc = tid / 8 + kOutPerPass * i, orr = (tid % 8) * 8;  // input column -> W^T row
         const int64_t c = cc0 + oc, r = cr0 + orr;
         if (c < cur.cols && r < cur.rows) {
           u16x8 o;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = tile[(orr + j) * kAtPitch + oc];
+          for (int j = 0; j < 8; ++j) o[j] = tile[(orr + j) * kPitch + oc];
           *reinterpret_cast<u16x8*>(pt + cur.toff + c * cur.rows + r) = o;
         }
       }
@@ -321,12 +360,13 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(uint16_t* __restrict__ p, 
 void adamw_t_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g, const at::Tensor& m,
               const at::Tensor& v, const at::Tensor& pt, const at::Tensor& mats, int64_t ntiles, double lr,
               double beta1, double beta2, double eps, double wd, int64_t step, double grad_scale,
-              const c10::optional<at::Tensor>& hyper) {
+              const c10::optional<at::Tensor>& hyper, int64_t tile_cols) {
   DTG_CHECK_CUDA_BF16(p);
   DTG_CHECK_CUDA_BF16(pt);
   DTG_CHECK(g.scalar_type() == at::kBFloat16, "adamw_t_: grads must be bf16");
   DTG_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous() && pt.is_contiguous(),
             "adamw_t_: buffers must be contiguous");
+  DTG_CHECK(tile_cols == 64 || tile_cols == 128 || tile_cols == 256, "adamw_t_: tile_cols must be 64, 128 or 256");
   const int64_t n = p.numel();
   DTG_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adamw_t_: size mismatch");
   DTG_CHECK(m.scalar_type() == v.scalar_type(), "adamw_t_: exp_avg/exp_avg_sq dtype mismatch");
@@ -357,21 +397,28 @@ void adamw_t_(const at::Tensor& p, const c10::optional<at::Tensor>& master, cons
   h.bc1 = 1.0 - std::pow(beta1, (double)step);
   h.bc2_sqrt = std::sqrt(1.0 - std::pow(beta2, (double)step));
   h.grad_scale = grad_scale;
-  const int blocks = (int)std::min<int64_t>(ntiles, 256 * 32);
   float* mp = has_master ? master->data_ptr<float>() : nullptr;
   const auto* md = reinterpret_cast<const MatDesc*>(mats.data_ptr<int64_t>());
   const auto* gp = reinterpret_cast<const uint16_t*>(g.data_ptr());
   uint16_t* ptp = bf16_mut(pt);
-#define DTG_ADAMT_LAUNCH(ST, MASTER)                                                                   \
-  adamw_t_kernel<ST, MASTER><<<blocks, 256, 0, stream()>>>(bf16_mut(p), mp, gp, reinterpret_cast<ST*>(m.data_ptr()), \
-                                                           reinterpret_cast<ST*>(v.data_ptr()), ptp, md, nm, ntiles, h, hp)
   const bool sb = m.scalar_type() == at::kBFloat16;
   DTG_CHECK(sb || m.scalar_type() == at::kFloat, "adamw_t_: states must be bf16 or f32");
+#define DTG_ADAMT_LAUNCH(ST, MASTER, TC, NT)                                                              \
+  adamw_t_kernel<ST, MASTER, TC, NT><<<(int)std::min<int64_t>(ntiles, 256 * 32 * 256 / NT), NT, 0, stream()>>>( \
+      bf16_mut(p), mp, gp, reinterpret_cast<ST*>(m.data_ptr()), reinterpret_cast<ST*>(v.data_ptr()), ptp, md, nm, \
+      ntiles, h, hp)
+#define DTG_ADAMT_TILES(ST, MASTER)                                    \
+  do {                                                                 \
+    if (tile_cols == 64) DTG_ADAMT_LAUNCH(ST, MASTER, 64, 256);        \
+    else if (tile_cols == 128) DTG_ADAMT_LAUNCH(ST, MASTER, 128, 256); \
+    else DTG_ADAMT_LAUNCH(ST, MASTER, 256, 512);                       \
+  } while (0)
   if (has_master) {
-    if (sb) DTG_ADAMT_LAUNCH(uint16_t, true); else DTG_ADAMT_LAUNCH(float, true);
+    if (sb) DTG_ADAMT_TILES(uint16_t, true); else DTG_ADAMT_TILES(float, true);
   } else {
-    if (sb) DTG_ADAMT_LAUNCH(uint16_t, false); else DTG_ADAMT_LAUNCH(float, false);
+    if (sb) DTG_ADAMT_TILES(uint16_t, false); else DTG_ADAMT_TILES(float, false);
   }
+#undef DTG_ADAMT_TILES
 #undef DTG_ADAMT_LAUNCH
   DTG_LAUNCH_CHECK();
 }

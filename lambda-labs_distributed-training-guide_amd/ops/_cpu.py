@@ -109,7 +109,8 @@ def ce_grad_(logits, labels, lse, vocab_start, ignore_index, grad_scale):
     logits.copy_(g.to(logits.dtype))
 
 
-def adamw_t_(p, master, g, m, v, pt, mats, ntiles, lr, beta1, beta2, eps, wd, step, grad_scale, hyper=None):
+def adamw_t_(p, master, g, m, v, pt, mats, ntiles, lr, beta1, beta2, eps, wd, step, grad_scale, hyper=None,
+             tile_cols=64):
     """The HIP kernel's semantics: only the elements of the listed matrices are updated; each
     matrix with a transposed slot gets its new values transposed into `pt`."""
     for off, rows, cols, toff, _ in mats.tolist():

@@ -23,10 +23,11 @@ _DEFS = [
     "adamw_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!) m, Tensor(d!) v, float lr, float beta1, "
     "float beta2, float eps, float wd, int step, float grad_scale, Tensor? hyper=None) -> ()",
     # AdamW over the matrices `mats` (int64 [n, 5]: offset, rows, cols, transposed offset or -1,
-    # first tile) of the flat buffers, also writing each matrix's transpose into `pt`
+    # first tile, counted in 64 x tile_cols tiles) of the flat buffers, also writing each matrix's
+    # transpose into `pt`
     "adamw_t_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) pt, Tensor mats, "
     "int ntiles, float lr, float beta1, float beta2, float eps, float wd, int step, float grad_scale, "
-    "Tensor? hyper=None) -> ()",
+    "Tensor? hyper=None, int tile_cols=64) -> ()",
     "adamw_cpu_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float lr, float beta1, float beta2, "
     "float eps, float wd, int step, float grad_scale) -> ()",
     # window > 0 (causal only): sliding window, query i sees keys (i - window, i]

@@ -35,6 +35,7 @@ torch.optim.Optimizer (`FlatAdamW`) so LR schedulers and the reference's loop sh
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Optional
 
 import torch
@@ -138,6 +139,8 @@ class DataParallel:
         import math
 
         sp = self.space
+        # adamw_t_ tile width (64 x TC tiles; DTG_ADAMT_TC = 64 | 128 | 256; 128 measured fastest, profiles/r3_s07)
+        self._wt_tc = int(os.environ.get("DTG_ADAMT_TC", "128"))
         rows_desc, slots, toff, tile0 = [], {}, 0, 0
         for i in range(len(sp.names)):
             shape, off = sp.shapes[i], sp.offsets[i]
@@ -151,7 +154,7 @@ class DataParallel:
             else:  # updated as one row (within the flat buffer's 16-element padding), no W^T
                 rows, cols, t = 1, (n + 7) // 8 * 8, -1
             rows_desc.append([off, rows, cols, t, tile0])
-            tile0 += -(-rows // 64) * -(-cols // 64)
+            tile0 += -(-rows // 64) * -(-cols // self._wt_tc)
         if not slots:
             return
         dev = sp.param_buf.device
@@ -338,7 +341,7 @@ class DataParallel:
             torch.ops.dtg.adamw_t_(self.space.param_buf, self.master, self.space.grad_buf, self.exp_avg,
                                    self.exp_avg_sq, self._wt_buf, self._wt_mats, int(self._wt_tiles), float(lr),
                                    float(beta1), float(beta2), float(eps), float(weight_decay), int(self.step_count),
-                                   float(grad_scale), self.graph_hyper)
+                                   float(grad_scale), self.graph_hyper, self._wt_tc)
             self._wt_version = self.space.param_buf._version
         else:
             adamw_step(self.space.param_buf, self.space.grad_buf, self.exp_avg, self.exp_avg_sq, lr=lr,

@@ -216,8 +216,9 @@ def test_adamw(cuda, state_dtype, master, n):
         assert (tp.detach().float() - pm.float()).abs().max().item() <= 2 * 2**-7 * tp.detach().float().abs().max().item()
 
 
+@pytest.mark.parametrize("tile_cols", [64, 128, 256])
 @pytest.mark.parametrize("state_dtype,master", [(torch.bfloat16, False), (torch.float32, True)])
-def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master):
+def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master, tile_cols):
     """adamw_t_ (update + W^T of every listed matrix, 64 x 64 LDS tiles, edge tiles, [1, n]
     rows without a copy) == adamw_ on the same elements, bitwise; copies == W^T exactly;
     elements outside the listed matrices untouched."""
@@ -238,13 +239,13 @@ def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master):
     for (r, c), off in zip(shapes, offs):
         t = toff if r > 1 else -1
         desc.append([off, r, c, t, tile0])
-        tile0 += -(-r // 64) * -(-c // 64)
+        tile0 += -(-r // 64) * -(-c // tile_cols)
         if r > 1:
             toff += r * c
     pt = torch.zeros(toff, dtype=torch.bfloat16, device=cuda)
     mats = torch.tensor(desc, dtype=torch.long, device=cuda)
     for step in (1, 2):
-        dops.adamw_t_(p, mw, g, m, v, pt, mats, tile0, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, 0.5)
+        dops.adamw_t_(p, mw, g, m, v, pt, mats, tile0, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, 0.5, None, tile_cols)
         for (r, c), off in zip(shapes, offs):
             sl = slice(off, off + r * c)
             dops.adamw_(ref[0][sl], None if ref[4] is None else ref[4][sl], ref[1][sl], ref[2][sl], ref[3][sl],

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=4096)
     ap.add_argument("--inter", type=int, default=14336)
     ap.add_argument("--params", type=float, default=8.03e9, help="AdamW buffer length")
+    ap.add_argument("--layers", type=int, default=8, help="decoder layers of matrices for adamw_t_")
+    ap.add_argument("--only", default="", help="run only the cases whose name contains this")
     a = ap.parse_args()
     import torch
 
@@ -65,7 +67,35 @@ def main():
     m = torch.zeros(n, **bf)
     v = torch.zeros(n, **bf)
     cases["adamw (bf16 p/g/m/v)"] = (lambda: ops.adamw_(p, None, g, m, v, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0), 14 * n)
+    # adamw_t_ over Llama-3-8B's matrix shapes (a.layers decoder layers), each tile width
+    shapes = [(6144, H), (H, H), (2 * I, H), (H, I)] * a.layers
+    for tc in (64, 128, 256):
+        desc, off, toff, tile0 = [], 0, 0, 0
+        for r, c in shapes:
+            desc.append([off, r, c, toff, tile0])
+            off += r * c
+            toff += r * c
+            tile0 += -(-r // 64) * -(-c // tc)
+        nt = off
+        pw, gw = torch.randn(nt, **bf), torch.randn(nt, **bf)
+        mw, vw, ptw = torch.zeros(nt, **bf), torch.zeros(nt, **bf), torch.empty(nt, **bf)
+        mats = torch.tensor(desc, dtype=torch.long, device=dev)
+        runs = {f"adamw_t_ 64x{tc} (+W^T)": (lambda: ops.adamw_t_(pw, None, gw, mw, vw, ptw, mats, tile0, 1e-4, 0.9,
+                                                               0.999, 1e-8, 0.01, 3, 1.0, None, tc), 16 * nt)}
+        if tc == 64:
+            runs["adamw_ (same buffers)"] = (lambda: ops.adamw_(pw, None, gw, mw, vw, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3,
+                                                                1.0), 14 * nt)
+        for name, (fn, nbytes) in runs.items():
+            if a.only and a.only not in name:
+                continue
+            ms = timeit(torch, fn)
+            print(json.dumps({"kernel": name, "ms": round(ms, 4), "bytes": nbytes, "TBps": round(nbytes / ms / 1e9, 2)}),
+                  flush=True)
+        del pw, gw, mw, vw, ptw, runs
+        torch.cuda.empty_cache()
     for name, (fn, nbytes) in cases.items():
+        if a.only and a.only not in name:
+            continue
         ms = timeit(torch, fn)
         print(json.dumps({"kernel": name, "ms": round(ms, 4), "bytes": nbytes, "TBps": round(nbytes / ms / 1e9, 2)}),
               flush=True)
