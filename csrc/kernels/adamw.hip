@@ -69,7 +69,7 @@ __device__ __forceinline__ void adam_elem(float& pv, float gv, float& mv, float&
 // `dev_hyper` (optional, f32 [3] = lr, 1 - beta1^t, sqrt(1 - beta2^t)) overrides the launch
 // arguments: a HIP-graph-captured step replays the same kernel arguments every time, so the
 // step-dependent values live in device memory the host rewrites before each replay.
-template <typename GT, typename ST, bool MASTER, bool VEC>
+template <typename GT, typename ST, bool MASTER, bool VEC, int U = 2>
 __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ p, float* __restrict__ master,
                                                     const GT* __restrict__ g, ST* __restrict__ m,
                                                     ST* __restrict__ v, int64_t n, AdamHyper h,
@@ -82,15 +82,15 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ p, fl
   const float step_size = h.lr / h.bc1;
   const float decay = 1.f - h.lr * h.wd;
   if constexpr (VEC) {
-    // Two 8-element vectors per lane per iteration (the second one grid-stride away): eight
-    // 16-byte loads in flight per lane before the first use, which is what lifts this purely
+    // U 8-element vectors per lane per iteration (each one grid-stride away from the last):
+    // 4U 16-byte loads in flight per lane before the first use, which is what lifts this purely
     // streaming kernel toward HBM bandwidth (4 in flight left it latency-bound).
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
     int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-    for (; i + stride < n; i += 2 * stride) {
-      float pv[2][8], gv[2][8], mv[2][8], vv[2][8];
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+      float pv[U][8], gv[U][8], mv[U][8], vv[U][8];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t k = i + u * stride;
         if (MASTER) ld8<float>(master + k, pv[u]); else load8(p + k, pv[u]);
         ld8<GT>(g + k, gv[u]);
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ p, fl
         ld8<ST>(v + k, vv[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t k = i + u * stride;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ p, fl
         store8(p + k, pv[u]);
       }
     }
-    if (i < n) {
+    for (; i < n; i += stride) {
       float pv[8], gv[8], mv[8], vv[8];
       if (MASTER) ld8<float>(master + i, pv); else load8(p + i, pv);
       ld8<GT>(g + i, gv);
@@ -169,7 +169,13 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   h.grad_scale = grad_scale;
   const int threads = 256;
   const int64_t want = (n + threads * 8 - 1) / (threads * 8);
-  const int blocks = (int)std::min<int64_t>(want, 256 * 16);
+  // DTG_ADAM_UNROLL = 2 | 4 (vectors per lane per iteration), DTG_ADAM_WG_PER_CU: grid size
+  // (A/B knobs, tools/bench_kernels.py); read per call so a benchmark can switch in-process.
+  const char* ue = std::getenv("DTG_ADAM_UNROLL");
+  const char* we = std::getenv("DTG_ADAM_WG_PER_CU");
+  const int unroll = (ue && std::atoi(ue) == 4) ? 4 : 2;
+  const int wg_per_cu = we ? std::max(1, std::atoi(we)) : 16;
+  const int blocks = (int)std::min<int64_t>(want, 256 * wg_per_cu);
   float* mp = has_master ? master->data_ptr<float>() : nullptr;
   const bool gb = g.scalar_type() == at::kBFloat16;
   const bool sb = m.scalar_type() == at::kBFloat16;
@@ -179,7 +185,10 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   const bool vec = (n % 8 == 0) && aligned(p) && aligned(g) && aligned(m) && aligned(v) &&
                    (!has_master || aligned(*master));
 #define DTG_ADAM_LAUNCH(GT, ST, MASTER)                                                      \
-  do { if (vec) adamw_kernel<GT, ST, MASTER, true><<<blocks, threads, 0, stream()>>>(            \
+  do { if (vec && unroll == 4) adamw_kernel<GT, ST, MASTER, true, 4><<<blocks, threads, 0, stream()>>>( \
+      bf16_mut(p), mp, reinterpret_cast<const GT*>(g.data_ptr()), reinterpret_cast<ST*>(m.data_ptr()), \
+      reinterpret_cast<ST*>(v.data_ptr()), n, h, hp);                                       \
+  else if (vec) adamw_kernel<GT, ST, MASTER, true, 2><<<blocks, threads, 0, stream()>>>(            \
       bf16_mut(p), mp, reinterpret_cast<const GT*>(g.data_ptr()), reinterpret_cast<ST*>(m.data_ptr()), \
       reinterpret_cast<ST*>(v.data_ptr()), n, h, hp);                                       \
   else adamw_kernel<GT, ST, MASTER, false><<<blocks, threads, 0, stream()>>>(               \

@@ -6,6 +6,7 @@
 // One fused GEMM replaces the two HF Linear calls; this kernel reads gu once and writes h
 // once (forward) and reads dh + gu once to write dgu (backward).  f32 math, one rounding.
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 
@@ -55,54 +56,68 @@ __global__ void swiglu_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_
 //   dgu  [T, 2I]   (row-major, for dX = dgu @ W_gu)
 //   dguT [2I, T]   (for dW_gu = dguT @ X)
 //   hT   [I, T]    (h = silu(g) * u recomputed from gu, for dW_down = dY^T @ h)
-// One workgroup owns a 64-token x 64-feature tile: 16-byte row loads of g, u, dh; the three
-// transposed tiles are staged through LDS (pitch 66 halfwords) and stored as 16-byte columns.
-namespace {
-constexpr int kSgTile = 64;  // features per workgroup
-constexpr int kSgPitch = kSgTile + 2;
-}  // namespace
-
-// TT tokens x 64 features per workgroup.  TT = 64 stores the transposed tiles as 128-byte
-// row segments, TT = 128 as 256-byte segments (twice the LDS: 3 x 128 x 66 halfwords).
-template <int TT>
+// One workgroup owns a TT-token x TF-feature tile: 16-byte row loads of g, u, dh (TF x 2-byte
+// segments of TT token rows); the three transposed tiles are staged through LDS (pitch TF + 2
+// halfwords) and stored as 16-byte columns (TT x 2-byte segments of TF feature rows).  Segment
+// length is what the tile shape buys: 128-byte segments (64 x 64) leave HBM well short of its
+// streaming rate, 256-byte ones recover most of it (the adamw_t_ tile measurements, r3_s07).
+template <int TT, int TF>
 __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
     const uint16_t* __restrict__ dh, const uint16_t* __restrict__ gu, int64_t gu_stride,
     uint16_t* __restrict__ dgu, uint16_t* __restrict__ dguT, uint16_t* __restrict__ hT, int64_t T, int I, int gc) {
-  static_assert(TT == 64 || TT == 128, "token tile");
-  __shared__ uint16_t s_dg[TT * kSgPitch];
-  __shared__ uint16_t s_du[TT * kSgPitch];
-  __shared__ uint16_t s_h[TT * kSgPitch];
+  static_assert((TT == 64 || TT == 128) && (TF == 64 || TF == 128), "tile");
+  constexpr int kPitch = TF + 2;
+  constexpr int kVF = TF / 8;                 // 16-byte vectors per token row of the tile
+  constexpr int kRowsPerPass = 256 / kVF;     // token rows per phase-1 pass
+  constexpr int kVT = TT / 8;                 // 16-byte vectors per transposed row segment
+  constexpr int kOutPerPass = 256 / kVT;      // feature rows per phase-2 pass
+  extern __shared__ uint16_t smem[];
+  uint16_t* s_dg = smem;
+  uint16_t* s_du = smem + TT * kPitch;
+  uint16_t* s_h = smem + 2 * TT * kPitch;
   int64_t rt, ct;
-  tile_coords(gc, (T + TT - 1) / TT, (I + kSgTile - 1) / kSgTile, rt, ct);
+  tile_coords(gc, (T + TT - 1) / TT, (I + TF - 1) / TF, rt, ct);
   const int64_t t0 = rt * TT;
-  const int c0 = (int)ct * kSgTile;
+  const int c0 = (int)ct * TF;
   const int tid = threadIdx.x;
+  // all loads of the tile first (3 x TT*TF/2048 vectors per lane in flight), then the math
+  constexpr int kNP = TT / kRowsPerPass;
+  u16x8 rg[kNP], ru[kNP], rd[kNP];
 #pragma unroll
-  for (int i = 0; i < TT / 32; ++i) {
-    const int lt = (tid >> 3) + 32 * i;
-    const int lc = (tid & 7) * 8;
+  for (int i = 0; i < kNP; ++i) {
+    const int lt = tid / kVF + kRowsPerPass * i;
+    const int lc = (tid % kVF) * 8;
     const int64_t t = t0 + lt;
     const int c = c0 + lc;
-    float g[8], u[8], d[8];
+    if (t < T && c < I) {
+      rg[i] = *reinterpret_cast<const u16x8*>(gu + t * gu_stride + c);
+      ru[i] = *reinterpret_cast<const u16x8*>(gu + t * gu_stride + I + c);
+      rd[i] = *reinterpret_cast<const u16x8*>(dh + t * I + c);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kNP; ++i) {
+    const int lt = tid / kVF + kRowsPerPass * i;
+    const int lc = (tid % kVF) * 8;
+    const int64_t t = t0 + lt;
+    const int c = c0 + lc;
     u16x8 vdg = {0, 0, 0, 0, 0, 0, 0, 0}, vdu = vdg, vh = vdg;
     if (t < T && c < I) {
-      load8(gu + t * gu_stride + c, g);
-      load8(gu + t * gu_stride + I + c, u);
-      load8(dh + t * I + c, d);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float sg = sigmoidf_(g[j]);
-        const float silu = g[j] * sg;
-        vdu[j] = f2bf(d[j] * silu);
-        vdg[j] = f2bf(d[j] * u[j] * sg * (1.f + g[j] * (1.f - sg)));
-        vh[j] = f2bf(silu * u[j]);
+        const float g = bf2f(rg[i][j]), u = bf2f(ru[i][j]), d = bf2f(rd[i][j]);
+        const float sg = sigmoidf_(g);
+        const float silu = g * sg;
+        vdu[j] = f2bf(d * silu);
+        vdg[j] = f2bf(d * u * sg * (1.f + g * (1.f - sg)));
+        vh[j] = f2bf(silu * u);
       }
       *reinterpret_cast<u16x8*>(dgu + t * 2 * I + c) = vdg;
       *reinterpret_cast<u16x8*>(dgu + t * 2 * I + I + c) = vdu;
     }
-    uint32_t* a = reinterpret_cast<uint32_t*>(s_dg + lt * kSgPitch + lc);
-    uint32_t* b = reinterpret_cast<uint32_t*>(s_du + lt * kSgPitch + lc);
-    uint32_t* h = reinterpret_cast<uint32_t*>(s_h + lt * kSgPitch + lc);
+    uint32_t* a = reinterpret_cast<uint32_t*>(s_dg + lt * kPitch + lc);
+    uint32_t* b = reinterpret_cast<uint32_t*>(s_du + lt * kPitch + lc);
+    uint32_t* h = reinterpret_cast<uint32_t*>(s_h + lt * kPitch + lc);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       a[j] = (uint32_t)vdg[2 * j] | ((uint32_t)vdg[2 * j + 1] << 16);
@@ -111,21 +126,19 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
     }
   }
   __syncthreads();
-  constexpr int kVecPerRow = TT / 8;          // 16-byte vectors per transposed row segment
-  constexpr int kRowsPerIter = 256 / kVecPerRow;
 #pragma unroll
-  for (int i = 0; i < kSgTile / kRowsPerIter; ++i) {
-    const int oc = tid / kVecPerRow + kRowsPerIter * i;  // feature within the tile -> output row
-    const int ot = (tid % kVecPerRow) * 8;               // first token of this 8-token vector
+  for (int i = 0; i < TF / kOutPerPass; ++i) {
+    const int oc = tid / kVT + kOutPerPass * i;  // feature within the tile -> output row
+    const int ot = (tid % kVT) * 8;              // first token of this 8-token vector
     const int c = c0 + oc;
     const int64_t t = t0 + ot;
     if (c >= I || t >= T) continue;
     u16x8 a, b, h;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      a[j] = s_dg[(ot + j) * kSgPitch + oc];
-      b[j] = s_du[(ot + j) * kSgPitch + oc];
-      h[j] = s_h[(ot + j) * kSgPitch + oc];
+      a[j] = s_dg[(ot + j) * kPitch + oc];
+      b[j] = s_du[(ot + j) * kPitch + oc];
+      h[j] = s_h[(ot + j) * kPitch + oc];
     }
     *reinterpret_cast<u16x8*>(dguT + (int64_t)c * T + t) = a;
     *reinterpret_cast<u16x8*>(dguT + (int64_t)(I + c) * T + t) = b;
@@ -147,17 +160,30 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& dh
   auto dguT = at::empty({2 * I, T}, gu.options());
   auto hT = at::empty({I, T}, gu.options());
   if (T == 0 || I == 0) return {dgu, dguT, hT};
-  // DTG_SWIGLU_TT=64|128: token tile (A/B knob; see the kernel comment)
-  const char* tt_env = std::getenv("DTG_SWIGLU_TT");  // read per call: tests switch it in-process
-  const int tt = (tt_env && std::atoi(tt_env) == 128) ? 128 : 64;
+  // DTG_SWIGLU_TILE = TTxTF (64x64 | 64x128 | 128x64 | 128x128): token x feature tile (A/B knob;
+  // read per call so tests and benchmarks switch it in-process)
+  const char* te = std::getenv("DTG_SWIGLU_TILE");
+  int tt = 64, tf = 64;
+  if (te) {
+    if (!std::strcmp(te, "64x64")) tt = 64, tf = 64;
+    else if (!std::strcmp(te, "128x64")) tt = 128, tf = 64;
+    else if (!std::strcmp(te, "128x128")) tt = 128, tf = 128;
+  }
   const int gc = tile_group_env(kDefaultTileGroup);
-  const dim3 grid = tile_grid(gc, (T + tt - 1) / tt, (I + kSgTile - 1) / kSgTile);
-  if (tt == 128)
-    swiglu_bwd_t_kernel<128><<<grid, 256, 0, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu),
-                                                         bf16_mut(dguT), bf16_mut(hT), T, I, gc);
-  else
-    swiglu_bwd_t_kernel<64><<<grid, 256, 0, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu),
-                                                        bf16_mut(dguT), bf16_mut(hT), T, I, gc);
+  const dim3 grid = tile_grid(gc, (T + tt - 1) / tt, (I + tf - 1) / tf);
+  const size_t lds = 3 * (size_t)tt * (tf + 2) * sizeof(uint16_t);
+#define DTG_SG_LAUNCH(TT_, TF_)                                                                            \
+  do {                                                                                                     \
+    auto fn = swiglu_bwd_t_kernel<TT_, TF_>;                                                               \
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    fn<<<grid, 256, lds, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu), bf16_mut(dguT),  \
+                                     bf16_mut(hT), T, I, gc);                                              \
+  } while (0)
+  if (tt == 64 && tf == 64) DTG_SG_LAUNCH(64, 64);
+  else if (tt == 64) DTG_SG_LAUNCH(64, 128);
+  else if (tf == 64) DTG_SG_LAUNCH(128, 64);
+  else DTG_SG_LAUNCH(128, 128);
+#undef DTG_SG_LAUNCH
   DTG_LAUNCH_CHECK();
   return {dgu, dguT, hT};
 }

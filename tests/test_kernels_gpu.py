@@ -93,10 +93,10 @@ def test_transpose2d(cuda, R, C, ld, group, monkeypatch):
 
 
 @pytest.mark.parametrize("group", ["0", "3", "16"])
-@pytest.mark.parametrize("tt", ["64", "128"])
+@pytest.mark.parametrize("tile", ["64x64", "64x128", "128x64", "128x128"])
 @pytest.mark.parametrize("T,I", [(64, 64), (4096, 1792), (520, 136)])
-def test_swiglu_bwd_t(cuda, T, I, tt, group, monkeypatch):
-    monkeypatch.setenv("DTG_SWIGLU_TT", tt)
+def test_swiglu_bwd_t(cuda, T, I, tile, group, monkeypatch):
+    monkeypatch.setenv("DTG_SWIGLU_TILE", tile)
     monkeypatch.setenv("DTG_TILE_GROUP", group)
     torch.manual_seed(0)
     gu = (2 * torch.randn(T, 2 * I)).bfloat16()

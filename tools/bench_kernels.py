@@ -56,7 +56,9 @@ def main():
         "add_rmsnorm_fwd": (lambda: ops.add_rmsnorm_fwd(x, res, w, 1e-5), 4 * T * H * E),
         "rmsnorm_bwd(+dres)": (lambda: ops.rmsnorm_bwd(dy, hh, w, rstd, dy), 4 * T * H * E),
         "swiglu_fwd": (lambda: ops.swiglu_fwd(gu), 3 * T * I * E),
-        "swiglu_bwd_t (dgu, dgu^T, h^T)": (lambda: ops.swiglu_bwd_t(dh, gu), (3 + 5) * T * I * E),
+        **{f"swiglu_bwd_t (dgu, dgu^T, h^T) tile {tl}": (lambda tl=tl: (os.environ.__setitem__("DTG_SWIGLU_TILE", tl),
+                                                                       ops.swiglu_bwd_t(dh, gu)), (3 + 5) * T * I * E)
+           for tl in ("64x64", "64x128", "128x64", "128x128")},
         "transpose [T,H]": (lambda: ops.transpose2d(x), 2 * T * H * E),
         "transpose [T,2I]": (lambda: ops.transpose2d(gu), 2 * T * 2 * I * E),
     }
@@ -83,8 +85,16 @@ def main():
         runs = {f"adamw_t_ 64x{tc} (+W^T)": (lambda: ops.adamw_t_(pw, None, gw, mw, vw, ptw, mats, tile0, 1e-4, 0.9,
                                                                0.999, 1e-8, 0.01, 3, 1.0, None, tc), 16 * nt)}
         if tc == 64:
-            runs["adamw_ (same buffers)"] = (lambda: ops.adamw_(pw, None, gw, mw, vw, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3,
-                                                                1.0), 14 * nt)
+            for un, wg in ((2, 16), (4, 16), (2, 8), (4, 8), (2, 32), (4, 4)):
+                def lin(un=un, wg=wg):
+                    os.environ["DTG_ADAM_UNROLL"], os.environ["DTG_ADAM_WG_PER_CU"] = str(un), str(wg)
+                    ops.adamw_(pw, None, gw, mw, vw, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0)
+                runs[f"adamw_ (same buffers) unroll {un} wg/cu {wg}"] = (lin, 14 * nt)
+        if tc == 128:  # the tile walk with no transposed copies (toff = -1): layout effect alone
+            mats_nt = mats.clone()
+            mats_nt[:, 3] = -1
+            runs["adamw_t_ 64x128 tile walk, no W^T"] = (lambda: ops.adamw_t_(
+                pw, None, gw, mw, vw, ptw, mats_nt, tile0, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0, None, tc), 14 * nt)
         for name, (fn, nbytes) in runs.items():
             if a.only and a.only not in name:
                 continue
