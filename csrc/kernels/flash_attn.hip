@@ -592,6 +592,54 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   __syncthreads();
 
   const int wave_q0 = q0 + 32 * w, wave_qmax = wave_q0 + 31;
+  // The three pieces of a 32-key half: S / dP MFMAs, softmax -> dS fragments, dQ MFMAs.
+  auto sd_mfma = [&](const char* K, const char* V, int kt, f32x16& s, f32x16& dp) {
+    bf16x8 f[NC], g[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) f[c] = lds_frag(K + kt * 32 * RB + koff[c]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) s = mfma(f[c], qf[c], s);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) g[c] = lds_frag(V + kt * 32 * RB + koff[c]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dp = mfma(g[c], dof[c], dp);
+  };
+  // Does any element of the 32-key half at key0 need the causal / length / window mask?
+  auto half_masked = [&](int key0) {
+    return (CAUSAL && key0 + 31 > wave_q0 + koff_c) || key0 + 32 > klen ||
+           (win > 0 && key0 < wave_qmax + koff_c - win + 1);
+  };
+  auto softmax_ds = [&](int key0, f32x16& s, const f32x16& dp, bf16x8* dsf) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = fexp2(__builtin_fmaf(s[i], P.c2, -lse2));
+    if (half_masked(key0)) {
+      const int lim = (CAUSAL ? min(qrow + koff_c, klen - 1) : klen - 1) - (key0 + 4 * h);
+      const int llim = win > 0 ? qrow + koff_c - win + 1 - (key0 + 4 * h) : INT_MIN;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) > lim || acc_row0(i) < llim) ? 0.f : s[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] *= dp[i] - delta;  // dS^T / scale
+    dsf[0] = pack8(s, 0);
+    dsf[1] = pack8(s, 1);
+  };
+  auto dq_mfma = [&](const char* K, int kt, const bf16x8* dsf) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const char* kb = K + (32 * kt + 16 * st) * RB;
+      bf16x8 kt_[ND];
+#pragma unroll
+      for (int d = 0; d < ND; ++d) kt_[d] = tr_frag_at(kb + toa[d], kb + tob[d]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) acc[d] = mfma(kt_[d], dsf[st], acc[d]);
+    }
+  };
+  // Wave-uniform: a 32-key half entirely above the diagonal, past the end, or before every
+  // query's sliding window contributes nothing.
+  auto half_live = [&](int key0) {
+    return !((CAUSAL && key0 > wave_qmax + koff_c) || key0 >= klen) &&
+           !(win > 0 && key0 + 31 < wave_q0 + koff_c - win + 1);
+  };
   // Tile loop unrolled by two so the double-buffer offsets are compile-time immediates.
   auto tile_step = [&](int t, auto buf) {
     constexpr int B = decltype(buf)::value;
@@ -604,52 +652,24 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     }
     const char* K = smem + B * 2 * TILE;
     const char* V = K + TILE;
+    const bool live0 = half_live(kt0), live1 = half_live(kt0 + 32);
+    {  // (a software-pipelined body -- half 1's S / dP under half 0's softmax -- measured no
+       // faster, bitwise equal: profiles/r3_s09)
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const int key0 = kt0 + 32 * kt;
-      // Wave-uniform skip of 32-key halves entirely above the diagonal, past the end, or before
-      // every query's sliding window.
-      if ((CAUSAL && key0 > wave_qmax + koff_c) || key0 >= klen) continue;
-      if (win > 0 && key0 + 31 < wave_q0 + koff_c - win + 1) continue;
-      f32x16 s = f32x16{}, dp = f32x16{};
-      __builtin_amdgcn_sched_barrier(0);
-      {
-        bf16x8 f[NC], g[NC];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) f[c] = lds_frag(K + kt * 32 * RB + koff[c]);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) s = mfma(f[c], qf[c], s);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) g[c] = lds_frag(V + kt * 32 * RB + koff[c]);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) dp = mfma(g[c], dof[c], dp);
+      for (int kt = 0; kt < 2; ++kt) {
+        if (!(kt == 0 ? live0 : live1)) continue;
+        f32x16 s = f32x16{}, dp = f32x16{};
+        __builtin_amdgcn_sched_barrier(0);
+        sd_mfma(K, V, kt, s, dp);
+        pipeline_reads<2 * NC, 1, 4>();
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 dsf[2];
+        softmax_ds(kt0 + 32 * kt, s, dp, dsf);
+        __builtin_amdgcn_sched_barrier(0);
+        dq_mfma(K, kt, dsf);
+        pipeline_reads<2 * ND, 2, 3>();
+        __builtin_amdgcn_sched_barrier(0);
       }
-      pipeline_reads<2 * NC, 1, 4>();
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] = fexp2(__builtin_fmaf(s[i], P.c2, -lse2));
-      if ((CAUSAL && key0 + 31 > wave_q0 + koff_c) || key0 + 32 > klen ||
-          (win > 0 && key0 < wave_qmax + koff_c - win + 1)) {
-        const int lim = (CAUSAL ? min(qrow + koff_c, klen - 1) : klen - 1) - (key0 + 4 * h);
-        const int llim = win > 0 ? qrow + koff_c - win + 1 - (key0 + 4 * h) : INT_MIN;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) > lim || acc_row0(i) < llim) ? 0.f : s[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] *= dp[i] - delta;  // dS^T / scale
-      const bf16x8 dsf[2] = {pack8(s, 0), pack8(s, 1)};
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const char* kb = K + (32 * kt + 16 * st) * RB;
-        bf16x8 kt_[ND];
-#pragma unroll
-        for (int d = 0; d < ND; ++d) kt_[d] = tr_frag_at(kb + toa[d], kb + tob[d]);
-#pragma unroll
-        for (int d = 0; d < ND; ++d) acc[d] = mfma(kt_[d], dsf[st], acc[d]);
-      }
-      pipeline_reads<2 * ND, 2, 3>();
-      __builtin_amdgcn_sched_barrier(0);
     }
     if (more) {
       char* nb = smem + (1 - B) * 2 * TILE;

@@ -35,7 +35,13 @@ def main():
     ap.add_argument("--ab", default=None,
                     help="comma list of DTG_FA_FWD variants (e.g. v0,v1): forward timed in interleaved "
                          "rounds in ONE process (same device, same clocks), medians reported")
+    ap.add_argument("--ab-bwd", default=None,
+                    help="VAR=v1,v2 (e.g. DTG_FA_OCC=1,2): backward timed under each value of the environment "
+                         "knob in interleaved rounds in ONE process, medians reported, outputs compared bitwise")
     a = ap.parse_args()
+    if a.ab_bwd:
+        var, vals = a.ab_bwd.split("=", 1)
+        return ab_bwd(a, var, vals.split(","))
     if a.ab:
         return ab(a, a.ab.split(","))
     if a.sweep:
@@ -104,6 +110,45 @@ def ab(a, variants, rounds=7):
         for vv in variants:
             med = statistics.median(times[vv])
             rec[vv] = {"ms": round(med, 4), "min_ms": round(min(times[vv]), 4), "TFLOPs": round(flops / med / 1e9, 1)}
+        print(json.dumps(rec), flush=True)
+
+
+def ab_bwd(a, var, variants, rounds=7):
+    import statistics
+
+    cases = [("S1024c", dict(B=16, S=1024, hq=32, hkv=8, d=128, docs=None), True),
+             ("S4096c", dict(B=4, S=4096, hq=32, hkv=8, d=128, docs=None), True),
+             ("S8192nc", dict(B=2, S=8192, hq=32, hkv=8, d=128, docs=None), False),
+             ("rime", SHAPES["rime"], True)]
+    ops = torch.ops.dtg
+    for name, c, causal in cases:
+        q, k, v, cu, maxlen, flops, scale = _inputs(c, causal)
+        qkv = q.as_strided((q.shape[0], q.stride(0)), (q.stride(0), 1))  # the fused projection output
+        hq, hkv, d = c["hq"], c["hkv"], c["d"]
+        do = torch.randn(q.shape[0], hq, d, device=q.device).bfloat16()
+        o, lse = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal)
+        ref = None
+        times = {vv: [] for vv in variants}
+        for r in range(rounds):
+            for vv in variants:
+                os.environ[var] = vv
+                for _ in range(3):
+                    g = ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, causal)
+                if ref is None:
+                    ref = g.clone()
+                elif r == 0:
+                    assert torch.equal(g, ref), (name, vv, (g.float() - ref.float()).abs().max().item())
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, causal)
+                e1.record()
+                torch.cuda.synchronize()
+                times[vv].append(e0.elapsed_time(e1) / a.iters)
+        rec = {"case": name, "bitwise_equal": True}
+        for vv in variants:
+            med = statistics.median(times[vv])
+            rec[vv] = {"ms": round(med, 4), "min_ms": round(min(times[vv]), 4), "TFLOPs": round(2.5 * flops / med / 1e9, 1)}
         print(json.dumps(rec), flush=True)
 
 
