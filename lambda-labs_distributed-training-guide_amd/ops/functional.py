@@ -386,9 +386,11 @@ def embedding(ids, w):
 # Fused lm_head + causal-LM cross entropy (chunked; logits never materialised whole)
 # --------------------------------------------------------------------------------------------
 def _default_chunk(vocab, hidden_rows):
-    """Rows per chunk: ~1 GiB of bf16 logits, split evenly over the rows (16,384 rows x 128,256
-    vocab -> 4 x 4,096), a multiple of 64 rows (transposable, MFMA-tile aligned), >= 1024."""
-    n = max(1, -(-hidden_rows * max(vocab, 1) // (1 << 29)))
+    """Rows per chunk: ~1 GiB of bf16 logits (DTG_CE_CHUNK_GIB), split evenly over the rows
+    (16,384 rows x 128,256 vocab -> 4 x 4,096), a multiple of 64 rows (transposable, MFMA-tile
+    aligned), >= 1024."""
+    gib = float(os.environ.get("DTG_CE_CHUNK_GIB", "1"))
+    n = max(1, -(-hidden_rows * max(vocab, 1) // max(1, int(gib * (1 << 29)))))
     per = -(-hidden_rows // n)
     return max(1024, min(hidden_rows, -(-per // 64) * 64))
 
