@@ -151,10 +151,21 @@ class DataParallel:
                 rows, cols, t = shape[0], shape[1], toff
                 slots[i] = (toff, rows, cols)
                 toff += (n + 127) // 128 * 128  # 256-byte aligned copies, like the allocator's
-            else:  # updated as one row (within the flat buffer's 16-element padding), no W^T
-                rows, cols, t = 1, (n + 7) // 8 * 8, -1
-            rows_desc.append([off, rows, cols, t, tile0])
-            tile0 += -(-rows // 64) * -(-cols // self._wt_tc)
+                rows_desc.append([off, rows, cols, t, tile0])
+                tile0 += -(-rows // 64) * -(-cols // self._wt_tc)
+                continue
+            # No W^T (norm weights, a vocabulary that is not a multiple of 8): updated as full
+            # [*, TC] rows plus one short row (within the flat buffer's 16-element padding), so
+            # every tile is full -- one [1, n] row would leave 63 of a tile's 64 rows idle
+            # (a 157k x 3072 embedding took the update from 8 to 16 ms, profiles/r3_s10).
+            n8 = (n + 7) // 8 * 8
+            full, rem = divmod(n8, self._wt_tc)
+            if full:
+                rows_desc.append([off, full, self._wt_tc, -1, tile0])
+                tile0 += -(-full // 64)
+            if rem:
+                rows_desc.append([off + full * self._wt_tc, 1, rem, -1, tile0])
+                tile0 += 1
         if not slots:
             return
         dev = sp.param_buf.device

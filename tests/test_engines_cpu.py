@@ -118,20 +118,23 @@ def test_optimizer_in_backward_distributed(mode, accum):
             torch.testing.assert_close(res[r][0][n], ref[n], atol=3e-4, rtol=1e-3, msg=f"rank {r} {n}")
 
 
-def test_weight_t_copies_refreshed_by_optimizer_match_plain_training(monkeypatch):
+@pytest.mark.parametrize("vocab", [512, 1003])
+def test_weight_t_copies_refreshed_by_optimizer_match_plain_training(monkeypatch, vocab):
     """Single-device engine with persistent W^T (written by the adamw_t_ optimizer kernel):
     the same parameters after 3 steps as the plain engine, every copy equal to its weight's
     transpose after each step, the backward reads the copies (no per-weight transposes), and a
     weight edited outside the optimizer is never paired with its stale copy."""
     import dtg.ops.functional as F_
-    from dtg.models import build_model
+    from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
 
+    # vocab 1003: embedding / lm_head get no W^T (not a multiple of 8) and are walked as full
+    # [*, TC] rows plus a short row
     batches = _batches(512, 2, 32, n=3)
     res = {}
     for wt in (False, True):
         torch.manual_seed(0)
-        m = build_model("llama-tiny", device="cpu", dtype=torch.float32)
+        m = build_model(resolve_config("llama-tiny", vocab_size=vocab), device="cpu", dtype=torch.float32)
         eng = DataParallel(m, mode="single", weight_t=wt)
         opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
         calls = []
@@ -160,3 +163,49 @@ def test_weight_t_copies_refreshed_by_optimizer_match_plain_training(monkeypatch
     # the plain engine transposes every weight (and activations) per backward; with W^T only
     # activations (tokens < 4096 here: the TN path is off on CPU, so both counts may be 0)
     assert res[True][1] <= res[False][1]
+
+
+def test_weight_t_descriptors_cover_every_element_once():
+    """adamw_t_ descriptors: W^T matrices as themselves, everything else as full [*, TC] rows
+    plus one short row -- together every element of every parameter exactly once (and the
+    optimizer result equals the plain engine's)."""
+    import torch.nn as nn
+
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Parameter(torch.randn(128, 64))   # W^T copy
+            self.b = nn.Parameter(torch.randn(1000))      # 1-D, not a multiple of the tile width
+            self.c = nn.Parameter(torch.randn(24, 40))    # too small for a copy
+            self.d = nn.Parameter(torch.randn(1003, 64))  # rows not a multiple of 8
+
+        def forward(self, x):
+            return (x @ self.a.t()).sum() + self.b.sum() + self.c.sum() + (x @ self.d.t()).sum()
+
+    outs = {}
+    for wt in (False, True):
+        torch.manual_seed(0)
+        m = M()
+        eng = DataParallel(m, mode="single", weight_t=wt)
+        opt = FlatAdamW(eng, lr=1e-2)
+        if wt:
+            sp = eng.space
+            seen = torch.zeros(sp.param_buf.numel(), dtype=torch.int32)
+            for off, rows, cols, toff, _ in eng._wt_mats.tolist():
+                seen[off:off + rows * cols] += 1
+            for i, shape in enumerate(sp.shapes):
+                n = 1
+                for d in shape:
+                    n *= d
+                o = sp.offsets[i]
+                assert torch.all(seen[o:o + n] == 1), sp.names[i]
+            assert len(eng._wt_views) == 1  # only `a` gets a transposed copy
+        for _ in range(2):
+            opt.zero_grad()
+            eng.backward(m(torch.randn(4, 64)))
+            opt.step()
+        outs[wt] = {n: p.detach().clone() for n, p in m.named_parameters()}
+    for n in outs[False]:
+        assert torch.equal(outs[False][n], outs[True][n]), n
