@@ -11,7 +11,8 @@ import os
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-TABLE = os.path.join(ROOT, "tunableop", "tunableop_results_partial.csv")
+# DTG_TUNABLEOP_TABLE: an alternative table (A/B of pinned solutions, tools/tunableop_variants.py)
+TABLE = os.environ.get("DTG_TUNABLEOP_TABLE") or os.path.join(ROOT, "tunableop", "tunableop_results_partial.csv")
 
 
 def enable_tunableop(tune: bool = False, max_tuning_ms: int = 30, table: str = TABLE):

@@ -52,7 +52,7 @@ def _known(table):
     return {tuple(l.split(",")[:2]) for l in open(table) if l.startswith("Gemm")}
 
 
-def _worker(shapes_file, results_file, max_tuning_ms):
+def _worker(shapes_file, results_file, max_tuning_ms, rotating_mb=0):
     """Tune every shape in shapes_file in order; after each, append its result line (JSON)."""
     # Compare every candidate's output with the default kernel's and drop the ones that differ:
     # without this TunableOp ranks on time alone, and one hipBLASLt solution for GPT-2's batched
@@ -69,6 +69,10 @@ def _worker(shapes_file, results_file, max_tuning_ms):
     t.tuning_enable(True)
     t.set_max_tuning_duration(max_tuning_ms)
     t.set_max_tuning_iterations(50)
+    if rotating_mb > 0:
+        # candidates timed over a rotating set of operand copies larger than the caches: cold
+        # inputs, as in a training step where each GEMM reads what another kernel just wrote
+        t.set_rotating_buffer_size(rotating_mb)
     one = os.path.join(tempfile.gettempdir(), f"dtg_tune_one_{os.getpid()}.csv")
     for line in open(shapes_file).read().splitlines():
         with open(one, "w") as fp:
@@ -90,13 +94,15 @@ def main():
     ap.add_argument("--budget-s", type=float, default=600.0, help="stop starting new shapes after this")
     ap.add_argument("--shape-timeout-s", type=float, default=90.0)
     ap.add_argument("--max-tuning-ms", type=int, default=30)
+    ap.add_argument("--rotating-mb", type=int, default=0, help="TunableOp rotating operand buffer (cold-cache timing)")
+    ap.add_argument("--retune", action="store_true", help="tune shapes even if the committed table has them")
     ap.add_argument("--worker", nargs=2, metavar=("SHAPES", "RESULTS"), help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.worker:
-        return _worker(args.worker[0], args.worker[1], args.max_tuning_ms)
+        return _worker(args.worker[0], args.worker[1], args.max_tuning_ms, args.rotating_mb)
 
     table = args.table or os.path.join(ROOT, "tunableop", "tunableop_results_partial.csv")
-    todo = _shapes(args.untuned, _known(table))
+    todo = _shapes(args.untuned, set() if args.retune else _known(table))
     print(f"[tune_gemms] {len(todo)} new GEMM shapes", flush=True)
     header = [l for l in open(table) if l.startswith("Validator")] if os.path.exists(table) else []
     work = tempfile.mkdtemp(prefix="dtg_tune_")
@@ -110,7 +116,7 @@ def main():
         with open(shapes_file, "w") as fp:
             fp.write("\n".join(todo) + "\n")
         proc = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--worker", shapes_file, results_file,
-                                 "--max-tuning-ms", str(args.max_tuning_ms)])
+                                 "--max-tuning-ms", str(args.max_tuning_ms), "--rotating-mb", str(args.rotating_mb)])
         last = time.time()
         while True:
             time.sleep(1.0)
