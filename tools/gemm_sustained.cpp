@@ -13,8 +13,10 @@
 // spelling) with a short burst, then re-times the best candidates -- plus the library's
 // heuristic default and the best 32x32-MFMA solutions -- under sustained back-to-back load,
 // round-robin so clock drift hits every candidate alike.  It prints one JSON line per
-// candidate; tools/merge_tunableop.py writes the sustained winner into the TunableOp table as
-// "Gemm_Hipblaslt_<index>".
+// candidate.  Caveat: this binary links the system hipBLASLt (/opt/rocm), while PyTorch runs
+// its own bundled copy, whose solution indices differ (TunableOp's Gemm_Hipblaslt_618xxx vs
+// 439xxx here, profiles/r3_s14): rank solutions here, but pin them through TunableOp itself
+// (tools/tune_gemms.py --retune [--rotating-mb]).
 //
 //   hipcc -O2 --offload-arch=gfx950 tools/gemm_sustained.cpp -lhipblaslt -o build/gemm_sustained
 //   build/gemm_sustained tn_28672_16384_4096_ld_4096_4096_28672 [secs_per_round=0.4] [top=12]
