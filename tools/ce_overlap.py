@@ -17,11 +17,10 @@ import glob
 import os
 
 
-def load(d):
+def load(f):
     rows = []
-    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    for r in csv.DictReader(open(f)):
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     return sorted(rows)
 
 
@@ -33,25 +32,29 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     a = ap.parse_args()
-    ks = load(a.dir)
+    # one kernel-trace CSV per process (rocprofv3 -o %pid%_run): each rank analysed on its own
+    for f in sorted(glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)):
+        print(f"== {os.path.relpath(f, a.dir)}")
+        analyse(load(f))
+
+
+def analyse(ks):
     stats = [i for i, k in enumerate(ks) if "ce_stats_kernel" in k[2]]
     grads = [i for i, k in enumerate(ks) if "ce_grad_kernel" in k[2]]
     gemms = [k for k in ks if is_gemm(k[2])]
     print(f"{len(ks)} kernels, {len(stats)} ce_stats, {len(grads)} ce_grad")
     pipelined = total = 0
     overlap_ns = coll_ns = 0
-    for si in stats:
-        s_end = ks[si][1]
-        gi = next((g for g in grads if g > si), None)
-        if gi is None:
+    # the k-th stats kernel belongs to the k-th gradient kernel (chunks run in order); with the
+    # pipeline, stats(j + 1) is issued before grad(j)
+    for k, (si, gi) in enumerate(zip(stats, grads)):
+        if gi < si:
             continue
-        nxt = next((j for j in range(si + 1, len(ks)) if "ce_stats_kernel" in ks[j][2]), None)
         total += 1
-        # the next chunk's GEMM starts before this chunk's gradient kernel
-        if nxt is not None and nxt < gi:
+        if k + 1 < len(stats) and stats[k + 1] < gi:  # (a forward's last chunk has no successor)
             pipelined += 1
         # collective kernels of this chunk: xgmi barrier / gather kernels between stats and grad
-        coll = [k for k in ks[si + 1:gi] if "xgmi" in k[2] or "barrier_kernel" in k[2] or "all_gather_kernel" in k[2]]
+        coll = [c for c in ks[si + 1:gi] if "xgmi" in c[2] or "barrier_kernel" in c[2] or "all_gather_kernel" in c[2]]
         for c0, c1, _ in coll:
             coll_ns += c1 - c0
             for g0, g1, _ in gemms:
