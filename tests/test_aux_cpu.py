@@ -202,3 +202,76 @@ def test_trainer_wandb_every_rank_with_stub_module(tmp_path):
         assert (kw["group"], kw["name"], kw["save_code"]) == ("wb", f"rank-{rank}", True)
         assert kw["dir"].endswith(f"wb/rank-{rank}")
         assert (out / f"log-wb-{rank}.txt").read_text().split() == ["1", "2"]
+
+
+def test_num_layers_flag_builds_reduced_depth():
+    """--num-layers overrides the bundled config's depth (exact-width reduced-depth runs such
+    as chapter 05 at the 405B width, tools/run_405b_gpu.sh); absent, the config's depth."""
+    import torch
+
+    from dtg.train import trainer
+    from dtg.train.cli import get_parser
+
+    for argv, depth in ((["--num-layers", "3"], 3), ([], None)):
+        args = get_parser("01").parse_args(["-e", "x", "-d", "synthetic", "-m", "llama-tiny"] + argv)
+        model = trainer._build(args, "01", torch.device("cpu"), 1)[0]
+        want = depth if depth is not None else trainer.resolve_config("llama-tiny").num_hidden_layers
+        assert len(model.layers) == want
+
+
+def _ch05_log(path, fwd, bwd, upd):
+    lines = []
+    for step in range(1, 7):
+        rec = {"global_step": step, "time/forward": fwd, "time/backward": bwd, "time/update": upd,
+               "time/total": fwd + bwd + upd}
+        lines.append(f"[rank=0] INFO:{rec!r}")
+    path.write_text("\n".join(lines) + "\n")
+
+
+def test_extrapolate_405b_from_depth_logs(tmp_path):
+    """Per-layer costs = (depth 4 - depth 2) / 2 of the chapter-05 phase timers; the projection
+    reports compute-only and the two labelled recipes."""
+    _ch05_log(tmp_path / "ch05_405b_d2_no_offload.log", 82.0, 141.0, 29.7)
+    _ch05_log(tmp_path / "ch05_405b_d4_no_offload.log", 122.2, 275.0, 43.0)
+    _ch05_log(tmp_path / "ch05_405b_d2.log", 82.0, 511.0, 339.0)
+    _ch05_log(tmp_path / "ch05_405b_d4.log", 122.2, 835.0, 602.0)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "extrapolate_405b.py"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout)
+    m = res["measured"]
+    assert abs(m["layer_fwd_ms"] - 20.1) < 0.01 and abs(m["layer_bwd_ms"] - 67.0) < 0.01
+    assert abs(m["compute_only_step_s"] - (126 * 87.1 + 49.2) / 1e3) < 0.02
+    assert res["A_full_shard_offload"]["tok_s_gpu"] < res["B_hybrid_xgmi_optimizer_offload"]["tok_s_gpu"]
+    assert res["reference_tok_s_gpu"] == 136.5
+
+
+def test_ce_overlap_pairs_chunks_in_order(tmp_path):
+    """tools/ce_overlap.py on a synthetic trace of the pipelined vocab-parallel loss head:
+    issue(0) issue(1) finish(0) issue(2) finish(1) finish(2) -> 2 of 3 chunks pipelined."""
+    ev, t = [], 0
+
+    def k(name, dur=10):
+        nonlocal t
+        ev.append((t, t + dur, name))
+        t += dur
+
+    for j in range(2):
+        k("Cijk_gemm_logits")
+        k("dtg::ce_stats_kernel()")
+        k("dtg::xgmi::barrier_kernel()", 1)
+    k("dtg::ce_grad_kernel()")
+    k("Cijk_gemm_logits")
+    k("dtg::ce_stats_kernel()")
+    k("dtg::ce_grad_kernel()")
+    k("dtg::ce_grad_kernel()")
+    d = tmp_path / "trace"
+    d.mkdir()
+    with open(d / "123_run_kernel_trace.csv", "w") as fp:
+        fp.write("Kernel_Name,Start_Timestamp,End_Timestamp\n")
+        for s, e, n in ev:
+            fp.write(f"\"{n}\",{s},{e}\n")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ce_overlap.py"), str(d)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "3 ce_stats, 3 ce_grad" in r.stdout and "2 / 3" in r.stdout, r.stdout
