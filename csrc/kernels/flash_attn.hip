@@ -694,6 +694,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 // double-buffered in LDS.  S and dP start from the row constants
 // (-lse/scale, -delta) so p = exp2(c2 S') and dS = p dP' need no per-element subtraction;
 // only the causal diagonal is masked (padded query rows carry Q = dO = 0 and contribute 0).
+// D = 128 at one wave per SIMD: every value stays in registers (306 of them).  Forced to two
+// waves the allocator spills ~50 dwords per lane to scratch and the kernel runs at half speed
+// (profiles/r3_s20).
 template <int D, bool CAUSAL, int PF, bool WIN = false>
 __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
   constexpr int RB = 2 * D;
