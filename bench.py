@@ -69,6 +69,10 @@ def parse(argv=None):
     ap.add_argument("--fsdp-mem-batch", type=int, default=10)
     ap.add_argument("--fsdp-mem-seq", type=int, default=1024)
     ap.add_argument("--fsdp-mem-steps", type=int, default=3, help="0 skips the FSDP memory phase")
+    ap.add_argument("--fsdp-mem-world", type=int, default=8,
+                    help="run with fewer ranks than this: also measure one rank of a job of this size "
+                         "(tools/fsdp_mem_one_rank.py: the other ranks are a fake process group), the "
+                         "reference's 8-GPU memory row; 0 = off")
     ap.add_argument("--numel-to-wrap", type=int, default=100_000_000)
     # After the timed region, N > 1 only: RCCL reduce-scatter / all-gather / all-reduce bus
     # bandwidth at these message sizes (MiB), so the multi-GPU run also measures the curve the
@@ -237,6 +241,25 @@ def fsdp_memory_phase(args, torch, dist, device, world, rank, cuda):
     return dict(valley=valley, peak=peak, ms=ms, model=cfg.hf_name or args.fsdp_mem_model)
 
 
+def fsdp_mem_one_rank(args):
+    """Valley / peak of ONE rank of an --fsdp-mem-world-rank FSDP job on this GPU: a child process
+    (tools/fsdp_mem_one_rank.py) runs rank 0 with a fake process group for the other ranks --
+    exact allocations, meaningless numerics (validated against real W = 1/2/4 runs,
+    profiles/r3_s22/).  Returns the child's JSON record, or None if it failed."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "fsdp_mem_one_rank.py"), "--world", str(args.fsdp_mem_world),
+           "--model", args.fsdp_mem_model, "--batch", str(args.fsdp_mem_batch), "--seq", str(args.fsdp_mem_seq),
+           "--numel-to-wrap", str(args.numel_to_wrap), "--steps", str(max(2, args.fsdp_mem_steps))]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        if r.returncode == 0 and lines:
+            return json.loads(lines[-1])
+        print(f"[bench] fsdp one-rank memory run failed ({r.returncode}): {r.stderr[-500:]}", file=sys.stderr)
+    except subprocess.TimeoutExpired:
+        print("[bench] fsdp one-rank memory run timed out", file=sys.stderr)
+    return None
+
+
 def collective_sweep(args, torch, dist, device, world, cuda):
     """[{op, mib, us, busbw_gbs}] measured on every rank (rank 0's numbers reported), nccl-tests
     bus-bandwidth conventions: reduce-scatter / all-gather x (W-1)/W, all-reduce x 2(W-1)/W."""
@@ -327,6 +350,10 @@ def main(argv=None):
     if args.fsdp_mem_steps > 0:
         mem = fsdp_memory_phase(args, torch, dist, device, world, rank, cuda)
         gc.collect()
+    mem_one = None
+    if args.fsdp_mem_steps > 0 and cuda and rank == 0 and world < args.fsdp_mem_world:
+        torch.cuda.empty_cache()
+        mem_one = fsdp_mem_one_rank(args)
 
     # per-rank facts, gathered to rank 0: elapsed, device ordinal, PCI bus, peaks
     me = [res["elapsed"], float(dev_idx), float(res["peak_gb"]),
@@ -391,6 +418,11 @@ def main(argv=None):
                                "ms_per_step": round(max(r[5] for r in rows), 1),
                                "reference_a100x8": {"valley_gb": 8, "peak_gb": 74}}
             rec["fsdp_peak_mem_gb"] = rec["fsdp_mem"]["peak_gb_max_rank"]
+        if mem_one is not None:
+            rec["fsdp_mem_one_rank_of_w"] = {"world": mem_one["world"], "valley_gb": mem_one["valley_gib"],
+                                             "peak_gb": mem_one["peak_gib"], "method": "rank 0 alone, other ranks a "
+                                             "fake process group (tools/fsdp_mem_one_rank.py)",
+                                             "reference_a100x8": {"valley_gb": 8, "peak_gb": 74}}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()
