@@ -36,6 +36,13 @@ def init_distributed(backend: Optional[str] = None, timeout_minutes: int = 30, l
     """Initialise torch.distributed from launcher env. Returns (rank, local_rank, world_size, device)."""
     rank = _env_int("RANK", "OMPI_COMM_WORLD_RANK", "SLURM_PROCID", "PMI_RANK", default=0)
     world = _env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "SLURM_NTASKS", "PMI_SIZE", default=1)
+    # DTG_FAKE_WORLD=W (one process, no launcher): run as rank 0 of a W-rank job whose other ranks
+    # are PyTorch's `fake` process group -- every collective returns at once with its output
+    # untouched.  Shard sizes, gathered buffers, allocations and per-rank compute are those of a
+    # real W-rank job; the numerics are not (a memory / per-rank-compute rehearsal only).
+    fake_world = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0)
+    if fake_world > 1:
+        rank, world = 0, fake_world
     local_rank = local_rank_arg if local_rank_arg is not None else _env_int(
         "LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID", "MPI_LOCALRANKID", default=None)
     cuda = torch.cuda.is_available()
@@ -53,6 +60,12 @@ def init_distributed(backend: Optional[str] = None, timeout_minutes: int = 30, l
     device = torch.device("cuda:0" if shared else f"cuda:{local_rank}") if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(device)
+    if fake_world > 1 and not dist.is_initialized():
+        from torch.testing._internal.distributed.fake_pg import FakeStore
+
+        os.environ["RANK"], os.environ["WORLD_SIZE"], os.environ["LOCAL_RANK"] = "0", str(world), "0"
+        dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=world)
+        return 0, 0, world, torch.device("cuda:0") if cuda else torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         backend = backend or ("nccl" if cuda and not shared else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(minutes=timeout_minutes))
