@@ -275,3 +275,18 @@ def test_ce_overlap_pairs_chunks_in_order(tmp_path):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     assert "3 ce_stats, 3 ce_grad" in r.stdout and "2 / 3" in r.stdout, r.stdout
+
+
+def test_fake_world_runs_one_rank_of_a_larger_job(tmp_path):
+    """DTG_FAKE_WORLD=W: chapter 05 (FSDP + AC + offload) runs as rank 0 of a W-rank job with a
+    fake process group for the others; the shard is 1/W of the model (memory / per-rank compute
+    rehearsal; numerics not meaningful)."""
+    env = dict(os.environ, DTG_FAKE_WORLD="8", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "train_llm.py", "-e", "fw", "-m", "llama-tiny", "-b", "1", "-s", "64", "-d", "synthetic",
+           "--save-dir", str(tmp_path), "--ckpt-freq", "1000", "--max-steps", "2", "--log-freq", "1",
+           "--num-workers", "0"]
+    r = subprocess.run(cmd, cwd=os.path.join(ROOT, "05-training-llama-405b"), env=env, capture_output=True,
+                       text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "'global_step': 2" in out, out[-3000:]
