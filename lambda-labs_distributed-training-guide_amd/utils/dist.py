@@ -64,6 +64,8 @@ def init_distributed(backend: Optional[str] = None, timeout_minutes: int = 30, l
         from torch.testing._internal.distributed.fake_pg import FakeStore
 
         os.environ["RANK"], os.environ["WORLD_SIZE"], os.environ["LOCAL_RANK"] = "0", str(world), "0"
+        # one node = 8 GPUs (chapter 06's TP degree, HYBRID's shard group)
+        os.environ["LOCAL_WORLD_SIZE"] = str(min(world, int(os.environ.get("DTG_FAKE_NODE_GPUS", "8"))))
         dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=world)
         return 0, 0, world, torch.device("cuda:0") if cuda else torch.device("cpu")
     if world > 1 and not dist.is_initialized():
