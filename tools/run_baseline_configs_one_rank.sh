@@ -18,7 +18,7 @@ run() {  # name dir args...
   echo "$name rc=$rc: $(grep -E "global_step': 8," $O/$name.log | grep -oE "'(tok/s|tok/s/gpu|peak_alloc_gb|peak_alloc_in_gb|time/forward|time/backward|time/update)': [0-9.]+" | tr '\n' ' ')"
   [ $rc -eq 0 ] || { tail -30 $O/$name.log; exit $rc; }
 }
-#run ch02_ddp_w8 02-distributed-data-parallel -m meta-llama/Meta-Llama-3-8B -b 16
-#run ch04_fsdp_w8 04-fully-sharded-data-parallel -m meta-llama/Meta-Llama-3-8B -b 16
+run ch02_ddp_w8 02-distributed-data-parallel -m meta-llama/Meta-Llama-3-8B -b 16
+run ch04_fsdp_w8 04-fully-sharded-data-parallel -m meta-llama/Meta-Llama-3-8B -b 16
 run ch06_tp8 06-tensor-parallel -m meta-llama/Llama-3.1-8B -b 16
-#run ch07_tp4dp2 07-2d-parallel -m meta-llama/Llama-3.1-8B -b 16 --tp 4
+run ch07_tp4dp2 07-2d-parallel -m meta-llama/Llama-3.1-8B -b 16 --tp 4
