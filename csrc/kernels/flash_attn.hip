@@ -466,6 +466,11 @@ struct BwdParams {
   float scale, c2;
   const int *kstart, *klen;  // optional per-sequence key ranges (see KeyRange)
   int window;                // causal sliding window, as FwdParams::window
+  // dK/dV with the query items of each key block split over `nsplit` workgroups (grids too small
+  // for the chip: one KV head per TP rank): f32 partials [nsplit, T, Hkv, D], summed in split
+  // order by bwd_kv_combine_kernel (deterministic).  nsplit <= 1: bf16 dK / dV written directly.
+  float *dk_part, *dv_part;
+  int nsplit;
 };
 
 constexpr int kDqBQ = 128;  // query rows per workgroup (4 waves x 32)
@@ -712,7 +717,9 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
   const int seqlen = P.cu[seq + 1] - s0;
   const KeyRange kr = key_range(P.kstart, P.klen, seq, s0, seqlen);
   const int klen = kr.len, koff_c = kr.off;  // query q attends key k iff k <= q + koff_c
-  const int kb = blockIdx.z * kKvBK;  // z = 0 first: the heaviest causal key blocks
+  const int nsplit = P.nsplit > 1 ? P.nsplit : 1;
+  const int split = blockIdx.z % nsplit;
+  const int kb = (blockIdx.z / nsplit) * kKvBK;  // z = 0 first: the heaviest causal key blocks
   if (kb >= klen) return;
   const int group = P.hq / P.hkv;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -874,14 +881,16 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     }
     if (it < nitems) step(it, std::integral_constant<int, 0>{});
   } else {
-    if (nitems > 0) {
-      load_item(ia, 0);
-      store_item(ia, 0);
+    // this workgroup's share of the key block's items (all of them unless split)
+    const int it0 = (int)((int64_t)split * nitems / nsplit), it1 = (int)((int64_t)(split + 1) * nitems / nsplit);
+    if (it0 < it1) {
+      load_item(ia, it0);
+      store_item(ia, it0 & 1);
     }
     __syncthreads();
-    for (int it = 0; it < nitems; ++it) {
+    for (int it = it0; it < it1; ++it) {
       const int buf = it & 1;
-      const bool more = it + 1 < nitems;
+      const bool more = it + 1 < it1;
       if (more) load_item(ia, it + 1);
       compute(it, buf);
       if (more) store_item(ia, buf ^ 1);
@@ -890,8 +899,60 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
   }
 
   const int64_t krow = kr.start + min(key, klen - 1);
+  if (nsplit > 1) {  // f32 partials (lane = key row; registers = columns 32d + 8g + 4h + e)
+    if (key < klen) {
+      const int64_t o = (((int64_t)split * P.T + krow) * P.hkv + kvh) * D + 4 * h;
+      float* pk = P.dk_part + o;
+      float* pv = P.dv_part + o;
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          *reinterpret_cast<f32x4*>(pk + 32 * d + 8 * g) = f32x4{dk[d][4 * g], dk[d][4 * g + 1], dk[d][4 * g + 2], dk[d][4 * g + 3]};
+          *reinterpret_cast<f32x4*>(pv + 32 * d + 8 * g) = f32x4{dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]};
+        }
+      }
+    }
+    return;
+  }
   store_rows_wide<ND>(dk, P.scale, P.dk + krow * P.sdk + (int64_t)kvh * D, key < klen);
   store_rows_wide<ND>(dv, 1.f, P.dv + krow * P.sdv + (int64_t)kvh * D, key < klen);
+}
+
+// dK = scale * sum_s dk_part[s], dV = sum_s dv_part[s] in split order, to bf16 [T, Hkv, D] views
+// (token strides sdk / sdv).  One lane per 8 consecutive elements of a (token, head) row.
+template <int D>
+__global__ __launch_bounds__(256) void bwd_kv_combine_kernel(const float* __restrict__ dk_part,
+                                                             const float* __restrict__ dv_part, int nsplit,
+                                                             int64_t T, int hkv, float scale, uint16_t* __restrict__ dk,
+                                                             int64_t sdk, uint16_t* __restrict__ dv, int64_t sdv) {
+  constexpr int V = D / 8;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // vector index
+  const int64_t rows = T * hkv;
+  if (i >= rows * V) return;
+  const int64_t row = i / V;
+  const int c = (int)(i % V) * 8;
+  const int64_t t = row / hkv;
+  const int hh = (int)(row % hkv);
+  float a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+  for (int sp = 0; sp < nsplit; ++sp) {
+    const int64_t o = ((int64_t)sp * rows + row) * D + c;
+    const f32x4 k0 = *reinterpret_cast<const f32x4*>(dk_part + o), k1 = *reinterpret_cast<const f32x4*>(dk_part + o + 4);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(dv_part + o), v1 = *reinterpret_cast<const f32x4*>(dv_part + o + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] += k0[j];
+      a[4 + j] += k1[j];
+      b[j] += v0[j];
+      b[4 + j] += v1[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] *= scale;
+  store8(dk + t * sdk + (int64_t)hh * D + c, a);
+  store8(dv + t * sdv + (int64_t)hh * D + c, b);
 }
 
 }  // namespace fa
@@ -996,8 +1057,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_fwd_stamped(const at::
 
 static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen, int64_t hq, int nseq,
                           hipStream_t st, bool pre_delta);
-static void launch_bwd_dkdv(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
-                            int nseq, hipStream_t st);
+static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
+                            int nseq, hipStream_t st, const at::Tensor& dk_t, const at::Tensor& dv_t);
 
 // Shared backward driver: outputs are [T, H, D] views (contiguous heads, any token stride).
 static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, const at::Tensor& k,
@@ -1071,13 +1132,13 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
     DTG_CHECK(hipEventRecord(ev_fork, main_st) == hipSuccess, "flash_attn: event record");
     DTG_CHECK(hipStreamWaitEvent(dq_st, ev_fork, 0) == hipSuccess, "flash_attn: stream wait");
     launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, dq_st, true);
-    launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, main_st);
+    launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, main_st, dk, dv);
     DTG_CHECK(hipEventRecord(ev_join, dq_st) == hipSuccess, "flash_attn: event record");
     DTG_CHECK(hipStreamWaitEvent(main_st, ev_join, 0) == hipSuccess, "flash_attn: stream wait");
     return;
   }
   launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, main_st, false);
-  launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, main_st);
+  launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, main_st, dk, dv);
 }
 
 static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen, int64_t hq, int nseq,
@@ -1106,8 +1167,8 @@ static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_
   }
 }
 
-static void launch_bwd_dkdv(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
-                            int nseq, hipStream_t st) {
+static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
+                            int nseq, hipStream_t st, const at::Tensor& dk_t, const at::Tensor& dv_t) {
   // Items the dK/dV kernel stages ahead (DTG_FA_KV_PF=1|2).  Equal on MI355X once the kernel's
   // false vmcnt waits were gone (bwd 0.767 vs 0.768 ms at the 8B shape, profiles/r1_s51_*), so
   // the single-set form with fewer registers is the default.
@@ -1115,8 +1176,28 @@ static void launch_bwd_dkdv(const fa::BwdParams& P, int64_t D, bool causal, int6
     const char* e = std::getenv("DTG_FA_KV_PF");
     return (e != nullptr && e[0] == '2') ? 2 : 1;
   }();
+  // Split the query items of each key block over several workgroups when the grid cannot fill
+  // the chip (e.g. TP = 8: one KV head per rank -> 16 x 8 workgroups for 256 CUs): aim for
+  // >= 2 workgroups per CU.  DTG_FA_KV_SPLIT = N forces N (1 = off); read per call (A/B).
+  const int nkb = (int)((max_seqlen_k + fa::kKvBK - 1) / fa::kKvBK);
+  const int64_t wgs = (int64_t)hkv * nseq * nkb;
+  int nsplit = 1;
+  const char* se = std::getenv("DTG_FA_KV_SPLIT");
+  if (se != nullptr && std::atoi(se) > 0) nsplit = std::min(8, std::atoi(se));
+  else if (wgs > 0 && wgs < 512) nsplit = (int)std::min<int64_t>(4, (512 + wgs - 1) / wgs);
+  at::Tensor dk_part, dv_part;
+  if (nsplit > 1 && P.kstart == nullptr && P.window == 0 && kv_pf == 1) {
+    dk_part = at::empty({nsplit, P.T, hkv, D}, dk_t.options().dtype(at::kFloat));
+    dv_part = at::empty({nsplit, P.T, hkv, D}, dk_t.options().dtype(at::kFloat));
+    P.dk_part = dk_part.data_ptr<float>();
+    P.dv_part = dv_part.data_ptr<float>();
+    P.nsplit = nsplit;
+  } else {
+    nsplit = 1;
+    P.nsplit = 1;
+  }
   {
-    dim3 grid(hkv, nseq, (max_seqlen_k + fa::kKvBK - 1) / fa::kKvBK);
+    dim3 grid(hkv, nseq, nkb * nsplit);
     const size_t lds = 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
 #define DTG_BWD_KV(DD, C, PF, ...)                                                        \
   do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>, lds);      \
@@ -1131,6 +1212,16 @@ static void launch_bwd_dkdv(const fa::BwdParams& P, int64_t D, bool causal, int6
       else { if (causal) DTG_BWD_KV(64, true, 1); else DTG_BWD_KV(64, false, 1); }
     }
 #undef DTG_BWD_KV
+    DTG_LAUNCH_CHECK();
+  }
+  if (nsplit > 1) {
+    const int64_t nv = P.T * hkv * (D / 8);
+    if (D == 128)
+      fa::bwd_kv_combine_kernel<128><<<(nv + 255) / 256, 256, 0, st>>>(P.dk_part, P.dv_part, nsplit, P.T, (int)hkv,
+                                                                      P.scale, P.dk, P.sdk, P.dv, P.sdv);
+    else
+      fa::bwd_kv_combine_kernel<64><<<(nv + 255) / 256, 256, 0, st>>>(P.dk_part, P.dv_part, nsplit, P.T, (int)hkv,
+                                                                     P.scale, P.dk, P.sdk, P.dv, P.sdv);
     DTG_LAUNCH_CHECK();
   }
 }

@@ -357,6 +357,31 @@ def test_flash_attn_fwd_variants(cuda, variant, causal, monkeypatch):
     _attn_case(cuda, [1024, 77], hq=4, hkv=2, D=128, causal=causal, qscale=8.0)
 
 
+@pytest.mark.parametrize("split", ["1", "2", "4"])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attn_bwd_kv_split(cuda, split, causal, monkeypatch):
+    """dK/dV with each key block's query items split over workgroups (f32 partials summed in
+    split order, DTG_FA_KV_SPLIT): matches the fp32 reference, is bitwise reproducible, and the
+    single-GPU default (no split) is unchanged."""
+    monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
+    qkv, cu = _attn_case(cuda, [1024, 77, 300], hq=8, hkv=2, D=128, causal=causal, stride_extra=8)
+    T, D, hq, hkv = qkv.shape[0], 128, 8, 2
+    g = qkv.to(cuda)
+    q, k, v = (g[:, a * D:b * D].view(T, b - a, D) for a, b in ((0, hq), (hq, hq + hkv), (hq + hkv, hq + 2 * hkv)))
+    o, lse = dops.flash_attn_fwd(q, k, v, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    torch.manual_seed(3)
+    do = torch.randn(T, hq, D, device=cuda).bfloat16()
+    a = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    b = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    monkeypatch.setenv("DTG_FA_KV_SPLIT", "1")
+    ref = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    assert torch.equal(a[0], ref[0])  # dQ is not affected
+    for x, y in zip(a[1:], ref[1:]):
+        assert _rel(x, y) < 1e-2
+
+
 @pytest.mark.parametrize("window", [2, 64, 200, 5000])
 @pytest.mark.parametrize("D,hq,hkv", [(128, 8, 2), (64, 4, 4)])
 def test_flash_attn_sliding_window(cuda, window, D, hq, hkv):

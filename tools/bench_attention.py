@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--ab-bwd", default=None,
                     help="VAR=v1,v2 (e.g. DTG_FA_OCC=1,2): backward timed under each value of the environment "
                          "knob in interleaved rounds in ONE process, medians reported, outputs compared bitwise")
+    ap.add_argument("--ab-tolerant", action="store_true",
+                    help="--ab-bwd variants that change the summation order: compare within 1e-2 relative")
     a = ap.parse_args()
     if a.ab_bwd:
         var, vals = a.ab_bwd.split("=", 1)
@@ -117,6 +119,7 @@ def ab_bwd(a, var, variants, rounds=7):
     import statistics
 
     cases = [("S1024c", dict(B=16, S=1024, hq=32, hkv=8, d=128, docs=None), True),
+             ("S1024c-tp8", SHAPES["llama8b-tp8"], True), ("S1024c-tp4", dict(B=16, S=1024, hq=8, hkv=2, d=128, docs=None), True),
              ("S4096c", dict(B=4, S=4096, hq=32, hkv=8, d=128, docs=None), True),
              ("S8192nc", dict(B=2, S=8192, hq=32, hkv=8, d=128, docs=None), False),
              ("rime", SHAPES["rime"], True)]
@@ -136,8 +139,11 @@ def ab_bwd(a, var, variants, rounds=7):
                     g = ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, causal)
                 if ref is None:
                     ref = g.clone()
-                elif r == 0:
+                elif r == 0 and not a.ab_tolerant:
                     assert torch.equal(g, ref), (name, vv, (g.float() - ref.float()).abs().max().item())
+                elif r == 0:
+                    err = ((g.float() - ref.float()).norm() / ref.float().norm().clamp_min(1e-12)).item()
+                    assert err < 1e-2, (name, vv, err)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
@@ -145,7 +151,7 @@ def ab_bwd(a, var, variants, rounds=7):
                 e1.record()
                 torch.cuda.synchronize()
                 times[vv].append(e0.elapsed_time(e1) / a.iters)
-        rec = {"case": name, "bitwise_equal": True}
+        rec = {"case": name, "bitwise_equal": not a.ab_tolerant}
         for vv in variants:
             med = statistics.median(times[vv])
             rec[vv] = {"ms": round(med, 4), "min_ms": round(min(times[vv]), 4), "TFLOPs": round(2.5 * flops / med / 1e9, 1)}
