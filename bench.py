@@ -187,8 +187,9 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
                 fp.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
     res = dict(elapsed=elapsed, peak_gb=peak_gb, loss=float(loss.item()), cfg=cfg,
                mode=getattr(engine, "mode", args.parallel), dp=dp_size)
-    if not math.isfinite(res["loss"]):
+    if not math.isfinite(res["loss"]) and int(os.environ.get("DTG_FAKE_WORLD", "0") or 0) <= 1:
         # a step that produced NaN/inf (e.g. a wrong GEMM solution) is not a measurement
+        # (a fake-world rehearsal computes on buffers no collective filled: its loss means nothing)
         raise SystemExit(f"bench.py: rank {rank} final loss is {res['loss']}; refusing to report a throughput")
     if hasattr(engine, "wait_param_gather"):
         engine.wait_param_gather()
@@ -295,7 +296,11 @@ def collective_sweep(args, torch, dist, device, world, cuda):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    # DTG_FAKE_WORLD=N: rehearsal of rank 0 of an N-rank job on one GPU; the other ranks are
+    # PyTorch's fake process group (collectives return at once).  Shapes, shard layouts, kernels
+    # and memory are those of the real N-rank job; the time excludes communication and is labelled.
+    fake_world = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and fake_world <= 1:
         return self_launch(args, argv)
 
     import gc
@@ -319,6 +324,9 @@ def main(argv=None):
                 print(f"[bench] tuning GEMMs... {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
 
         threading.Thread(target=_heartbeat, daemon=True).start()
+    if fake_world > 1:
+        os.environ.update(WORLD_SIZE=str(fake_world), RANK="0", LOCAL_RANK="0",
+                          LOCAL_WORLD_SIZE=str(min(fake_world, 8)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -334,7 +342,12 @@ def main(argv=None):
     if cuda:
         torch.cuda.set_device(device)
     backend = None
-    if world > 1:
+    if world > 1 and fake_world > 1:
+        from torch.testing._internal.distributed.fake_pg import FakeStore
+
+        backend = "fake"
+        dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=world)
+    elif world > 1:
         backend = args.backend or ("nccl" if cuda else "gloo")
         dist.init_process_group(backend, device_id=device if (cuda and backend == "nccl") else None)
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
@@ -345,7 +358,7 @@ def main(argv=None):
     gc.collect()
     if cuda:
         torch.cuda.empty_cache()
-    coll = collective_sweep(args, torch, dist, device, world, cuda) if (world > 1 and args.coll_sweep_mb) else None
+    coll = collective_sweep(args, torch, dist, device, world, cuda) if (world > 1 and fake_world <= 1 and args.coll_sweep_mb) else None
     mem = None
     if args.fsdp_mem_steps > 0:
         mem = fsdp_memory_phase(args, torch, dist, device, world, rank, cuda)
@@ -359,7 +372,9 @@ def main(argv=None):
     me = [res["elapsed"], float(dev_idx), float(res["peak_gb"]),
           mem["valley"] if mem else 0.0, mem["peak"] if mem else 0.0, mem["ms"] if mem else 0.0]
     mine = torch.tensor(me, dtype=torch.float64, device=device)
-    if world > 1:
+    if world > 1 and fake_world > 1:
+        rows = [mine.cpu().tolist()]  # the other ranks do not exist
+    elif world > 1:
         allv = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allv, mine)
         rows = [v.cpu().tolist() for v in allv]
@@ -400,7 +415,7 @@ def main(argv=None):
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
             "peak_mem_gb": round(max(r[2] for r in rows), 2),
-            "final_loss": round(res["loss"], 4),
+            "final_loss": round(res["loss"], 4) if math.isfinite(res["loss"]) else None,
             "world_size_seen_by_pg": pg_world,
             "backend": backend or "none",
             "rank_devices": [int(r[1]) for r in rows],
@@ -408,7 +423,11 @@ def main(argv=None):
             "rank_ms_per_step": {"max": round(1000 * elapsed / args.steps, 2),
                                  "min": round(1000 * min(r[0] for r in rows) / args.steps, 2)},
         }
-        if coll is not None:
+        if fake_world > 1:
+            rec["metric"] = "REHEARSAL (not a measurement of the job): " + METRIC
+            rec["rehearsal"] = (f"rank 0 of a {world}-rank job alone on one GPU, other ranks a fake process "
+                                "group: communication not included, value = one rank's compute rate x world")
+        if coll is not None and fake_world <= 1:
             rec["collectives"] = coll
         if mem is not None:
             rec["fsdp_mem"] = {"model": mem["model"], "batch_per_gpu": args.fsdp_mem_batch,

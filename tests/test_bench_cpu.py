@@ -97,3 +97,23 @@ def test_bench_tensor_parallel_two_ranks():
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 2
     assert rec["config"]["parallelism"] == "dp1-single-tp2-gloo"  # TP collectives on the PG backend
     assert abs(rec["value"] - 2 * 64 * 2 / (rec["ms_per_step"] * 2 / 1000)) < 0.02 * rec["value"]
+
+
+@pytest.mark.slow
+def test_bench_fake_world_rehearsal_is_labelled():
+    """DTG_FAKE_WORLD=8: rank 0 of the 8-rank job alone (fake process group for the others).
+    The line is labelled a rehearsal, carries no collective sweep, and its tokens/s counts
+    8 ranks' worth of batches."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="2", DTG_FAKE_WORLD="8")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"] + ARGS,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["metric"].startswith("REHEARSAL") and "fake process group" in rec["rehearsal"]
+    assert rec["backend"] == "fake" and rec["world_size_seen_by_pg"] == 8 and rec["rank_devices"] == [0]
+    assert rec["config"]["global_batch"] == 16 and rec["config"]["parallelism"] == "dp8-zero"
+    assert "collectives" not in rec
+    assert abs(rec["value"] - 8 * 2 * 64 * 2 / (rec["ms_per_step"] * 2 / 1000)) < 0.02 * rec["value"]
