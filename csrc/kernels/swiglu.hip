@@ -162,10 +162,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& dh
   if (T == 0 || I == 0) return {dgu, dguT, hT};
   // DTG_SWIGLU_TILE = TTxTF (64x64 | 64x128 | 128x64 | 128x128): token x feature tile (A/B knob;
   // read per call so tests and benchmarks switch it in-process)
+  // Default 64 x 128: -2.1 ms per 8B step against 64 x 64, three alternating same-box pairs
+  // (profiles/r3_s32; the parser had dropped "64x128" before, so round 3's first A/B never ran it).
   const char* te = std::getenv("DTG_SWIGLU_TILE");
-  int tt = 64, tf = 64;
+  int tt = 64, tf = 128;
   if (te) {
     if (!std::strcmp(te, "64x64")) tt = 64, tf = 64;
+    else if (!std::strcmp(te, "64x128")) tt = 64, tf = 128;
     else if (!std::strcmp(te, "128x64")) tt = 128, tf = 64;
     else if (!std::strcmp(te, "128x128")) tt = 128, tf = 128;
   }

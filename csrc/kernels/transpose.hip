@@ -68,10 +68,8 @@ at::Tensor transpose2d(const at::Tensor& x) {
   const c10::DeviceGuard g(x.device());
   auto out = at::empty({C, R}, x.options());
   if (R == 0 || C == 0) return out;
-  static const int tile = [] {
-    const char* e = std::getenv("DTG_TRANSPOSE_TILE");
-    return e ? std::atoi(e) : 64;
-  }();
+  const char* te = std::getenv("DTG_TRANSPOSE_TILE");  // per call: tests and A/B runs switch it in-process
+  const int tile = te ? std::atoi(te) : 64;
   const int gc = tile_group_env(kDefaultTileGroup);
   if (tile == 64) {
     const dim3 grid = tile_grid(gc, (R + 63) / 64, (C + 63) / 64);

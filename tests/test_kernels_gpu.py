@@ -82,10 +82,12 @@ def test_swiglu(cuda):
     _close(dops.swiglu_bwd(dh.to(cuda), gu.to(cuda)), dops.swiglu_bwd(dh, gu), 3e-2, 2e-2, "swiglu bwd")
 
 
+@pytest.mark.parametrize("tile", ["64", "128"])
 @pytest.mark.parametrize("group", ["0", "3", "16"])
 @pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (4096, 6144, 6144), (1000, 520, 528), (8, 8, 8), (136, 7000, 7000)])
-def test_transpose2d(cuda, R, C, ld, group, monkeypatch):
+def test_transpose2d(cuda, R, C, ld, group, tile, monkeypatch):
     monkeypatch.setenv("DTG_TILE_GROUP", group)  # 2-D grid, and banded 1-D grids (ragged last band)
+    monkeypatch.setenv("DTG_TRANSPOSE_TILE", tile)
     x = torch.randn(R, ld).bfloat16()[:, :C]
     y = dops.transpose2d(x.to(cuda))
     assert y.shape == (C, R) and y.is_contiguous()

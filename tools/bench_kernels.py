@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--inter", type=int, default=14336)
     ap.add_argument("--params", type=float, default=8.03e9, help="AdamW buffer length")
     ap.add_argument("--layers", type=int, default=8, help="decoder layers of matrices for adamw_t_")
-    ap.add_argument("--only", default="", help="run only the cases whose name contains this")
+    ap.add_argument("--only", default="", help="run only the cases whose name contains one of these (comma-separated)")
     a = ap.parse_args()
     import torch
 
@@ -56,12 +56,19 @@ def main():
         "add_rmsnorm_fwd": (lambda: ops.add_rmsnorm_fwd(x, res, w, 1e-5), 4 * T * H * E),
         "rmsnorm_bwd(+dres)": (lambda: ops.rmsnorm_bwd(dy, hh, w, rstd, dy), 4 * T * H * E),
         "swiglu_fwd": (lambda: ops.swiglu_fwd(gu), 3 * T * I * E),
-        **{f"swiglu_bwd_t (dgu, dgu^T, h^T) tile {tl}": (lambda tl=tl: (os.environ.__setitem__("DTG_SWIGLU_TILE", tl),
-                                                                       ops.swiglu_bwd_t(dh, gu)), (3 + 5) * T * I * E)
-           for tl in ("64x64", "64x128", "128x64", "128x128")},
-        "transpose [T,H]": (lambda: ops.transpose2d(x), 2 * T * H * E),
-        "transpose [T,2I]": (lambda: ops.transpose2d(gu), 2 * T * 2 * I * E),
     }
+    # A/B pairs run twice in alternating order (A B A B) against clock drift
+    for rep in (1, 2):
+        for tl in ("64x64", "64x128", "128x64", "128x128"):
+            cases[f"swiglu_bwd_t (dgu, dgu^T, h^T) tile {tl} #{rep}"] = (
+                lambda tl=tl: (os.environ.__setitem__("DTG_SWIGLU_TILE", tl), ops.swiglu_bwd_t(dh, gu)),
+                (3 + 5) * T * I * E)
+        for tt in ("64", "128"):
+            def tr(src, tt=tt):
+                os.environ["DTG_TRANSPOSE_TILE"] = tt
+                return ops.transpose2d(src)
+            cases[f"transpose [T,H] tile {tt} #{rep}"] = (lambda tr=tr: tr(x), 2 * T * H * E)
+            cases[f"transpose [T,2I] tile {tt} #{rep}"] = (lambda tr=tr: tr(gu), 2 * T * 2 * I * E)
     n = int(a.params) // 16 * 16
     n = min(n, 2_000_000_000)  # keep the AdamW buffers at <= 14 GB
     p = torch.randn(n, **bf)
@@ -96,7 +103,7 @@ def main():
             runs["adamw_t_ 64x128 tile walk, no W^T"] = (lambda: ops.adamw_t_(
                 pw, None, gw, mw, vw, ptw, mats_nt, tile0, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0, None, tc), 14 * nt)
         for name, (fn, nbytes) in runs.items():
-            if a.only and a.only not in name:
+            if a.only and not any(o in name for o in a.only.split(',')):
                 continue
             ms = timeit(torch, fn)
             print(json.dumps({"kernel": name, "ms": round(ms, 4), "bytes": nbytes, "TBps": round(nbytes / ms / 1e9, 2)}),
@@ -104,7 +111,7 @@ def main():
         del pw, gw, mw, vw, ptw, runs
         torch.cuda.empty_cache()
     for name, (fn, nbytes) in cases.items():
-        if a.only and a.only not in name:
+        if a.only and not any(o in name for o in a.only.split(',')):
             continue
         ms = timeit(torch, fn)
         print(json.dumps({"kernel": name, "ms": round(ms, 4), "bytes": nbytes, "TBps": round(nbytes / ms / 1e9, 2)}),
