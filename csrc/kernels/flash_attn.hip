@@ -702,15 +702,20 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 // D = 128 at one wave per SIMD: every value stays in registers (306 of them).  Forced to two
 // waves the allocator spills ~50 dwords per lane to scratch and the kernel runs at half speed
 // (profiles/r3_s20).
-template <int D, bool CAUSAL, int PF, bool WIN = false>
+// QB: query rows per item, 32 or 64.  QB = 64 runs each item as two 32-row halves in a software
+// pipeline (S/dP MFMAs of half 1 under the softmax VALU of half 0, dK/dV MFMAs of half 0 under
+// the softmax of half 1): at one wave per SIMD there is no partner wave to fill the matrix pipe
+// while a wave does its VALU, so the overlap has to come from the wave's own instruction stream.
+template <int D, bool CAUSAL, int PF, bool WIN = false, int QB = kKvBQ>
 __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
+  static_assert(QB == 32 || QB == 64, "query rows per item");
   constexpr int RB = 2 * D;
   constexpr int NC = D / 16;
   constexpr int ND = D / 32;
-  constexpr int SLICE = kKvBQ * RB;
+  constexpr int SLICE = QB * RB;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [Q0 | dO0 | Q1 | dO1 | rowc]
   char* qd = smem;
-  float* rowc = reinterpret_cast<float*>(qd + 4 * SLICE);      // [2][-lse/scale x32, -delta x32]
+  float* rowc = reinterpret_cast<float*>(qd + 4 * SLICE);      // [2][-lse/scale x QB, -delta x QB]
 
   const int seq = blockIdx.y, kvh = blockIdx.x;
   const int s0 = P.cu[seq];
@@ -747,10 +752,10 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     dv[i] = f32x16{};
   }
 
-  const int first_slice = CAUSAL ? (max(0, kb - koff_c) / kKvBQ) : 0;
+  const int first_slice = CAUSAL ? (max(0, kb - koff_c) / QB) : 0;
   const int win = (CAUSAL && WIN) ? P.window : 0;  // sliding window: the last query that sees this block
-  const int end_slice = win > 0 ? min((seqlen + kKvBQ - 1) / kKvBQ, (kb + kKvBK - 1 - koff_c + win - 1) / kKvBQ + 1)
-                                : (seqlen + kKvBQ - 1) / kKvBQ;
+  const int end_slice = win > 0 ? min((seqlen + QB - 1) / QB, (kb + kKvBK - 1 - koff_c + win - 1) / QB + 1)
+                                : (seqlen + QB - 1) / QB;
   const int per_head = max(0, end_slice - first_slice);
   const int nitems = per_head * group;
   const float inv_scale = 1.f / P.scale;
@@ -759,13 +764,13 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
   // use, so its global loads have a whole item of compute to land in (PF = 1: one set, loads
   // issued one item ahead and waited for at the end of the current item).
   struct Item {
-    Stager<kKvBQ, D, 256> q, dout;
-    uint32_t lse, dlt;  // raw f32 bits of this lane's row (lane & 31)
+    Stager<QB, D, 256> q, dout;
+    uint32_t lse, dlt;  // raw f32 bits of this lane's row (threadIdx.x & (QB - 1))
   };
   Item ia, ib;
   auto load_item = [&](Item& X, int it) {
     const int hqi = kvh * group + it / per_head;
-    const int qs = (first_slice + it % per_head) * kKvBQ;
+    const int qs = (first_slice + it % per_head) * QB;
     const int nv = seqlen - qs;
     X.q.load(P.q + (int64_t)(s0 + qs) * P.sq + (int64_t)hqi * D, P.sq, nv);
     X.dout.load(P.dout + ((int64_t)(s0 + qs) * P.hq + hqi) * D, (int64_t)P.hq * D, nv);
@@ -774,34 +779,34 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     // (or math on it here) made hipcc put an s_waitcnt vmcnt(0) right behind it -- which also
     // waits for the Q/dO prefetch just issued, exposing its whole latency in every item.  The
     // volatile bit (aux bit 31) keeps the loads from being sunk into store_item's branch.
-    const int nrow = min(kKvBQ, seqlen - qs);
+    const int nrow = min(QB, seqlen - qs);
     const int64_t ro = (int64_t)hqi * P.T + s0 + qs;
-    const int vo = (threadIdx.x & 31) * 4;
+    const int vo = (threadIdx.x & (QB - 1)) * 4;
     X.lse = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(P.lse + ro, nrow * 4), vo, 0, (int)(1u << 31));
     X.dlt = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(P.delta + ro, nrow * 4), vo, 0, (int)(1u << 31));
   };
   auto store_item = [&](const Item& X, int buf) {
     X.q.store(qd + buf * 2 * SLICE);
     X.dout.store(qd + buf * 2 * SLICE + SLICE);
-    if (threadIdx.x < 64) {  // wave 0: lanes 0-31 -lse/scale, lanes 32-63 -delta
+    if (threadIdx.x < 2 * QB) {  // threads 0..QB-1: -lse/scale, QB..2QB-1: -delta of row threadIdx.x & (QB - 1)
       const float l = __builtin_bit_cast(float, X.lse), dl = __builtin_bit_cast(float, X.dlt);
-      rowc[buf * 64 + threadIdx.x] = (threadIdx.x & 32) ? -dl : -l * inv_scale;
+      rowc[buf * 2 * QB + threadIdx.x] = (threadIdx.x & QB) ? -dl : -l * inv_scale;
     }
   };
   auto compute = [&](int it, int buf) {
-    const int qs = (first_slice + it % per_head) * kKvBQ;
+    const int qs = (first_slice + it % per_head) * QB;
     // No skip of the (at most 3 per head) slices whose queries all precede this wave's keys:
     // a branch around the dK/dV updates makes hipcc carry the accumulators through VGPR copies
     // every item; the mask zeroes those slices' contributions instead.
     {
       const char* Ql = qd + buf * 2 * SLICE;
       const char* dOl = Ql + SLICE;
-      const float* c0 = rowc + buf * 64;
+      const float* c0 = rowc + buf * 2 * QB;
       f32x16 s, dp;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         s[i] = c0[acc_row(i, h)];
-        dp[i] = c0[32 + acc_row(i, h)];
+        dp[i] = c0[QB + acc_row(i, h)];
       }
       __builtin_amdgcn_sched_barrier(0);
       {
@@ -850,6 +855,83 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     }
   };
 
+  // QB = 64: halves u = 0, 1 (rows qs + 32u).  Masking is branch-free (a select per element) so
+  // the halves' MFMA and VALU phases stay in one basic block the scheduler can interleave.
+  auto sd_mfma = [&](const char* Ql, const char* dOl, f32x16& s, f32x16& dp) {
+    bf16x8 f[NC], g[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) f[c] = lds_frag(Ql + roff[c]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) s = mfma(f[c], kf[c], s);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) g[c] = lds_frag(dOl + roff[c]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dp = mfma(g[c], vf[c], dp);
+  };
+  auto softmax_half = [&](int qsu, f32x16& s, f32x16& dp, bf16x8 (&pf)[2], bf16x8 (&dsf)[2]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
+    if constexpr (CAUSAL) {
+      const int lim = key - koff_c - qsu - 4 * h;  // query row qsu + acc_row < key - koff_c is masked
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = acc_row0(i) < lim ? 0.f : s[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dp[i] *= s[i];
+    pf[0] = pack8(s, 0);
+    pf[1] = pack8(s, 1);
+    dsf[0] = pack8(dp, 0);
+    dsf[1] = pack8(dp, 1);
+  };
+  auto kv_mfma = [&](const char* Ql, const char* dOl, const bf16x8 (&pf)[2], const bf16x8 (&dsf)[2]) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const char* ob = dOl + 16 * st * RB;
+      const char* qb = Ql + 16 * st * RB;
+      bf16x8 a[ND], b[ND];
+#pragma unroll
+      for (int d = 0; d < ND; ++d) a[d] = tr_frag_at(ob + toa[d], ob + tob[d]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) dv[d] = mfma(a[d], pf[st], dv[d]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) b[d] = tr_frag_at(qb + toa[d], qb + tob[d]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) dk[d] = mfma(b[d], dsf[st], dk[d]);
+    }
+  };
+  auto compute64 = [&](int it, int buf) {
+    const int qs = (first_slice + it % per_head) * QB;
+    const char* Ql = qd + buf * 2 * SLICE;
+    const char* dOl = Ql + SLICE;
+    const float* c0 = rowc + buf * 2 * QB;
+    f32x16 s0, dp0, s1, dp1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s0[i] = c0[acc_row(i, h)];
+      dp0[i] = c0[QB + acc_row(i, h)];
+      s1[i] = c0[32 + acc_row(i, h)];
+      dp1[i] = c0[QB + 32 + acc_row(i, h)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    sd_mfma(Ql, dOl, s0, dp0);
+    pipeline_reads<2 * NC, 1, 4>();
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 pf0[2], dsf0[2], pf1[2], dsf1[2];
+    sd_mfma(Ql + 32 * RB, dOl + 32 * RB, s1, dp1);  // || softmax of half 0
+    softmax_half(qs, s0, dp0, pf0, dsf0);
+    __builtin_amdgcn_sched_barrier(0);
+    kv_mfma(Ql, dOl, pf0, dsf0);  // || softmax of half 1
+    softmax_half(qs + 32, s1, dp1, pf1, dsf1);
+    __builtin_amdgcn_sched_barrier(0);
+    kv_mfma(Ql + 32 * RB, dOl + 32 * RB, pf1, dsf1);
+    pipeline_reads<4 * ND, 2, 3>();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto run_item = [&](int it, int buf) {
+    if constexpr (QB == 64) compute64(it, buf);
+    else compute(it, buf);
+  };
+
   // Settle this lane's K/V fragment loads before the item loop, on every path into it.  Left
   // pending, hipcc's wait-count analysis carried them around the loop's back edge and put an
   // s_waitcnt vmcnt(1) / vmcnt(0) in front of the first S MFMA of every item -- a wait on the
@@ -857,6 +939,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
 #pragma unroll
   for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(kf[c]), "+v"(vf[c]));
 
+  static_assert(PF == 1 || QB == 32, "two-item prefetch only with 32-row items");
   if constexpr (PF == 2) {
     // Prefetch loads are issued unconditionally (a finished tail re-reads its last item): with
     // a branch around them hipcc's wait counting must assume they may be absent and drains
@@ -892,7 +975,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
       const int buf = it & 1;
       const bool more = it + 1 < it1;
       if (more) load_item(ia, it + 1);
-      compute(it, buf);
+      run_item(it, buf);
       if (more) store_item(ia, buf ^ 1);
       __syncthreads();
     }
@@ -1198,7 +1281,12 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
   }
   {
     dim3 grid(hkv, nseq, nkb * nsplit);
-    const size_t lds = 4 * fa::kKvBQ * D * 2 + 2 * 64 * 4;
+    // DTG_FA_KV_QB = 32 | 64: query rows per item; per call (A/B).  64 (the two-half software
+    // pipeline) is the default: backward 2-4 % faster on every benchmarked shape, -1.9 ms per 8B
+    // step (profiles/r3_s39).  Sliding windows and the two-item prefetch keep 32.
+    const char* qe = std::getenv("DTG_FA_KV_QB");
+    const int qb = ((qe == nullptr || std::atoi(qe) != 32) && P.window == 0 && kv_pf == 1) ? 64 : 32;
+    const size_t lds = 4 * (size_t)qb * D * 2 + 2 * 2 * qb * 4;
 #define DTG_BWD_KV(DD, C, PF, ...)                                                        \
   do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>, lds);      \
        hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>), grid, dim3(256), lds, st, P); } while (0)
@@ -1207,6 +1295,9 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
     } else if (kv_pf == 2) {
       if (D == 128) { if (causal) DTG_BWD_KV(128, true, 2); else DTG_BWD_KV(128, false, 2); }
       else { if (causal) DTG_BWD_KV(64, true, 2); else DTG_BWD_KV(64, false, 2); }
+    } else if (qb == 64) {
+      if (D == 128) { if (causal) DTG_BWD_KV(128, true, 1, false, 64); else DTG_BWD_KV(128, false, 1, false, 64); }
+      else { if (causal) DTG_BWD_KV(64, true, 1, false, 64); else DTG_BWD_KV(64, false, 1, false, 64); }
     } else {
       if (D == 128) { if (causal) DTG_BWD_KV(128, true, 1); else DTG_BWD_KV(128, false, 1); }
       else { if (causal) DTG_BWD_KV(64, true, 1); else DTG_BWD_KV(64, false, 1); }

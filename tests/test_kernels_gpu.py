@@ -384,6 +384,33 @@ def test_flash_attn_bwd_kv_split(cuda, split, causal, monkeypatch):
         assert _rel(x, y) < 1e-2
 
 
+@pytest.mark.parametrize("split", ["1", "4"])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("D,hq,hkv", [(128, 8, 2), (64, 4, 4)])
+def test_flash_attn_bwd_kv_qb64(cuda, D, hq, hkv, causal, split, monkeypatch):
+    """dK/dV with 64-query items (two-half software pipeline, DTG_FA_KV_QB=64): the fp32
+    reference on varlen sequences whose lengths are not multiples of 64, alone and split; dQ is
+    untouched and dK/dV agree with the 32-row items to summation-order rounding."""
+    monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
+    monkeypatch.setenv("DTG_FA_KV_QB", "64")
+    qkv, cu = _attn_case(cuda, [1024, 77, 300], hq=hq, hkv=hkv, D=D, causal=causal, stride_extra=8)
+    T = qkv.shape[0]
+    g = qkv.to(cuda)
+    q, k, v = (g[:, a * D:b * D].view(T, b - a, D) for a, b in ((0, hq), (hq, hq + hkv), (hq + hkv, hq + 2 * hkv)))
+    o, lse = dops.flash_attn_fwd(q, k, v, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    torch.manual_seed(3)
+    do = torch.randn(T, hq, D, device=cuda).bfloat16()
+    a = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    b = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    monkeypatch.setenv("DTG_FA_KV_QB", "32")
+    ref = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    assert torch.equal(a[0], ref[0])
+    for x, y in zip(a[1:], ref[1:]):
+        assert _rel(x, y) < 1e-2
+
+
 @pytest.mark.parametrize("window", [2, 64, 200, 5000])
 @pytest.mark.parametrize("D,hq,hkv", [(128, 8, 2), (64, 4, 4)])
 def test_flash_attn_sliding_window(cuda, window, D, hq, hkv):
