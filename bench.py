@@ -251,7 +251,11 @@ def fsdp_mem_one_rank(args):
            "--model", args.fsdp_mem_model, "--batch", str(args.fsdp_mem_batch), "--seq", str(args.fsdp_mem_seq),
            "--numel-to-wrap", str(args.numel_to_wrap), "--steps", str(max(2, args.fsdp_mem_steps))]
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        # the child is a one-process job of its own: none of this run's rank / fake-world env
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("DTG_FAKE_WORLD", "WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                            "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
         lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
         if r.returncode == 0 and lines:
             return json.loads(lines[-1])
