@@ -699,9 +699,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 // double-buffered in LDS.  S and dP start from the row constants
 // (-lse/scale, -delta) so p = exp2(c2 S') and dS = p dP' need no per-element subtraction;
 // only the causal diagonal is masked (padded query rows carry Q = dO = 0 and contribute 0).
-// D = 128 at one wave per SIMD: every value stays in registers (306 of them).  Forced to two
-// waves the allocator spills ~50 dwords per lane to scratch and the kernel runs at half speed
-// (profiles/r3_s20).
+// D = 128 at one wave per SIMD: every value stays in registers (306 of them with 32-row items,
+// 408 with the default 64-row items).  Forced to two waves the allocator spills ~50 dwords per
+// lane to scratch and the kernel runs at half speed (profiles/r3_s20).
 // QB: query rows per item, 32 or 64.  QB = 64 runs each item as two 32-row halves in a software
 // pipeline (S/dP MFMAs of half 1 under the softmax VALU of half 0, dK/dV MFMAs of half 0 under
 // the softmax of half 1): at one wave per SIMD there is no partner wave to fill the matrix pipe
