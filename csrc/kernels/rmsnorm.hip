@@ -147,20 +147,25 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
 // Column sums of an [nrows, H] f32 matrix -> bf16 [H].  A workgroup owns 32 columns; its 8
 // row-groups of 32 lanes read 128-B row segments (coalesced) and are combined through LDS,
 // so the reduction spreads over H/32 workgroups instead of H serial threads.
+// Column sums of the [nrows, H] f32 partials, fixed summation order (deterministic).  16 columns
+// x 16 row groups per workgroup: H / 16 workgroups (256 at H = 4096, one per CU) each walking
+// nrows / 16 rows -- the 32-column form had half the chip idle and twice the dependent-load depth.
+constexpr int kColsumCols = 16;
 __global__ __launch_bounds__(256) void colsum_to_bf16_kernel(const float* __restrict__ part, int nrows, int H,
                                                              uint16_t* __restrict__ out) {
-  __shared__ float red[8][33];
-  const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + lane;
+  constexpr int G = 256 / kColsumCols;
+  __shared__ float red[G][kColsumCols + 1];
+  const int lane = threadIdx.x % kColsumCols, grp = threadIdx.x / kColsumCols;
+  const int c = blockIdx.x * kColsumCols + lane;
   float s = 0.f;
   if (c < H)
-    for (int r = grp; r < nrows; r += 8) s += part[(int64_t)r * H + c];
+    for (int r = grp; r < nrows; r += G) s += part[(int64_t)r * H + c];
   red[grp][lane] = s;
   __syncthreads();
   if (grp == 0 && c < H) {
     float t = 0.f;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) t += red[g][lane];
+    for (int g = 0; g < G; ++g) t += red[g][lane];
     out[c] = f2bf(t);
   }
 }
@@ -269,7 +274,8 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy_, const at::
                               part.data_ptr<float>(), T, H, rpb));
   }
   DTG_LAUNCH_CHECK();
-  colsum_to_bf16_kernel<<<(H + 31) / 32, 256, 0, stream()>>>(part.data_ptr<float>(), nb, H, bf16_mut(dw));
+  colsum_to_bf16_kernel<<<(H + kColsumCols - 1) / kColsumCols, 256, 0, stream()>>>(part.data_ptr<float>(), nb, H,
+                                                                                    bf16_mut(dw));
   DTG_LAUNCH_CHECK();
   return {dx, dw};
 }
