@@ -54,7 +54,9 @@ def parse(argv=None):
     # inside groups of --tp ranks, data parallel (--parallel) across them; a step is dp x B x S
     # tokens (the reference's TP tok/s formula, 06-tensor-parallel/train_llm.py:256).
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--tp-comm", default="rccl", choices=["rccl", "xgmi", "xgmi-dma"])
+    # auto = xgmi-dma on a GPU (the README's recommendation for config 06; the N > 1 collective
+    # sweep records RCCL vs both xGMI engines at the TP message sizes), the PG backend on CPU
+    ap.add_argument("--tp-comm", default="auto", choices=["auto", "rccl", "xgmi", "xgmi-dma"])
     ap.add_argument("--tp-overlap-chunks", type=int, default=2)
     ap.add_argument("--overlap-optimizer", type=int, default=0,
                     help="1: per-bucket AdamW (and ZeRO all-gather) on a side stream during backward (measured +0.2%% on 1 GPU, off)")
@@ -78,6 +80,14 @@ def parse(argv=None):
     # bandwidth at these message sizes (MiB), so the multi-GPU run also measures the curve the
     # 256 MiB gradient-bucket default is chosen from.  Empty string = off.
     ap.add_argument("--coll-sweep-mb", default="16,64,256,1024")
+    # N > 1 only, after the timed region: ZeRO/DDP step time rebuilt at each bucket size (MiB)
+    ap.add_argument("--bucket-sweep-mb", default="64,128,256,512")
+    ap.add_argument("--sweep-steps", type=int, default=3)
+    # reference-mode throughput: this many extra steps under the reference's synchronising
+    # LocalTimer phases (outside the timed region); 0 = off
+    ap.add_argument("--ref-steps", type=int, default=3)
+    # N > 1: RCCL environment preset applied before init (dtg/utils/rccl.py; exported variables win)
+    ap.add_argument("--rccl-preset", default="node", choices=["node", "multinode", "none"])
     return ap.parse_args(argv)
 
 
@@ -107,23 +117,45 @@ def _sync(dist, world, cuda):
         torch.cuda.synchronize()
 
 
-def throughput_phase(args, torch, dist, device, world, rank, cuda):
+def _batches(torch, cfg, B, S, n, device, seed):
+    """n distinct batches of fresh uniform token ids, generated on the device before the timed
+    region.  Uniform ids carry no learnable signal, so the loss stays near ln(vocab) for the
+    whole run: a kernel whose numerics regress moves it off that value (the tripwire below),
+    where four recycled batches let the model memorise them down to ~0.04 and hid any such
+    regression."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    return [torch.randint(0, cfg.vocab_size, (B, S), device=device, generator=g) for _ in range(n)]
+
+
+def loss_in_band(loss: float, vocab: int) -> bool:
+    """Tripwire for the synthetic run: next-token loss on uniform ids must stay within
+    [ln V - 3.5, ln V + 1.5] (Llama-3-8B: 8.26 .. 13.26 around ln 128256 = 11.76)."""
+    lnv = math.log(vocab)
+    return math.isfinite(loss) and lnv - 3.5 < loss < lnv + 1.5
+
+
+def build_job(args, torch, device, cuda, bucket_mb=None):
+    """Model + engine + optimizer + scheduler of the flagship step, as the driver's command
+    builds them.  `bucket_mb` overrides --bucket-mb (the N > 1 bucket-size sweep)."""
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
 
     cfg = resolve_config(args.model)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
     dp_group = tp_group = xgmi = None
     dp_size, dp_rank = world, rank
+    tp_comm = resolve_tp_comm(args.tp_comm, cuda)
     if args.tp > 1:
         from dtg.parallel.tensor_parallel import make_mesh
 
         dp_group, tp_group, dp_rank, _, dp_size = make_mesh(args.tp)
-        if args.tp_comm != "rccl" and cuda:
+        if tp_comm != "rccl" and cuda:
             from dtg.parallel.xgmi import XgmiCommunicator
             from dtg.utils import comm as _comm
 
             xgmi = XgmiCommunicator(tp_group, capacity_bytes=256 << 20, device=device,
-                                    gather_engine="dma" if args.tp_comm == "xgmi-dma" else "kernel")
+                                    gather_engine="dma" if tp_comm == "xgmi-dma" else "kernel")
             _comm.register_xgmi(tp_group, xgmi)
     model = build_model(cfg, device=device, tp_group=tp_group)
     if tp_group is not None:
@@ -134,14 +166,47 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
         engine = FullyShard(model, group=dp_group, tp_group=tp_group)
     else:
         engine = DataParallel(model, mode=args.parallel if dp_size > 1 else "single", group=dp_group, tp_group=tp_group,
-                              bucket_mb=args.bucket_mb, broadcast_from_rank0=tp_group is None,
+                              bucket_mb=bucket_mb or args.bucket_mb, broadcast_from_rank0=tp_group is None,
                               overlap_optimizer=bool(args.overlap_optimizer))
     opt = FlatAdamW(engine, lr=args.lr)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=1000, eta_min=args.lr * 1e-2)
+    return dict(cfg=cfg, model=model, engine=engine, opt=opt, sched=sched, dp_size=dp_size, dp_rank=dp_rank,
+                tp_group=tp_group, xgmi=xgmi, tp_comm=tp_comm)
+
+
+def close_job(job, torch):
+    eng = job["engine"]
+    if hasattr(eng, "wait_param_gather"):
+        eng.wait_param_gather()
+    if job["xgmi"] is not None:
+        torch.cuda.synchronize()
+        job["xgmi"].check()
+        from dtg.utils import comm as _comm
+
+        _comm.unregister_xgmi(job["tp_group"])
+        job["xgmi"].close()
+    job.clear()
+
+
+def resolve_tp_comm(choice: str, cuda: bool) -> str:
+    """--tp-comm auto: the copy-engine xGMI path on a GPU (every TP group of this bench lives
+    inside one node, the xGMI island), the process group's collectives on CPU."""
+    if choice != "auto":
+        return choice
+    return "xgmi-dma" if cuda else "rccl"
+
+
+def throughput_phase(args, torch, dist, device, world, rank, cuda):
+    from dtg.utils.timers import make_timers
+
+    job = build_job(args, torch, device, cuda)
+    cfg, model, engine, opt, sched = job["cfg"], job["model"], job["engine"], job["opt"], job["sched"]
+    dp_size, dp_rank = job["dp_size"], job["dp_rank"]
 
     B, S = args.batch_size, args.seq_len
-    g = torch.Generator(device=device).manual_seed(1234 + dp_rank)  # one batch per TP group
-    batches = [torch.randint(0, cfg.vocab_size, (B, S), device=device, generator=g) for _ in range(4)]
+    # one batch per TP group; every step (warm-up, timed, reference-timer) gets fresh ids
+    n_batches = min(512, args.warmup + args.steps + args.ref_steps + max(0, args.profile_steps))
+    batches = _batches(torch, cfg, B, S, n_batches, device, 1234 + dp_rank)
     num_valid = B * (S - 1)
 
     def step(i):
@@ -168,11 +233,33 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
         loss = step(args.warmup + i)
     _sync(dist, world, cuda)
     elapsed = time.perf_counter() - t0
+    loss_val = float(loss.item())
     if args.tunableop == "tune" and cuda and rank == 0:
         from dtg.utils.gemm_tuning import save_tunableop
 
         save_tunableop()
     peak_gb = torch.cuda.max_memory_allocated(device) / 2**30 if cuda else 0.0
+
+    # Reference-mode throughput (outside the timed region): the reference's LocalTimer phases,
+    # each bracketed by a device synchronize (/root/reference/01-single-gpu/train_llm.py:156-170,
+    # 262-288), tok/s = 1000 * tok_per_step / sum of the phase averages.
+    ref_ms = None
+    if args.ref_steps > 0:
+        timers = make_timers(device, sync=True)
+        base = args.warmup + args.steps
+        for i in range(args.ref_steps):
+            with timers["data"]:
+                ids = batches[(base + i) % len(batches)]
+            with timers["forward"]:
+                opt.zero_grad()
+                out = model(input_ids=ids, labels=ids, num_valid=num_valid)
+            with timers["backward"]:
+                engine.backward(out.loss)
+            with timers["update"]:
+                opt.step()
+                sched.step()
+            del out
+        ref_ms = {k: t.avg_elapsed_ms() for k, t in timers.items()}
 
     if args.profile_steps > 0 and cuda:
         from torch.profiler import ProfilerActivity, profile
@@ -185,23 +272,71 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
             os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
             with open(os.path.join(ROOT, "gpurun_out", "torch_profile.txt"), "w") as fp:
                 fp.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
-    res = dict(elapsed=elapsed, peak_gb=peak_gb, loss=float(loss.item()), cfg=cfg,
-               mode=getattr(engine, "mode", args.parallel), dp=dp_size)
-    if not math.isfinite(res["loss"]) and int(os.environ.get("DTG_FAKE_WORLD", "0") or 0) <= 1:
-        # a step that produced NaN/inf (e.g. a wrong GEMM solution) is not a measurement
-        # (a fake-world rehearsal computes on buffers no collective filled: its loss means nothing)
-        raise SystemExit(f"bench.py: rank {rank} final loss is {res['loss']}; refusing to report a throughput")
+    fake = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0) > 1
+    # a fake-world rehearsal computes on buffers no collective filled: its loss means nothing
+    if not fake and not loss_in_band(loss_val, cfg.vocab_size):
+        # NaN/inf (e.g. a wrong GEMM solution) or a loss off ln(V) on uniform ids is a numerics
+        # failure, not a measurement
+        raise SystemExit(f"bench.py: rank {rank} final loss {loss_val} is outside the uniform-data band around "
+                         f"ln({cfg.vocab_size}) = {math.log(cfg.vocab_size):.2f}; refusing to report a throughput")
+    res = dict(elapsed=elapsed, peak_gb=peak_gb, loss=loss_val, cfg=cfg, ref_ms=ref_ms,
+               mode=getattr(engine, "mode", args.parallel), dp=dp_size, tp_comm=job["tp_comm"],
+               replica_sum=replica_checksum(engine, torch))
+    del model, engine, opt, sched, batches, loss
+    close_job(job, torch)
+    return res
+
+
+def replica_checksum(engine, torch):
+    """f64 sum of this rank's full parameter replica (DDP / ZeRO): after the step's all-gather
+    every data-parallel rank must hold bit-identical weights, so the values gathered from all
+    ranks must agree exactly -- a check that every collective of the timed run landed."""
+    space = getattr(engine, "space", None)
+    if space is None or getattr(engine, "mode", "single") not in ("ddp", "zero") or engine.tp_group is not None:
+        return float("nan")
     if hasattr(engine, "wait_param_gather"):
         engine.wait_param_gather()
-    if xgmi is not None:
-        torch.cuda.synchronize()
-        xgmi.check()
-        from dtg.utils import comm as _comm
+    return float(space.param_buf.double().sum().item())
 
-        _comm.unregister_xgmi(tp_group)
-        xgmi.close()
-    del model, engine, opt, sched, batches, loss
-    return res
+
+def bucket_sweep(args, torch, dist, device, world, rank, cuda):
+    """N > 1, after the timed region: the same step rebuilt at each gradient-bucket size of
+    --bucket-sweep-mb (1 warm-up + --sweep-steps timed steps each, max over ranks), so the run
+    records the curve the --bucket-mb default is chosen from.  Not part of `value`."""
+    sizes = [int(x) for x in args.bucket_sweep_mb.split(",") if x.strip()]
+    out = []
+    B, S = args.batch_size, args.seq_len
+    for mb in sizes:
+        job = build_job(args, torch, device, cuda, bucket_mb=mb)
+        model, engine, opt = job["model"], job["engine"], job["opt"]
+        ids_all = _batches(torch, job["cfg"], B, S, 1 + args.sweep_steps, device, 777 + job["dp_rank"])
+
+        def step(ids):
+            opt.zero_grad()
+            out_ = model(input_ids=ids, labels=ids, num_valid=B * (S - 1))
+            engine.backward(out_.loss)
+            opt.step()
+
+        step(ids_all[0])
+        _sync(dist, world, cuda)
+        t0 = time.perf_counter()
+        for ids in ids_all[1:]:
+            step(ids)
+        _sync(dist, world, cuda)
+        ms = torch.tensor([1000 * (time.perf_counter() - t0) / max(1, args.sweep_steps)], dtype=torch.float64,
+                          device=device)
+        if world > 1:
+            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        out.append({"bucket_mb": mb, "buckets": len(engine.space.buckets) if hasattr(engine, "space") else None,
+                    "ms_per_step": round(float(ms.item()), 2)})
+        del model, engine, opt, ids_all, step
+        close_job(job, torch)
+        import gc
+
+        gc.collect()
+        if cuda:
+            torch.cuda.empty_cache()
+    return out
 
 
 def fsdp_memory_phase(args, torch, dist, device, world, rank, cuda):
@@ -294,7 +429,62 @@ def collective_sweep(args, torch, dist, device, world, cuda):
             out.append({"op": op, "mib": mib, "us": round(dt * 1e6, 1),
                         "busbw_gbs": round((n * esz) / dt / 1e9 * factor, 4)})
         del x, shard, full
+    if cuda and 1 < world <= 8:
+        out.extend(_xgmi_sweep(torch, dist, device, world, cuda, [s for s in sizes if s <= 256]))
     return out
+
+
+def _xgmi_sweep(torch, dist, device, world, cuda, sizes):
+    """The same messages over the direct-peer xGMI library (parallel/xgmi.py), pull kernels and
+    copy engines, next to RCCL's rows: the evidence --tp-comm / --dp-comm defaults rest on."""
+    if not sizes:
+        return []
+    rows = []
+    xc = None
+    try:
+        from dtg.parallel.xgmi import XgmiCommunicator
+
+        xc = XgmiCommunicator(None, capacity_bytes=max(sizes) << 20, device=device)
+        for mib in sizes:
+            n = (mib << 20) // 2 // world * world
+            x = torch.randn(n, device=device).to(torch.bfloat16)
+            shard = torch.empty(n // world, device=device, dtype=torch.bfloat16)
+            full = torch.empty(n, device=device, dtype=torch.bfloat16)
+            for eng in ("kernel", "dma"):
+                xc.gather_engine = eng
+                for op, fn in (("reduce_scatter", lambda: xc.reduce_scatter_into(shard, x)),
+                               ("all_gather", lambda: xc.all_gather_into(full, shard))):
+                    iters = 5 if mib >= 128 else 10
+                    fn()
+                    _sync(dist, world, cuda)
+                    t0 = time.perf_counter()
+                    for _ in range(iters):
+                        fn()
+                    _sync(dist, world, cuda)
+                    dt = (time.perf_counter() - t0) / iters
+                    rows.append({"op": f"{op}_xgmi_{eng}", "mib": mib, "us": round(dt * 1e6, 1),
+                                 "busbw_gbs": round(n * 2 / dt / 1e9 * (world - 1) / world, 4)})
+            del x, shard, full
+        xc.check()
+    except Exception as e:  # a diagnostic: never lose the run's JSON line over it
+        rows.append({"op": "xgmi", "error": repr(e)[:300]})
+    finally:
+        if xc is not None:
+            try:
+                xc.close()
+            except Exception:
+                pass
+    return rows
+
+
+def _load_rccl_module():
+    import importlib.util
+
+    path = os.path.join(ROOT, "lambda-labs_distributed-training-guide_amd", "utils", "rccl.py")
+    spec = importlib.util.spec_from_file_location("_dtg_rccl_preinit", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
 
 def main(argv=None):
@@ -304,8 +494,21 @@ def main(argv=None):
     # PyTorch's fake process group (collectives return at once).  Shapes, shard layouts, kernels
     # and memory are those of the real N-rank job; the time excludes communication and is labelled.
     fake_world = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0)
+    if fake_world > 1 and ("TORCHELASTIC_RUN_ID" in os.environ or int(os.environ.get("WORLD_SIZE", "1") or 1) > 1):
+        raise SystemExit("bench.py: DTG_FAKE_WORLD is set inside a multi-rank launch; unset it "
+                         "(a rehearsal is one process)")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and fake_world <= 1:
         return self_launch(args, argv)
+
+    # A real multi-rank job (RCCL): the node preset (utils/rccl.py; never overrides an exported
+    # variable) goes in before anything initialises HIP, and RCCL's INIT/GRAPH log is captured
+    # to a per-rank file so the JSON line can say what RCCL built (transport, channels).
+    multi = int(os.environ.get("WORLD_SIZE", "1")) > 1 and fake_world <= 1
+    rccl_log = rccl_applied = None
+    if multi and args.rccl_preset != "none":
+        _rccl = _load_rccl_module()  # stdlib-only: importing it does not touch the GPU
+        rccl_applied = _rccl.apply_preset(args.rccl_preset)
+        rccl_log = _rccl.arm_log(f"rank{os.environ.get('RANK', '0')}_{os.getpid()}")
 
     import gc
 
@@ -362,7 +565,11 @@ def main(argv=None):
     gc.collect()
     if cuda:
         torch.cuda.empty_cache()
-    coll = collective_sweep(args, torch, dist, device, world, cuda) if (world > 1 and fake_world <= 1 and args.coll_sweep_mb) else None
+    # ---- after the timed region: diagnostics of the multi-rank run (none of this is in `value`)
+    coll = collective_sweep(args, torch, dist, device, world, cuda) if (multi and args.coll_sweep_mb) else None
+    sweep = None
+    if multi and args.bucket_sweep_mb and args.parallel in ("ddp", "zero") and args.tp == 1:
+        sweep = bucket_sweep(args, torch, dist, device, world, rank, cuda)
     mem = None
     if args.fsdp_mem_steps > 0:
         mem = fsdp_memory_phase(args, torch, dist, device, world, rank, cuda)
@@ -373,8 +580,11 @@ def main(argv=None):
         mem_one = fsdp_mem_one_rank(args)
 
     # per-rank facts, gathered to rank 0: elapsed, device ordinal, PCI bus, peaks
+    ref_sum = sum(res["ref_ms"].values()) if res["ref_ms"] else 0.0
     me = [res["elapsed"], float(dev_idx), float(res["peak_gb"]),
-          mem["valley"] if mem else 0.0, mem["peak"] if mem else 0.0, mem["ms"] if mem else 0.0]
+          mem["valley"] if mem else 0.0, mem["peak"] if mem else 0.0, mem["ms"] if mem else 0.0,
+          ref_sum, res["replica_sum"]] + ([res["ref_ms"][k] for k in ("data", "forward", "backward", "update")]
+                                         if res["ref_ms"] else [0.0] * 4)
     mine = torch.tensor(me, dtype=torch.float64, device=device)
     if world > 1 and fake_world > 1:
         rows = [mine.cpu().tolist()]  # the other ranks do not exist
@@ -399,7 +609,8 @@ def main(argv=None):
     flops_tok = cfg.flops_per_token(S)
     mfu = tps * flops_tok / (world * 2.5e15) if cuda else 0.0
     # TP collectives: "rccl" means the process group's own backend (gloo in CPU / shared-GPU rehearsals)
-    tp_comm_label = args.tp_comm if args.tp_comm != "rccl" else ("rccl" if backend in (None, "nccl") else backend)
+    tp_comm = res["tp_comm"]
+    tp_comm_label = tp_comm if tp_comm != "rccl" else ("rccl" if backend in (None, "nccl") else backend)
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -427,12 +638,29 @@ def main(argv=None):
             "rank_ms_per_step": {"max": round(1000 * elapsed / args.steps, 2),
                                  "min": round(1000 * min(r[0] for r in rows) / args.steps, 2)},
         }
+        rec["loss_band"] = [round(math.log(cfg.vocab_size) - 3.5, 2), round(math.log(cfg.vocab_size) + 1.5, 2)]
+        if res["ref_ms"]:
+            # the reference's own tok/s (synchronised LocalTimer phases, slowest rank)
+            ref_sum_max = max(r[6] for r in rows)
+            rec["tok_s_reference_timers"] = round(1000 * dp * B * S / ref_sum_max, 1)
+            rec["reference_timer_ms"] = {k: round(max(r[8 + j] for r in rows), 2)
+                                         for j, k in enumerate(("data", "forward", "backward", "update"))}
+            rec["reference_timer_steps"] = args.ref_steps
+        sums = [r[7] for r in rows]
+        if world > 1 and fake_world <= 1 and all(math.isfinite(s) for s in sums):
+            # every data-parallel replica must hold bit-identical weights after the last step
+            rec["replicas_consistent"] = len(set(sums)) == 1
         if fake_world > 1:
             rec["metric"] = "REHEARSAL (not a measurement of the job): " + METRIC
             rec["rehearsal"] = (f"rank 0 of a {world}-rank job alone on one GPU, other ranks a fake process "
                                 "group: communication not included, value = one rank's compute rate x world")
         if coll is not None and fake_world <= 1:
             rec["collectives"] = coll
+        if sweep is not None:
+            rec["bucket_sweep"] = sweep
+        if multi and backend == "nccl":
+            rec["rccl"] = _load_rccl_module().diagnose(rccl_log)
+            rec["rccl"]["preset_applied"] = rccl_applied
         if mem is not None:
             rec["fsdp_mem"] = {"model": mem["model"], "batch_per_gpu": args.fsdp_mem_batch,
                                "seq_len": args.fsdp_mem_seq, "wrap": f"size>={args.numel_to_wrap}",

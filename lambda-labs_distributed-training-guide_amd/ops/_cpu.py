@@ -280,6 +280,11 @@ def transpose2d(x):
     return x.t().contiguous()
 
 
+def transpose_mats_(x, out, mats, mats_host, ntiles):
+    for so, r, c, do, _t0 in mats_host.tolist():
+        out[do:do + r * c].copy_(x[so:so + r * c].view(r, c).t().reshape(-1))
+
+
 def embedding_bwd_(out, ids, dy):
     """out[id] += sum of dy rows with that id, f32 sums rounded once; ids outside [0, V) skipped."""
     acc = torch.zeros(out.shape, dtype=torch.float32)
@@ -293,7 +298,7 @@ for _name, _fn in list(globals().items()):
     if _name in (
         "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "adamw_t_", "flash_attn_fwd", "flash_attn_bwd",
-        "flash_attn_bwd_qkv", "transpose2d", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
+        "flash_attn_bwd_qkv", "transpose2d", "transpose_mats_", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
         "flash_attn_varlen_bwd",
     ):
         LIB.impl(_name, _fn, "CPU")

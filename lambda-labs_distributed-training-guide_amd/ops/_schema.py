@@ -38,6 +38,9 @@ _DEFS = [
     "flash_attn_bwd_qkv(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
     "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, int window=0) -> Tensor",
     "transpose2d(Tensor x) -> Tensor",
+    # many matrices of a flat buffer transposed in one launch: rows of `mats` (int64 [n, 5]:
+    # source offset, rows, cols, destination offset, first 64 x 64 tile); `mats_host` = its CPU copy
+    "transpose_mats_(Tensor x, Tensor(a!) out, Tensor mats, Tensor mats_host, int ntiles) -> ()",
     "embedding_bwd_(Tensor(a!) out, Tensor ids, Tensor dy) -> ()",
     # FlashAttention-2-style varlen with explicit per-sequence key ranges (disjoint), causal mask
     # bottom-right aligned: context parallelism's local query chunks over gathered key prefixes

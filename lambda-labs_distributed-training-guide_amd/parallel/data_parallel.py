@@ -11,7 +11,7 @@
                  not checkpointable) is strictly more traffic; this engine's state is
                  checkpointable (§2.11 #1).
 
-Transposed weights (single / DDP, bf16 on the GPU; `weight_t=True`): hipBLASLt runs the
+Transposed weights (bf16 on the GPU; `weight_t=True`): hipBLASLt runs the
 backward's dX = dY W at TN speed only with a K-contiguous W^T.  Weights change once per step,
 so the optimizer kernel (`adamw_t_`) writes W^T of every weight matrix while the updated values
 are in registers, into a persistent buffer the Linear backward reads (`ops.functional._wt`),
@@ -20,6 +20,10 @@ read is saved, the write moves into the optimizer).  Staleness is impossible by 
 the copy is used only while the flat parameter buffer's version counter still equals the value
 recorded after the last refresh, so any other write to the weights (a checkpoint or pretrained
 load, a manual edit) makes the backward fall back to transposing until the next step.
+Under ZeRO a rank updates only its 1/W slice of each bucket, so the copies are rebuilt instead
+as each bucket's parameter all-gather lands: one batched transpose launch per bucket
+(`transpose_mats_`) on a side stream, under the next forward's GEMMs, and the backward's dX
+GEMM waits for its bucket's event (the transposes left the backward's critical path).
 
 `overlap_optimizer=True` moves the AdamW update into backward: the moment a bucket's gradients
 are final (and, with DDP/ZeRO, its all-reduce / reduce-scatter has landed) its update runs on a
@@ -129,9 +133,11 @@ class DataParallel:
             weight_t = os.environ.get("DTG_WEIGHT_T", "1") == "1" and dev.type == "cuda"
         self._wt_buf = None
         self._wt_version = -1
-        if (weight_t and self.mode in ("single", "ddp") and not overlap_optimizer
+        self._wt_stream = None
+        self._wt_ready = {}  # zero: bucket -> event after its W^T transposes (side stream)
+        if (weight_t and not overlap_optimizer
                 and self.space.dtype == torch.bfloat16 and self.space.grad_dtype == torch.bfloat16) or \
-                (weight_t and dev.type == "cpu" and self.mode in ("single", "ddp") and not overlap_optimizer):
+                (weight_t and dev.type == "cpu" and not overlap_optimizer):
             self._build_weight_t()
 
     # ------------------------------------------------------------------ transposed weights
@@ -172,6 +178,24 @@ class DataParallel:
         self._wt_mats = torch.tensor(rows_desc, dtype=torch.long, device=dev)
         self._wt_tiles = tile0
         self._wt_buf = torch.empty(toff, dtype=sp.dtype, device=dev)
+        if self.mode == "zero":
+            # ZeRO updates 1/W of every bucket, so adamw_t_ cannot write whole W^T copies; they
+            # are rebuilt per bucket the moment its parameter all-gather lands, by one batched
+            # transpose launch on a side stream that runs under the next forward's GEMMs.
+            per_b = {}
+            for i, (t, rows, cols) in sorted(slots.items()):
+                per_b.setdefault(sp.param_bucket[i].index, []).append((sp.offsets[i], rows, cols, t))
+            self._wt_bucket_mats = {}
+            for b, mats in per_b.items():
+                desc, t0 = [], 0
+                for off, rows, cols, t in mats:
+                    desc.append([off, rows, cols, t, t0])
+                    t0 += -(-rows // 64) * -(-cols // 64)
+                host = torch.tensor(desc, dtype=torch.long)
+                self._wt_bucket_mats[b] = (host.to(dev), host, t0)
+            self._wt_valid = {b: False for b in self._wt_bucket_mats}
+            if dev.type == "cuda":
+                self._wt_stream = torch.cuda.Stream(device=dev)
         self._wt_views = {}
         for i, (o, rows, cols) in slots.items():
             self._wt_views[i] = self._wt_buf[o:o + rows * cols].view(cols, rows)
@@ -199,13 +223,46 @@ class DataParallel:
             w = ps[i]
             view.copy_(_F.ops.transpose2d(w) if w.is_cuda else w.t())
         self._wt_version = self.space.param_buf._version
+        if self.mode == "zero":
+            self._wt_ready.clear()
+            for b in self._wt_valid:
+                self._wt_valid[b] = True
 
     def weight_t(self, i):
         """The current W^T of flat parameter i, or None if the weights changed since the last
         refresh (the caller then transposes)."""
         if self._wt_buf is None or self.space.param_buf._version != self._wt_version:
             return None
+        if self.mode == "zero":
+            b = self.space.param_bucket[i].index
+            if not self._wt_valid.get(b, False):
+                return None
+            ev = self._wt_ready.pop(b, None)
+            if ev is not None:  # the side-stream transposes of this bucket
+                torch.cuda.current_stream(self.space.param_buf.device).wait_event(ev)
         return self._wt_views.get(i)
+
+    def _transpose_bucket(self, i, work):
+        """ZeRO: W^T of bucket i's matrices once its all-gather (`work`) has landed."""
+        ent = self._wt_bucket_mats.get(i) if self._wt_buf is not None and self.mode == "zero" else None
+        if ent is None:
+            return
+        mats_dev, mats_host, ntiles = ent
+        st = self._wt_stream
+        if st is None:  # CPU engine (gloo tests): in order
+            if work is not None:
+                work.wait()
+            torch.ops.dtg.transpose_mats_(self.space.param_buf.data, self._wt_buf, mats_dev, mats_host, ntiles)
+        else:
+            st.wait_stream(torch.cuda.current_stream(st.device))
+            with torch.cuda.stream(st):
+                if work is not None:
+                    work.wait()  # the side stream waits for the collective, the host does not
+                torch.ops.dtg.transpose_mats_(self.space.param_buf.data, self._wt_buf, mats_dev, mats_host, ntiles)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            self._wt_ready[i] = ev
+        self._wt_valid[i] = True
 
     # ------------------------------------------------------------------ grad sync
     @contextlib.contextmanager
@@ -341,12 +398,18 @@ class DataParallel:
             grad_scale = 1.0 / (self.grad_divisor * max(1, self.accum_count))
         if self.mode == "zero":
             self.wait_param_gather()  # never update a slice an all-gather may still be reading
+            if self._wt_stream is not None:  # ... or a W^T transpose
+                torch.cuda.current_stream(self._wt_stream.device).wait_stream(self._wt_stream)
             for (s, e), o in zip(self.shard_ranges, self.shard_offsets):
                 n = e - s
                 adamw_step(self.space.param_buf[s:e], self.grad_shard[o:o + n], self.exp_avg[o:o + n],
                            self.exp_avg_sq[o:o + n], lr=lr, step=self.step_count, beta1=beta1, beta2=beta2,
                            eps=eps, weight_decay=weight_decay, grad_scale=grad_scale,
                            master=None if self.master is None else self.master[o:o + n], hyper=self.graph_hyper)
+            if self._wt_buf is not None:
+                self._wt_version = self.space.param_buf._version
+                for b in self._wt_valid:
+                    self._wt_valid[b] = False  # until the bucket's gather + transposes are issued
             self._allgather_params(wait=not self.overlap_param_gather)
         elif self._wt_buf is not None:  # same update + every weight's W^T for the next backward
             torch.ops.dtg.adamw_t_(self.space.param_buf, self.master, self.space.grad_buf, self.exp_avg,
@@ -380,6 +443,7 @@ class DataParallel:
         src = buf[s:e]
         self._pending_ag[i] = comm.all_gather_into(buf[b.start:b.end], src.clone() if gloo else src,
                                                    group=self.group, async_op=True)
+        self._transpose_bucket(i, self._pending_ag[i])
 
     def wait_param_gather(self, buckets=None):
         for i in (list(self._pending_ag) if buckets is None else buckets):

@@ -271,6 +271,7 @@ class FullyShard:
         self.accum_count = 0
         self._sync_enabled = True
         self._first_micro = True
+        self._final_micro = True
         set_direct_loss_grad(True)
 
     # ------------------------------------------------------------------ memory helpers
@@ -436,16 +437,26 @@ class FullyShard:
     def _complete_rs(self, u, work, out, first, direct):
         if work is not None:
             work.wait()
-        if self.replicas > 1:
-            # HYBRID: this micro-batch's shard summed over the replicas (linear, so summing per
-            # micro-batch equals summing the accumulated shard).  RCCL: wait() only orders the
-            # current stream behind the all-reduce; the host keeps queueing backward kernels.
+        merged = False
+        if self.replicas > 1 and self._final_micro:
+            # HYBRID: the shard summed over the replicas once per optimizer step, on the last
+            # micro-batch: earlier micro-batches accumulate locally (no inter-replica traffic)
+            # and their sum joins this micro-batch's shard before the one all-reduce.  RCCL:
+            # wait() only orders the current stream behind it; the host keeps queueing kernels.
+            if not first:
+                gs = self._shard_view(u, self.shard_grads)
+                if gs.device.type == "cpu":
+                    self._sync_d2h()
+                    out.add_(gs.to(out.device, non_blocking=False))
+                else:
+                    out.add_(gs)
+                merged = True
             ar = dist.all_reduce(out, group=self.replicate_group, async_op=True)
             ar.wait()
         ev = None
         if not direct:
             gs = self._shard_view(u, self.shard_grads)
-            if first and self._d2h_stream is not None and gs.device.type == "cpu":
+            if (first or merged) and self._d2h_stream is not None and gs.device.type == "cpu":
                 # offload: the gradient shard goes to pinned host memory on a side stream, so the
                 # host thread keeps queueing backward kernels; the host update (or step()) waits
                 # for the copy's event
@@ -457,7 +468,7 @@ class FullyShard:
                     ev.record(self._d2h_stream)
                 out.record_stream(self._d2h_stream)
                 self._d2h_events.append(ev)
-            elif first:
+            elif first or merged:
                 gs.copy_(out)
             else:
                 self._sync_d2h()  # the previous micro-batch's copy into gs must have landed
@@ -543,6 +554,7 @@ class FullyShard:
                                "update (overlap_cpu_step); call step()/zero_grad() first, or mark earlier "
                                "micro-batches with no_sync() / last_microbatch=False")
         final = (not self._in_no_sync) if last_microbatch is None else bool(last_microbatch)
+        self._final_micro = final  # HYBRID: the replica all-reduce runs on the final micro-batch only
         overlap = (self.cpu_offload and self.overlap_cpu_step and self._hparams is not None and final)
         if overlap:  # the last micro-batch: its per-unit gradient shards are final on arrival
             scale = 1.0 / (self.world * self.replicas * (self.accum_count + 1))

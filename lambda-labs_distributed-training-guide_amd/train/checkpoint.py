@@ -51,6 +51,33 @@ def has_checkpoint(exp_dir) -> bool:
 # old state.json, and never loses the last complete checkpoint.
 PENDING = ".pending"
 COMMIT = "COMMIT"
+# Durability (host crash / power loss, not just a dead process): every payload file is fsynced
+# by its writer, every directory whose entries changed is fsynced, and the COMMIT marker is
+# written only after all of that -- so a durable COMMIT always sits next to complete payload,
+# and the roll-forward may delete the old copy.
+
+
+def fsync_file(path) -> None:
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def fsync_dir(path) -> None:
+    """Make the directory's entries (creations, renames) durable."""
+    fd = os.open(path, os.O_RDONLY | getattr(os, "O_DIRECTORY", 0))
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def save_durable(obj, path) -> None:
+    """torch.save + fsync of the file."""
+    torch.save(obj, path)
+    fsync_file(path)
 
 
 def _roll_forward(exp_dir: Path):
@@ -63,19 +90,26 @@ def _roll_forward(exp_dir: Path):
         if dst.is_dir():
             shutil.rmtree(dst)
         os.replace(item, dst)
+    fsync_dir(exp_dir)  # the new payload's entries are durable before state.json points at them
     if (pend / "state.json").exists():
         os.replace(pend / "state.json", exp_dir / "state.json")
+        fsync_dir(exp_dir)
     shutil.rmtree(pend, ignore_errors=True)
 
 
 def commit_pending(exp_dir):
-    """Rank 0, after every rank finished writing into .pending: publish it atomically."""
+    """Rank 0, after every rank finished writing (and fsyncing) into .pending: publish it
+    atomically."""
     exp_dir = Path(exp_dir)
-    marker = exp_dir / PENDING / COMMIT
+    pend = exp_dir / PENDING
+    for sub in [pend] + [d for d in pend.iterdir() if d.is_dir()]:
+        fsync_dir(sub)  # every payload entry is durable before the marker exists
+    marker = pend / COMMIT
     with open(marker, "w") as fp:
         fp.write("ok\n")
         fp.flush()
         os.fsync(fp.fileno())
+    fsync_dir(pend)
     _roll_forward(exp_dir)
 
 
@@ -337,10 +371,13 @@ def write_sharded(ckpt_dir, tensors, entry, meta):
     ckpt_dir = Path(ckpt_dir)
     ckpt_dir.mkdir(parents=True, exist_ok=True)
     if entry["index"]:
-        torch.save(tensors, ckpt_dir / entry["file"])
+        save_durable(tensors, ckpt_dir / entry["file"])
     if meta is not None:
         with open(ckpt_dir / INDEX, "w") as fp:
             json.dump(meta, fp)
+            fp.flush()
+            os.fsync(fp.fileno())
+    fsync_dir(ckpt_dir)
 
 
 def save_sharded(ckpt_dir, engine, global_step=None):
@@ -557,7 +594,7 @@ class CheckpointManager:
             pend = self.exp_dir / self.PENDING
             pend.mkdir(parents=True, exist_ok=True)
             for rel, obj in jobs:
-                torch.save(obj, pend / rel)
+                save_durable(obj, pend / rel)
             if shard is not None:
                 write_sharded(pend / "checkpoint", *shard)
         except BaseException as e:  # surfaced by finalize() on the main thread
@@ -567,13 +604,12 @@ class CheckpointManager:
         """Rank 0: the small files into .pending, then the atomic commit."""
         pend = self.exp_dir / self.PENDING
         pend.mkdir(parents=True, exist_ok=True)
-        torch.save(sched_sd, pend / "lr_scheduler.pt")
-        if isinstance(rng, _RngBox):
-            torch.save(rng.obj, pend / "rng.pt")
-        else:
-            torch.save(rng, pend / "rng.pt")
+        save_durable(sched_sd, pend / "lr_scheduler.pt")
+        save_durable(rng.obj if isinstance(rng, _RngBox) else rng, pend / "rng.pt")
         with open(pend / "state.json", "w") as fp:
             json.dump(state, fp)
+            fp.flush()
+            os.fsync(fp.fileno())
         commit_pending(self.exp_dir)
 
     def finalize(self):

@@ -53,9 +53,10 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                             "all-gathers and reduce-scatters on the copy engines, one stream per peer (no CU "
                             "time under the overlapped GEMMs)")
         p.add_argument("--tp-comm-mb", default=256, type=int, help="xGMI workspace per rank (largest TP message)")
-        p.add_argument("--tp-comm-timeout", default=60.0, type=float,
-                       help="seconds an xGMI barrier waits for a peer before the collective fails; the job then "
-                            "exits non-zero at the next log step / checkpoint")
+        p.add_argument("--tp-comm-timeout", default=None, type=float,
+                       help="seconds an xGMI barrier waits for a peer before the collective fails (default: "
+                            "DTG_XGMI_TIMEOUT, else 60; this flag wins over the variable); the job then exits "
+                            "non-zero at the end of that step")
         p.add_argument("--tp-overlap-chunks", default=2, type=int,
                        help="row chunks of the overlapped sequence-parallel regions (parallel/async_tp.py): the "
                             "all-gather / reduce-scatter of one chunk runs under the GEMMs of the next; 1 = off")

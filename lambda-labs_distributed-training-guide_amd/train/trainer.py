@@ -99,6 +99,17 @@ def _scheduler(args, opt):
     return torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=1000, eta_min=args.lr * 1e-2)
 
 
+def xgmi_timeout(flag) -> float:
+    """xGMI barrier timeout: an explicit --tp-comm-timeout wins over DTG_XGMI_TIMEOUT (logged
+    when they disagree), which wins over the 60 s default."""
+    env = os.environ.get("DTG_XGMI_TIMEOUT")
+    if flag is not None:
+        if env is not None and float(env) != float(flag):
+            LOGGER.warning(f"--tp-comm-timeout {flag:g} overrides DTG_XGMI_TIMEOUT={env}")
+        return float(flag)
+    return float(env) if env is not None else 60.0
+
+
 def _build(args, chapter, device, world):
     """Model + engine + optimizer for a chapter.  Returns (model, engine, dp_size, dp_rank, ckpt_style)."""
     depth = getattr(args, "num_layers", None)
@@ -119,7 +130,7 @@ def _build(args, chapter, device, world):
             from ..utils import comm as _comm
 
             engine = "dma" if args.tp_comm == "xgmi-dma" else "kernel"
-            timeout = float(os.environ.get("DTG_XGMI_TIMEOUT", getattr(args, "tp_comm_timeout", 60.0)))
+            timeout = xgmi_timeout(getattr(args, "tp_comm_timeout", None))
             _comm.register_xgmi(tp_group, XgmiCommunicator(tp_group, capacity_bytes=args.tp_comm_mb << 20, device=device,
                                                            gather_engine=engine, timeout_s=timeout))
             LOGGER.info(f"tp collectives: direct-peer xGMI ({args.tp_comm_mb} MiB workspace per rank, "
@@ -272,12 +283,20 @@ def run(chapter: str, argv=None):
     resumed = False
     mgr = CheckpointManager(exp_dir, engine, opt, lr_scheduler, style, local_rank,
                             async_save=getattr(args, "async_ckpt", "off") == "on")
-    if rank == 0 and exp_dir.exists():  # finish (or discard) a save interrupted by a crash
+    # DTG_FAKE_WORLD rehearsal: the other ranks are a fake process group, so its weights are
+    # not a training result -- never resume into it, never write (or journal-commit) a checkpoint
+    fake = udist.fake_world() > 1
+    if fake:
+        if has_checkpoint(exp_dir) or (exp_dir / CheckpointManager.PENDING).exists():
+            raise SystemExit(f"DTG_FAKE_WORLD rehearsal refuses to run in {exp_dir}: it holds a checkpoint "
+                             "(a rehearsal's state is not a training result); use a fresh --experiment-name")
+        LOGGER.warning("DTG_FAKE_WORLD rehearsal: checkpoint saving disabled")
+    elif rank == 0 and exp_dir.exists():  # finish (or discard) a save interrupted by a crash
         how = recover_checkpoint(exp_dir)
         if how != "clean":
             LOGGER.warning(f"{exp_dir}: interrupted checkpoint save {how}")
     udist.barrier()
-    if has_checkpoint(exp_dir):
+    if not fake and has_checkpoint(exp_dir):
         LOGGER.info(f"Resuming from {exp_dir}")
         state = mgr.load()
         resumed = True
@@ -396,6 +415,9 @@ def run(chapter: str, argv=None):
                 torch.distributed.all_reduce(loss_sum, group=model._dtg_seq[1])
             state["global_step"] += 1
             state["epoch_step"] += 1
+            # host read of the xGMI communicators' pinned error words (no device sync): a peer
+            # lost in this step's barriers stops the job here, not at the next log step
+            ucomm.poll_xgmi()
             if args.torch_profile_steps > 0:
                 prof = _profile_tick(prof, state["global_step"], prof_start, prof_stop, exp_dir, rank, device)
             # summed on the device; one host sync per --log-freq window / checkpoint instead of the
@@ -431,7 +453,7 @@ def run(chapter: str, argv=None):
                 for t in timers.values():
                     t.reset()
 
-            if state["global_step"] % args.ckpt_freq == 0:
+            if state["global_step"] % args.ckpt_freq == 0 and not fake:
                 ucomm.check_xgmi()  # never checkpoint state computed from stale peer data
                 LOGGER.info("Saving checkpoint.")
                 mgr.save(state)

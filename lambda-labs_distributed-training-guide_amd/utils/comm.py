@@ -45,6 +45,14 @@ def check_xgmi():
         c.check()
 
 
+def poll_xgmi():
+    """Like check_xgmi() but without synchronising the device: reads each communicator's
+    host-pinned error word (written by a barrier kernel that timed out).  Cheap enough for
+    every training step."""
+    for c in list(_XGMI.values()):
+        c.check(sync=False)
+
+
 def rs_input_buffer(group, shape, dtype, stage_bytes: int = 0):
     """Zero-copy reduce-scatter input: a workspace slot of the group's xGMI communicator for a
     producer to write into, or None (no communicator / does not fit)."""

@@ -42,6 +42,7 @@ def init_distributed(backend: Optional[str] = None, timeout_minutes: int = 30, l
     # real W-rank job; the numerics are not (a memory / per-rank-compute rehearsal only).
     fake_world = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0)
     if fake_world > 1:
+        check_fake_world_env(fake_world)
         rank, world = 0, fake_world
     local_rank = local_rank_arg if local_rank_arg is not None else _env_int(
         "LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID", "MPI_LOCALRANKID", default=None)
@@ -70,11 +71,49 @@ def init_distributed(backend: Optional[str] = None, timeout_minutes: int = 30, l
         return 0, 0, world, torch.device("cuda:0") if cuda else torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         backend = backend or ("nccl" if cuda and not shared else "gloo")
-        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(minutes=timeout_minutes))
+        timeout = datetime.timedelta(minutes=timeout_minutes)
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=timeout)
         if backend == "nccl":
             kw["device_id"] = device
+        store = elastic_store(world, timeout)
+        if store is not None:
+            kw["store"] = store
         dist.init_process_group(**kw)
     return rank, local_rank, world, device
+
+
+def elastic_store(world: int, timeout):
+    """Under torchrun: the agent's TCPStore with a per-restart-attempt key prefix, else None.
+
+    torchrun keeps one agent-hosted store for every restart of the worker group and the env://
+    rendezvous adds no per-attempt prefix, so after an elastic restart the
+    process-group bootstrap can read a previous attempt's keys -- gloo's full-mesh connect then
+    dials a dead worker's port and every later attempt inherits the stale keys
+    (tests/test_elastic_cpu.py reproduced it under load).  Attempt N's keys live under
+    attempt_N here."""
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") != "True" or "MASTER_ADDR" not in os.environ:
+        return None
+    store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, is_master=False,
+                          timeout=timeout)
+    return dist.PrefixStore(f"dtg/attempt_{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}", store)
+
+
+def fake_world() -> int:
+    """W of a DTG_FAKE_WORLD=W one-rank rehearsal, else 0."""
+    return int(os.environ.get("DTG_FAKE_WORLD", "0") or 0)
+
+
+def check_fake_world_env(fake: int, env=None) -> None:
+    """A rehearsal is ONE process.  DTG_FAKE_WORLD leaking into a real launcher's job would turn
+    every rank into "rank 0 on cuda:0" training on no-op collectives without an error, so it is
+    refused whenever a launcher says this process is one of several."""
+    env = os.environ if env is None else env
+    if "TORCHELASTIC_RUN_ID" in env:
+        raise RuntimeError("DTG_FAKE_WORLD is set inside a torchrun job; unset it (rehearsals are one process)")
+    for k in ("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "SLURM_NTASKS", "PMI_SIZE"):
+        v = env.get(k)
+        if v not in (None, "") and int(v) > 1 and int(v) != fake:
+            raise RuntimeError(f"DTG_FAKE_WORLD={fake} but the launcher set {k}={v}; unset DTG_FAKE_WORLD")
 
 
 def get_rank() -> int:

@@ -31,7 +31,20 @@ def main():
     a = ap.parse_args()
     # a bounded rendezvous/connect: a worker whose mesh connect fails must exit (and let torchrun
     # restart the group) instead of waiting out the 30-minute default
-    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=a.pg_timeout))
+    timeout = datetime.timedelta(seconds=a.pg_timeout)
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+        # torchrun keeps ONE agent-hosted TCPStore for every restart of the worker group, and
+        # init_process_group's env:// path adds no per-attempt prefix: gloo's full-mesh
+        # bootstrap then finds a peer's listening address from a previous attempt already in
+        # the store, connects to a dead port ("Connection refused") and the failed attempt
+        # leaves stale keys for the next one.  Keys of attempt N live under attempt_N instead.
+        store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]),
+                              int(os.environ["WORLD_SIZE"]), is_master=False, timeout=timeout)
+        store = dist.PrefixStore(f"toy/attempt_{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}", store)
+        dist.init_process_group("gloo", store=store, rank=int(os.environ["RANK"]),
+                                world_size=int(os.environ["WORLD_SIZE"]), timeout=timeout)
+    else:
+        dist.init_process_group("gloo", timeout=timeout)
     rank, world = dist.get_rank(), dist.get_world_size()
     state = {"num_steps": 0}
     if os.path.exists(a.state):

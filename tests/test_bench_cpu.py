@@ -2,6 +2,7 @@
 whole-job tokens/s, n_gpus / steps / warmup echoed, weak-scaling global batch, for N=1 and for
 torchrun N=2 (gloo)."""
 import json
+import math
 import os
 import subprocess
 import sys
@@ -13,7 +14,8 @@ from _dist import free_port
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--batch-size", "2", "--seq-len", "64",
         "--tunableop", "off", "--fsdp-mem-model", "llama-tiny", "--fsdp-mem-batch", "2", "--fsdp-mem-seq", "64",
-        "--fsdp-mem-steps", "1", "--numel-to-wrap", "10000", "--coll-sweep-mb", "1,2"]
+        "--fsdp-mem-steps", "1", "--numel-to-wrap", "10000", "--coll-sweep-mb", "1,2",
+        "--bucket-sweep-mb", "1,4", "--sweep-steps", "1", "--ref-steps", "2"]
 
 
 def _json_lines(out):
@@ -29,12 +31,23 @@ def _check(rec, n):
     assert rec["world_size_seen_by_pg"] == n and len(rec["rank_devices"]) == n
     assert rec["rank_ms_per_step"]["max"] >= rec["rank_ms_per_step"]["min"] > 0
     assert rec["fsdp_mem"]["peak_gb_max_rank"] >= rec["fsdp_mem"]["valley_gb_max_rank"] >= 0
+    # fresh uniform ids every step: the loss is a tripwire around ln(V) (llama-tiny: V = 512)
+    lo, hi = rec["loss_band"]
+    assert lo < rec["final_loss"] < hi and abs(rec["final_loss"] - math.log(512)) < 0.5
+    # reference-mode throughput (synchronised phase timers) next to the async headline
+    assert rec["reference_timer_steps"] == 2 and rec["tok_s_reference_timers"] > 0
+    assert set(rec["reference_timer_ms"]) == {"data", "forward", "backward", "update"}
     if n > 1:  # the collective sweep after the timed region (gloo: all-gather + all-reduce)
         ops = {(c["op"], c["mib"]) for c in rec["collectives"]}
         assert {("all_gather", 1), ("all_reduce", 2)} <= ops
         assert all(c["busbw_gbs"] > 0 for c in rec["collectives"])
+        assert rec["replicas_consistent"] is True
+        if rec["config"]["parallelism"].startswith(f"dp{n}-"):
+            assert [r["bucket_mb"] for r in rec["bucket_sweep"]] == [1, 4]
+            assert all(r["ms_per_step"] > 0 for r in rec["bucket_sweep"])
+        assert "rccl" not in rec  # gloo: no RCCL communicator to diagnose
     else:
-        assert "collectives" not in rec
+        assert "collectives" not in rec and "bucket_sweep" not in rec and "replicas_consistent" not in rec
 
 
 @pytest.mark.slow
@@ -117,3 +130,33 @@ def test_bench_fake_world_rehearsal_is_labelled():
     assert rec["config"]["global_batch"] == 16 and rec["config"]["parallelism"] == "dp8-zero"
     assert "collectives" not in rec
     assert abs(rec["value"] - 8 * 2 * 64 * 2 / (rec["ms_per_step"] * 2 / 1000)) < 0.02 * rec["value"]
+
+
+RCCL_LOG = """\
+box:1234:1234 [0] NCCL INFO RCCL version : 2.26.6-HEAD:abcdef
+box:1234:1234 [0] NCCL INFO comm 0x55d0 rank 0 nRanks 8 nNodes 1 localRanks 8 localRank 0 MNNVL 0
+box:1234:1234 [0] NCCL INFO Channel 00/16 :    0   1   2   3   4   5   6   7
+box:1234:1234 [0] NCCL INFO Channel 15/16 :    0   7   6   5   4   3   2   1
+box:1234:1234 [0] NCCL INFO 16 coll channels, 16 collnet channels, 0 nvls channels, 32 p2p channels, 4 p2p channels per peer
+box:1234:1234 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC
+box:1234:1234 [0] NCCL INFO Channel 01/0 : 0[0] -> 7[7] via P2P/IPC
+box:1234:1234 [0] NCCL INFO Channel 02/0 : 0[0] -> 1[1] [send] via SHM/direct/direct
+box:1234:1234 [0] NCCL INFO ncclCommInitRankConfig comm 0x55d0 rank 0 nranks 8 cudaDev 0 busId 5000 - Init COMPLETE
+"""
+
+
+def test_rccl_log_parse_and_preset():
+    """What the N > 1 bench line reports about RCCL: version, communicator shape, channels and
+    the transport of every connection, parsed from its INFO log; the preset never overrides an
+    exported variable."""
+    from dtg.utils import rccl
+
+    rec = rccl.parse_log(RCCL_LOG)
+    assert rec["version"].startswith("2.26.6")
+    assert rec["communicators"] == [{"rank": 0, "nranks": 8, "nnodes": 1, "local_ranks": 8}]
+    assert rec["channels_max"] == 16 and rec["coll_channels"] == [16] and rec["p2p_channels_per_peer"] == [4]
+    assert rec["transports"] == {"P2P/IPC": 2, "SHM/direct/direct": 1}
+    env = {"TORCH_NCCL_HIGH_PRIORITY": "0"}
+    applied = rccl.apply_preset("node", env)
+    assert env["TORCH_NCCL_HIGH_PRIORITY"] == "0" and "TORCH_NCCL_HIGH_PRIORITY" not in applied
+    assert applied["HSA_NO_SCRATCH_RECLAIM"] == "1" and rccl.apply_preset("none", env) == {}

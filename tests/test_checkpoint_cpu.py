@@ -288,3 +288,39 @@ def test_interrupted_save_keeps_previous_checkpoint(tmp_path):
     assert recover_checkpoint(tmp_path) == "rolled-forward"
     assert json.loads((tmp_path / "state.json").read_text())["global_step"] == 9 and not pend.exists()
     assert CheckpointManager(tmp_path, eng, opt, sched, "full").load()["global_step"] == 9
+
+
+@pytest.mark.parametrize("style", ["full", "dp"])
+def test_every_payload_is_fsynced_before_commit(tmp_path, monkeypatch, style):
+    """a durable COMMIT marker must never sit next to payload a power loss could
+    truncate.  Every file of the save (model / optimizer / shards / index / lr_scheduler / rng /
+    state.json) and the .pending directory are fsynced BEFORE the marker is written, and the
+    experiment directory after the roll-forward's renames."""
+    import os as _os
+
+    from dtg.train.checkpoint import CheckpointManager, new_state
+
+    events = []
+    real = _os.fsync
+
+    def spy(fd):
+        events.append(_os.readlink(f"/proc/self/fd/{fd}"))
+        return real(fd)
+
+    monkeypatch.setattr(_os, "fsync", spy)
+    m, eng, opt = _make("single")
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10)
+    st = new_state()
+    st["global_step"] = 3
+    CheckpointManager(tmp_path, eng, opt, sched, style).save(st)
+    marker = next(i for i, e in enumerate(events) if e.endswith("/.pending/COMMIT"))
+    before = set(events[:marker])
+    pend = str(tmp_path / ".pending")
+    payload = ["lr_scheduler.pt", "rng.pt", "state.json", "model.pt"]
+    payload += ["optimizer.pt"] if style == "full" else ["checkpoint/index.json", "checkpoint/shard_r00000.pt",
+                                                          "checkpoint"]
+    for rel in payload:
+        assert f"{pend}/{rel}" in before, rel
+    assert pend in before  # the directory entries of the payload
+    assert str(tmp_path) in events[marker + 1:]  # the renames into exp_dir
+    assert (tmp_path / "state.json").exists() and not (tmp_path / ".pending").exists()

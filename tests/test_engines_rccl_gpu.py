@@ -21,9 +21,9 @@ STEPS = 3
 SPIN = 20_000_000  # ~10 ms at ~2 GHz
 
 
-def _batches(vocab):
+def _batches(vocab, S=128):
     g = torch.Generator().manual_seed(0)
-    return [torch.randint(0, vocab, (4, 128), generator=g) for _ in range(STEPS)]
+    return [torch.randint(0, vocab, (4, S), generator=g) for _ in range(STEPS)]
 
 
 def _install_delay():
@@ -47,7 +47,7 @@ def _install_delay():
         setattr(dist, name, wrap(getattr(dist, name)))
 
 
-def _train(kind, force, delay, accum=1):
+def _train(kind, force, delay, accum=1, S=128, count_wt=False):
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
 
@@ -66,7 +66,19 @@ def _train(kind, force, delay, accum=1):
     opt = FlatAdamW(eng, lr=1e-3)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))
     losses = []
-    for ids in _batches(cfg.vocab_size):
+    used = []
+    if count_wt:  # which backward dX GEMMs got the engine's W^T copy instead of transposing
+        import dtg.ops.functional as F_
+
+        real = F_._wt
+
+        def counting(w):
+            ref = getattr(w, "_dtg_wt", None)
+            used.append(ref is not None and ref[0].weight_t(ref[1]) is not None)
+            return real(w)
+
+        F_._wt = counting
+    for ids in _batches(cfg.vocab_size, S):
         ids = ids.to(dev)
         opt.zero_grad()
         for j, mb in enumerate(ids.chunk(accum)):
@@ -78,6 +90,9 @@ def _train(kind, force, delay, accum=1):
         sched.step()
         losses.append(out.loss.item())
     mode = eng.mode
+    if count_wt:
+        F_._wt = real
+        return used, losses, mode
     if kind == "fsdp":
         sd = eng.full_state_dict(rank0_only=False)
         return {k: v.cpu() for k, v in sd.items()}, losses, mode
@@ -86,13 +101,13 @@ def _train(kind, force, delay, accum=1):
     return {n: p.detach().cpu().clone() for n, p in model.named_parameters()}, losses, mode
 
 
-def _worker(rank, world, kind, delay, accum):
-    return _train(kind, True, delay, accum)
+def _worker(rank, world, kind, delay, accum, S=128, count_wt=False):
+    return _train(kind, True, delay, accum, S, count_wt)
 
 
-def _single(kind, accum):
+def _single(kind, accum, S=128):
     torch.cuda.set_device(0)
-    return _train("single" if kind != "fsdp" else "fsdp", False, False, accum)
+    return _train("single" if kind != "fsdp" else "fsdp", False, False, accum, S)
 
 
 @pytest.mark.parametrize("kind", ["ddp", "zero", "fsdp"])
@@ -165,3 +180,19 @@ def test_fsdp_resident_param_offload_bit_identical_on_gpu(cuda, overlap, accum):
     for r in range(2):
         for n, t in full[r][0].items():
             assert torch.equal(res[r][0][n], t), (r, n)
+
+
+def test_rccl_world1_zero_weight_t_with_delayed_gathers(cuda):
+    """ZeRO's W^T copies are rebuilt per bucket on a side stream after the bucket's parameter
+    all-gather lands (parallel/data_parallel.py).  With every all-gather delayed ~10 ms on the
+    GPU, a transpose that did not wait for its gather would copy the pre-update weights and the
+    dX GEMMs would use them: training must stay bit-identical to the single-device engine (whose
+    copies the optimizer kernel writes), and every backward dX GEMM at >= 4096 tokens must use
+    a copy (no per-weight transposes in the backward)."""
+    ref, ref_losses, _ = _single("zero", 1, S=1024)
+    (params, losses, mode), = run_distributed(_worker, 1, "zero", True, 1, 1024, backend="nccl")
+    assert mode == "zero" and losses == ref_losses
+    for n, v in ref.items():
+        assert torch.equal(params[n], v), n
+    (used, _, _), = run_distributed(_worker, 1, "zero", True, 1, 1024, True, backend="nccl")
+    assert used and all(used), f"{used.count(False)} of {len(used)} dX GEMMs transposed W in the backward"

@@ -90,7 +90,9 @@ def test_size_policy_units():
     assert all(not getattr(u, "_dtg_param_holder", False) for u in units)
 
 
-def _hybrid_train(rank, world, model_name, batches, shard):
+def _hybrid_train(rank, world, model_name, batches, shard, accum=1, offload=False):
+    import torch.distributed as dist
+
     from dtg.models import build_model
     from dtg.parallel.data_parallel import FlatAdamW
     from dtg.parallel.fsdp import FullyShard
@@ -99,16 +101,32 @@ def _hybrid_train(rank, world, model_name, batches, shard):
     torch.manual_seed(0)
     replicate, shard_group, _, _, n_rep = make_mesh(shard)
     model = build_model(model_name, device="cpu", dtype=torch.float32)
-    eng = FullyShard(model, group=shard_group, replicate_group=replicate, device="cpu")
+    eng = FullyShard(model, group=shard_group, replicate_group=replicate, device="cpu", cpu_offload=offload)
     opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
-    for ids in batches:
-        per = ids.shape[0] // world
-        mine = ids[rank * per:(rank + 1) * per]
-        opt.zero_grad()
-        out = model(input_ids=mine, labels=mine)
-        eng.backward(out.loss)
-        opt.step()
-    return eng.full_state_dict(rank0_only=False), eng.mode, eng.world, eng.replicas
+    n_rep_ar = [0]
+    real = dist.all_reduce
+
+    def counting(t, *a, group=None, **kw):
+        if group is replicate:
+            n_rep_ar[0] += 1
+        return real(t, *a, group=group, **kw)
+
+    dist.all_reduce = counting
+    try:
+        for ids in batches:
+            per = ids.shape[0] // world
+            mine = ids[rank * per:(rank + 1) * per]
+            opt.zero_grad()
+            for j, mb in enumerate(mine.chunk(accum)):
+                if j < accum - 1:
+                    with eng.no_sync():
+                        eng.backward(model(input_ids=mb, labels=mb).loss)
+                else:
+                    eng.backward(model(input_ids=mb, labels=mb).loss)
+            opt.step()
+    finally:
+        dist.all_reduce = real
+    return eng.full_state_dict(rank0_only=False), eng.mode, eng.world, eng.replicas, n_rep_ar[0], len(eng.all_units)
 
 
 def test_hybrid_shard_matches_single():
@@ -117,8 +135,23 @@ def test_hybrid_shard_matches_single():
     ref, _ = _train("llama-tiny", "single", 0, 1, batches)
     res = run_distributed(_hybrid_train, 4, "llama-tiny", batches, 2)
     for r in range(4):
-        sd, mode, w, reps = res[r]
+        sd, mode, w, reps, _, _ = res[r]
         assert (mode, w, reps) == ("hybrid", 2, 2)
+        for n in ref:
+            torch.testing.assert_close(sd[n], ref[n], **TOL, msg=f"rank {r} {n}")
+
+
+@pytest.mark.parametrize("offload", [False, True])
+def test_hybrid_shard_accumulation_one_replica_allreduce_per_step(offload):
+    """with 2 accumulated micro-batches the inter-replica all-reduce runs once per
+    unit per optimizer step (on the final micro-batch, over the accumulated shard), not once per
+    micro-batch -- and the result still equals single-process training on the full batch."""
+    batches = _batches(512, 8, 16)
+    ref, _ = _train("llama-tiny", "single", 0, 1, batches)
+    res = run_distributed(_hybrid_train, 4, "llama-tiny", batches, 2, 2, offload)
+    for r in range(4):
+        sd, mode, _, _, n_ar, n_units = res[r]
+        assert mode == "hybrid" and n_ar == n_units * len(batches), (n_ar, n_units)
         for n in ref:
             torch.testing.assert_close(sd[n], ref[n], **TOL, msg=f"rank {r} {n}")
 

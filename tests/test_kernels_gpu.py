@@ -94,6 +94,32 @@ def test_transpose2d(cuda, R, C, ld, group, tile, monkeypatch):
     assert torch.equal(y.cpu(), x.t().contiguous())
 
 
+def test_transpose_mats_batched(cuda):
+    """One launch transposing several matrices of a flat buffer (ZeRO's per-bucket W^T rebuild)
+    == per-matrix transposes, ragged edge tiles included; a descriptor out of range is refused
+    on the host before any launch."""
+    torch.manual_seed(0)
+    shapes = [(64, 128), (520, 136), (8, 4096), (4096, 8)]
+    n = sum(r * c for r, c in shapes)
+    x = torch.randn(n).bfloat16()
+    desc, so, do, t0 = [], 0, 0, 0
+    for r, c in shapes:
+        desc.append([so, r, c, n - do - r * c, t0])  # destinations in reverse order
+        so += r * c
+        do += r * c
+        t0 += -(-r // 64) * -(-c // 64)
+    h = torch.tensor(desc, dtype=torch.long)
+    out = torch.zeros(n, dtype=torch.bfloat16, device=cuda)
+    torch.ops.dtg.transpose_mats_(x.to(cuda), out, h.to(cuda), h, t0)
+    ref = torch.zeros(n, dtype=torch.bfloat16)
+    torch.ops.dtg.transpose_mats_(x, ref, h, h, t0)
+    assert torch.equal(out.cpu(), ref)
+    bad = h.clone()
+    bad[1, 3] = n  # destination past the end
+    with pytest.raises(RuntimeError, match="out of range"):
+        torch.ops.dtg.transpose_mats_(x.to(cuda), out, bad.to(cuda), bad, t0)
+
+
 @pytest.mark.parametrize("group", ["0", "3", "16"])
 @pytest.mark.parametrize("tile", ["64x64", "64x128", "128x64", "128x128"])
 @pytest.mark.parametrize("T,I", [(64, 64), (4096, 1792), (520, 136)])
