@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import time
 from collections import deque
 from typing import Callable, Dict, Iterable, List, Optional, Sequence
 
@@ -133,7 +134,8 @@ class FullyShard:
                  device=None, reshard_after_forward: bool = True, cpu_offload: bool = False,
                  state_dtype=torch.bfloat16, init_fn: Optional[Callable] = None, seed: int = 0,
                  prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None, replicate_group=None,
-                 overlap_cpu_step: bool = True, force_collectives: bool = False, offload_params: bool = True):
+                 overlap_cpu_step: bool = True, force_collectives: bool = False, offload_params: bool = True,
+                 grad_ring: int = 0):
         self.module = model
         self.group = group
         # HYBRID_SHARD (ZeRO++-style): shard inside `group` (one node's xGMI island), replicate
@@ -196,8 +198,20 @@ class FullyShard:
         total = sum(u.shard_numel for u in all_units)
         home = torch.device("cpu") if cpu_offload else self.device
         pin = cpu_offload and torch.cuda.is_available()
-        self.shard_params = torch.zeros(total, dtype=self.dtype, device=home, pin_memory=pin)
-        self.shard_grads = torch.zeros(total, dtype=self.dtype, device=home, pin_memory=pin)
+        # grad_ring=K (CPU offload with the overlapped host step): no host gradient shard for the
+        # whole model -- each unit's reduced gradient lands in one of K unit-sized pinned slots,
+        # the host AdamW of that unit consumes it, and the slot is reused.  Saves 2 B per
+        # parameter of host RAM (101 GB per rank for Llama-3.1-405B at W = 8: the difference
+        # between fitting eight ranks' offloaded state in one node's 3 TB or not).
+        self.grad_ring = int(grad_ring) if cpu_offload else 0
+        if pin:  # exact-size page-locked buffers (the caching host allocator rounds to 2^k)
+            from ..utils.pinned import pinned_zeros
+
+            self.shard_params = pinned_zeros(total, self.dtype)
+            self.shard_grads = pinned_zeros(total if not self.grad_ring else 0, self.dtype)
+        else:
+            self.shard_params = torch.zeros(total, dtype=self.dtype, device=home)
+            self.shard_grads = torch.zeros(total if not self.grad_ring else 0, dtype=self.dtype, device=home)
         self.exp_avg = torch.zeros(total, dtype=state_dtype, device=home)
         self.exp_avg_sq = torch.zeros(total, dtype=state_dtype, device=home)
         # resident mode: the GPU copy every gather reads (the host shard_params is the master)
@@ -205,11 +219,23 @@ class FullyShard:
         self._h2d_stream = torch.cuda.Stream(device=self.device) if (self.resident and self.device.type == "cuda") else None
         self._d2h_stream = torch.cuda.Stream(device=self.device) if (cpu_offload and self.device.type == "cuda") else None
         self._d2h_events = []
+        # offload traffic / host-update accounting (offload_stats): timed copies and updates
+        self._xfer = {"d2h": [], "h2d": []}  # (start event, end event, bytes)
+        self._host_upd = [0.0, 0]  # seconds in host AdamW, parameters updated
+        self._stat_steps = 0
         o = 0
         for u in all_units:
             u.shard_off = o
             o += u.shard_numel
         self.all_units = all_units
+        self._ring, self._ring_busy, self._ring_next = [], [], 0
+        if self.grad_ring:
+            from ..utils.pinned import pinned_zeros
+
+            slot = max(u.shard_numel for u in all_units)
+            self._ring = [pinned_zeros(slot, self.dtype) if pin else torch.zeros(slot, dtype=self.dtype)
+                          for _ in range(self.grad_ring)]
+            self._ring_busy = [None] * self.grad_ring
         # ---- materialise params: full buffers per unit, shard extraction, param rebinding
         where = {}
         for mn, mm in model.named_modules():
@@ -454,8 +480,10 @@ class FullyShard:
             ar = dist.all_reduce(out, group=self.replicate_group, async_op=True)
             ar.wait()
         ev = None
+        gsrc = None
         if not direct:
-            gs = self._shard_view(u, self.shard_grads)
+            gs = self._ring_slot(u) if self.grad_ring else self._shard_view(u, self.shard_grads)
+            gsrc = gs
             if (first or merged) and self._d2h_stream is not None and gs.device.type == "cpu":
                 # offload: the gradient shard goes to pinned host memory on a side stream, so the
                 # host thread keeps queueing backward kernels; the host update (or step()) waits
@@ -463,9 +491,12 @@ class FullyShard:
                 cur = torch.cuda.current_stream(self.device)
                 self._d2h_stream.wait_stream(cur)
                 with torch.cuda.stream(self._d2h_stream):
+                    t0 = torch.cuda.Event(enable_timing=True)
+                    t0.record(self._d2h_stream)
                     gs.copy_(out, non_blocking=True)
-                    ev = torch.cuda.Event()
+                    ev = torch.cuda.Event(enable_timing=True)
                     ev.record(self._d2h_stream)
+                self._xfer_add("d2h", t0, ev, out.numel() * out.element_size())
                 out.record_stream(self._d2h_stream)
                 self._d2h_events.append(ev)
             elif first or merged:
@@ -474,7 +505,7 @@ class FullyShard:
                 self._sync_d2h()  # the previous micro-batch's copy into gs must have landed
                 gs.add_(out.to(gs.device))
         if self._bwd_step is not None:
-            self._submit_host_step(u, ev)
+            self._submit_host_step(u, ev, gsrc)
         u.full_grad = None
         for p in u.params:
             p.main_grad = None
@@ -508,7 +539,18 @@ class FullyShard:
         for ev in evs:
             ev.synchronize()
 
-    def _submit_host_step(self, u, ev=None):
+    def _ring_slot(self, u):
+        """Next gradient staging slot (grad_ring), once the host update that last read it is done."""
+        k = self._ring_next
+        self._ring_next = (k + 1) % len(self._ring)
+        fut = self._ring_busy[k]
+        if fut is not None:
+            fut.result()  # normally long finished: the host update keeps pace with the backward
+            self._ring_busy[k] = None
+        self._ring_k = k
+        return self._ring[k][:u.shard_numel]
+
+    def _submit_host_step(self, u, ev=None, grad=None):
         import concurrent.futures as cf
 
         from ..ops.adamw import adamw_step_cpu
@@ -517,16 +559,23 @@ class FullyShard:
             self._cpu_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="dtg-host-adamw")
         step, scale, (lr, b1, b2, eps, wd) = self._bwd_step
         sl = slice(u.shard_off, u.shard_off + u.shard_numel)
+        g = grad if (grad is not None and self.grad_ring) else self.shard_grads[sl]
 
         def update():
             if ev is not None:  # this unit's gradient shard has landed in host memory
                 ev.synchronize()
-            adamw_step_cpu(self.shard_params[sl], self.shard_grads[sl], self.exp_avg[sl], self.exp_avg_sq[sl],
+            t0 = time.perf_counter()
+            adamw_step_cpu(self.shard_params[sl], g, self.exp_avg[sl], self.exp_avg_sq[sl],
                            lr=lr, step=step, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, grad_scale=scale)
+            self._host_upd[0] += time.perf_counter() - t0
+            self._host_upd[1] += u.shard_numel
             if self.resident:
                 self._copy_back(u, sl)
 
-        self._cpu_futs.append(self._cpu_pool.submit(update))
+        fut = self._cpu_pool.submit(update)
+        self._cpu_futs.append(fut)
+        if self.grad_ring and grad is not None:
+            self._ring_busy[self._ring_k] = fut
 
     def _copy_back(self, u, sl):
         """Resident mode: updated host shard -> its HBM copy on the H2D side stream; the next
@@ -535,9 +584,12 @@ class FullyShard:
             self.gpu_params[sl].copy_(self.shard_params[sl])
             return
         with torch.cuda.device(self.device), torch.cuda.stream(self._h2d_stream):
+            t0 = torch.cuda.Event(enable_timing=True)
+            t0.record(self._h2d_stream)
             self.gpu_params[sl].copy_(self.shard_params[sl], non_blocking=True)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=True)
             ev.record(self._h2d_stream)
+        self._xfer_add("h2d", t0, ev, (sl.stop - sl.start) * self.gpu_params.element_size())
         u.h2d_event = ev
 
     def backward(self, loss, last_microbatch: Optional[bool] = None):
@@ -556,6 +608,10 @@ class FullyShard:
         final = (not self._in_no_sync) if last_microbatch is None else bool(last_microbatch)
         self._final_micro = final  # HYBRID: the replica all-reduce runs on the final micro-batch only
         overlap = (self.cpu_offload and self.overlap_cpu_step and self._hparams is not None and final)
+        if self.grad_ring and not (overlap and self.accum_count == 0):
+            raise RuntimeError("FullyShard(grad_ring=...): the host gradient ring has no whole-model gradient "
+                               "shard to accumulate into; it needs the overlapped host step (overlap_cpu_step, a "
+                               "bound FlatAdamW) on the only micro-batch of each step (no gradient accumulation)")
         if overlap:  # the last micro-batch: its per-unit gradient shards are final on arrival
             scale = 1.0 / (self.world * self.replicas * (self.accum_count + 1))
             self._bwd_step = (self.step_count + 1, scale, self._hparams())
@@ -599,6 +655,8 @@ class FullyShard:
     def step(self, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, grad_scale=None):
         if self._poisoned:
             raise RuntimeError("FullyShard.step: a failed backward left units partially updated")
+        if self.grad_ring and not self._bwd_stepped:
+            raise RuntimeError("FullyShard.step: grad_ring engines update during backward only")
         if self._bwd_stepped:  # overlap_cpu_step: every unit was updated during backward
             step, scale, hp = self._bwd_snapshot
             if grad_scale is not None or tuple(hp) != (lr, beta1, beta2, eps, weight_decay):
@@ -618,14 +676,51 @@ class FullyShard:
         if self.cpu_offload:
             from ..ops.adamw import adamw_step_cpu
 
+            t0 = time.perf_counter()
             adamw_step_cpu(self.shard_params, self.shard_grads, self.exp_avg, self.exp_avg_sq, lr=lr,
                            step=self.step_count, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
                            grad_scale=grad_scale)
+            self._host_upd[0] += time.perf_counter() - t0
+            self._host_upd[1] += self.shard_params.numel()
             if self.resident:
                 self.sync_params_after_load()
         else:
             adamw_step(self.shard_params, self.shard_grads, self.exp_avg, self.exp_avg_sq, lr=lr, step=self.step_count,
                        beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale)
+
+    def _xfer_add(self, kind, t0, t1, nbytes):
+        xs = self._xfer[kind]
+        xs.append((t0, t1, nbytes))
+        if len(xs) > 4096:  # fold resolved copies into a running (ms, bytes) entry: bounded lists
+            xs[-1][1].synchronize()
+            ms = sum(a.elapsed_time(b) if a is not None else b for a, b, _ in xs)
+            self._xfer[kind] = [(None, ms, sum(b for _, _, b in xs))]
+
+    def offload_stats(self, reset: bool = True) -> dict:
+        """CPU offload accounting since the last reset, per optimizer step: host AdamW seconds and
+        GB/s (14 B per parameter: p, m, v read + written in bf16, g read), gradient D2H and
+        parameter H2D GB and GB/s (sum of each copy's own HIP-event time on its side stream).
+        Synchronises the copies it reads (call at log time)."""
+        steps = max(1, self.step_count - self._stat_steps)
+        out = {}
+        secs, n = self._host_upd
+        if n:
+            out["host_adamw_s"] = secs / steps
+            out["host_adamw_gbs"] = 14 * n / secs / 1e9 if secs > 0 else 0.0
+        for k in ("d2h", "h2d"):
+            xs = self._xfer[k]
+            if xs:
+                if xs[-1][0] is not None:
+                    xs[-1][1].synchronize()
+                ms = sum(a.elapsed_time(b) if a is not None else b for a, b, _ in xs)
+                nbytes = sum(b for _, _, b in xs)
+                out[f"{k}_gb"] = nbytes / steps / 1e9
+                out[f"{k}_gbs"] = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        if reset:
+            self._xfer = {"d2h": [], "h2d": []}
+            self._host_upd = [0.0, 0]
+            self._stat_steps = self.step_count
+        return out
 
     def sync_params_after_load(self):
         """Resident offload: the host master shard changed (checkpoint / pretrained load, a

@@ -44,6 +44,11 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                        help="with --cpu-offload on: on = parameters on the host too (reference); off = parameter "
                             "shard resident in HBM, only gradients + AdamW state offloaded; auto = off when the "
                             "shard fits a third of HBM")
+        p.add_argument("--offload-grad-ring", default="auto",
+                       help="with --cpu-offload on: stage each unit's reduced gradient in one of N unit-sized "
+                            "pinned host slots consumed by the overlapped host AdamW, instead of a host gradient "
+                            "shard for the whole model (saves 2 B/param of host RAM: 101 GB per rank for 405B at "
+                            "W = 8); auto = 4 slots without gradient accumulation, else off; 0 = off")
     if chapter == "07":
         p.add_argument("--tp", default=8, type=int)
     if chapter in ("06", "07"):
@@ -112,6 +117,9 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     g.add_argument("--pin-numa", default="off", choices=["on", "off"],
                    help="restrict each rank's CPU affinity to its GPU's NUMA node (host AdamW / D2H locality); "
                         "the placement is logged at startup either way")
+    g.add_argument("--cpu-share", default=0, type=int,
+                   help="restrict this rank to N CPUs (after --pin-numa; the host AdamW's OpenMP team follows "
+                        "OMP_NUM_THREADS): rehearse one rank's share of a node's cores on a bigger host; 0 = all")
     g.add_argument("--num-layers", default=None, type=int,
                    help="override the model's num_hidden_layers (exact-width, reduced-depth runs)")
     g.add_argument("--init-from", default=None, help="HF safetensors directory to load pretrained weights from")

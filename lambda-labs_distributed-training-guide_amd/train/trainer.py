@@ -196,11 +196,17 @@ def _build(args, chapter, device, world):
         if cpu_offload:
             LOGGER.info("cpu offload: " + ("parameters, gradients and AdamW state on the host" if offload_params else
                                            "gradients and AdamW state on the host, parameter shard resident in HBM"))
+        ring = str(getattr(args, "offload_grad_ring", "0"))
+        ring = (4 if max(1, args.grad_accum) == 1 else 0) if ring == "auto" else int(ring)
+        ring = ring if cpu_offload else 0
+        if ring:
+            LOGGER.info(f"cpu offload: host gradient ring of {ring} unit-sized pinned slots (no whole-model "
+                        "host gradient shard)")
         engine = FullyShard(model, group=dp_group, tp_group=tp_group, policy=policy,
                             min_num_params=getattr(args, "numel_to_wrap", 100_000_000), device=device,
                             reshard_after_forward=args.reshard_after_forward == "on",
                             cpu_offload=cpu_offload, offload_params=offload_params, seed=args.seed,
-                            replicate_group=replicate_group)
+                            replicate_group=replicate_group, grad_ring=ring)
         style = "sharded"
     else:
         if world == 1 or (pp > 1 and dp_size == 1):
@@ -250,7 +256,7 @@ def run(chapter: str, argv=None):
     LOGGER.info(args)
     LOGGER.info(f"local_rank={local_rank} rank={rank} world size={world}")
     # host CPU share and NUMA placement of this rank (chapter 05's offload is host-bound)
-    LOGGER.info(f"host placement: {udist.host_placement(device, pin=getattr(args, 'pin_numa', 'off') == 'on')}")
+    LOGGER.info(f"host placement: {udist.host_placement(device, pin=getattr(args, 'pin_numa', 'off') == 'on', share=getattr(args, 'cpu_share', 0))}")
     if args.tunableop != "off" and device.type == "cuda":
         from ..utils.gemm_tuning import enable_tunableop
 
@@ -445,6 +451,8 @@ def run(chapter: str, argv=None):
                     "time/total": ms_per_step,
                     **{f"time/{k}": t.avg_elapsed_ms() for k, t in timers.items()},
                 }
+                if getattr(engine, "cpu_offload", False):
+                    info.update(_offload_info(engine))
                 LOGGER.info(info)
                 sink.log(info, state["global_step"])
                 if device.type == "cuda":
@@ -472,6 +480,24 @@ def run(chapter: str, argv=None):
     mgr.finalize()
     ucomm.check_xgmi()
     return state
+
+
+def _offload_info(engine) -> dict:
+    """CPU-offload record of the log window: host AdamW time and bandwidth, gradient D2H and
+    parameter H2D volume and bandwidth per step (FullyShard.offload_stats), and this process's
+    host memory: resident set, pinned shard buffers, and the host's MemAvailable."""
+    out = {f"offload/{k}": v for k, v in engine.offload_stats().items()}
+    bufs = [engine.shard_params, engine.shard_grads] + list(getattr(engine, "_ring", []))
+    pinned = sum(t.numel() * t.element_size() for t in bufs if t.numel() and t.is_pinned())
+    out["host/pinned_gb"] = pinned / 1e9
+    try:
+        import psutil
+
+        out["host/rss_gb"] = psutil.Process().memory_info().rss / 1e9
+        out["host/mem_available_gb"] = psutil.virtual_memory().available / 1e9
+    except Exception:
+        pass
+    return out
 
 
 def _report_nonfinite(model, engine, loss, step, rank, what):

@@ -200,7 +200,7 @@ def _parse_cpulist(text: str):
     return cpus
 
 
-def host_placement(device, pin: bool = False) -> dict:
+def host_placement(device, pin: bool = False, share: int = 0) -> dict:
     """Where this rank's host work runs relative to its GPU: the CPUs it may use
     (`os.sched_getaffinity`), the GPU's NUMA node and that node's CPUs (sysfs, from the PCI bus
     id), and OMP_NUM_THREADS.  Chapter 05's backward is bound by gradient D2H and the host AdamW
@@ -242,6 +242,17 @@ def host_placement(device, pin: bool = False) -> dict:
                     break
         except Exception as e:  # informational only: never fail a run over sysfs layout
             info["error"] = repr(e)[:120]
+    if share and share > 0:
+        # one rank's share of a node's cores (threads created from here on inherit it)
+        try:
+            cur = sorted(os.sched_getaffinity(0))
+            keep = set(cur[:share])
+            os.sched_setaffinity(0, keep)
+            torch.set_num_threads(len(keep))
+            info["cpu_share"] = len(keep)
+            info["affinity_cpus"] = len(keep)
+        except (AttributeError, OSError) as e:
+            info["cpu_share_error"] = repr(e)[:120]
     return info
 
 

@@ -109,3 +109,43 @@ def test_export_rejects_incomplete_checkpoint(tmp_path):
     (tmp_path / "index.json").write_text(json.dumps(meta))
     with pytest.raises(RuntimeError, match="covered"):
         dict(iter_full_params(tmp_path))
+
+
+def test_dcp_export_readable_by_torch_format_utils_and_imports_back():
+    """a 2-D (FSDP W=2 x TP=2) checkpoint exported as a torch DCP directory is
+    read by torch's own `dcp_to_torch_save` into the reference's {"model", "optimizer"} layout
+    with HF names (same values as the trained model, moments included), and imports back onto a
+    TP=2 layout bit-exactly."""
+    import ckpt_export
+    from torch.distributed.checkpoint.format_utils import dcp_to_torch_save
+
+    from dtg.models import resolve_config
+    from dtg.models.hf_compat import llama_to_hf
+    from dtg.parallel.tensor_parallel import unshard_state_dicts
+
+    cfg = resolve_config(MODEL)
+    batches = _batches(cfg.vocab_size, 4, 32, n=2)
+    with tempfile.TemporaryDirectory() as d:
+        res = run_distributed(_save_2d, 4, batches, d)
+        by_tp = {tp: sd for sd, tp in res}
+        trained = unshard_state_dicts([by_tp[0], by_tp[1]], cfg)
+        out = os.path.join(d, "dcp")
+        s = ckpt_export.export_dcp(os.path.join(d, "checkpoint"), out, MODEL, with_optimizer=True)
+        assert s["format"] == "dcp" and os.path.exists(os.path.join(out, ".metadata"))
+        assert not os.path.exists(os.path.join(out, ".dcp_scratch"))
+        dcp_to_torch_save(out, os.path.join(d, "full.pt"))
+        sd = torch.load(os.path.join(d, "full.pt"), weights_only=True)
+        want = llama_to_hf(trained, cfg)
+        assert set(sd["model"]) == {k for k in want if not (k == "lm_head.weight" and cfg.tie_word_embeddings)}
+        for k, v in sd["model"].items():
+            assert torch.equal(v, want[k]), k
+        st = sd["optimizer"]["state"]
+        assert set(st) == set(sd["model"]) and all(float(x["step"]) == 2 for x in st.values())
+        assert all(x["exp_avg"].shape == sd["model"][k].shape for k, x in st.items())
+        # DCP -> one-shard checkpoint -> TP=2 resume, bit-exact parameters
+        ck2 = os.path.join(d, "imported")
+        ckpt_export.import_dcp(out, ck2, MODEL)
+        res2 = run_distributed(_load_tp2, 2, ck2)
+        back = unshard_state_dicts([r[0] for r in sorted(res2, key=lambda r: r[1])], cfg)
+        for n, v in trained.items():
+            assert torch.equal(back[n], v), n

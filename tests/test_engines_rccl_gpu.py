@@ -130,7 +130,7 @@ def test_rccl_world1_grad_accumulation(cuda, kind):
         assert torch.equal(params[n], v), (kind, n)
 
 
-def _offload_worker(rank, world, overlap, accum, offload_params=True):
+def _offload_worker(rank, world, overlap, accum, offload_params=True, ring=0):
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import FlatAdamW
     from dtg.parallel.fsdp import FullyShard
@@ -140,7 +140,8 @@ def _offload_worker(rank, world, overlap, accum, offload_params=True):
     cfg = resolve_config(MODEL)
     torch.manual_seed(0)
     model = build_model(cfg, device=dev)
-    eng = FullyShard(model, device=dev, cpu_offload=True, overlap_cpu_step=overlap, offload_params=offload_params)
+    eng = FullyShard(model, device=dev, cpu_offload=True, overlap_cpu_step=overlap, offload_params=offload_params,
+                     grad_ring=ring)
     opt = FlatAdamW(eng, lr=1e-3)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))  # lr changes every step
     stepped = []
@@ -196,3 +197,17 @@ def test_rccl_world1_zero_weight_t_with_delayed_gathers(cuda):
         assert torch.equal(params[n], v), n
     (used, _, _), = run_distributed(_worker, 1, "zero", True, 1, 1024, True, backend="nccl")
     assert used and all(used), f"{used.count(False)} of {len(used)} dX GEMMs transposed W in the backward"
+
+
+@pytest.mark.parametrize("offload_params,ring", [(False, 4), (False, 1), (True, 2)])
+def test_fsdp_offload_grad_ring_bit_identical_on_gpu(cuda, offload_params, ring):
+    """Host gradient ring on the GPU: each unit's reduced gradient is copied D2H on the side
+    stream into a reused pinned slot while the host AdamW of earlier units reads other slots
+    (one slot: every D2H waits for the previous unit's host update) == the whole-model host
+    gradient shard, bit for bit."""
+    full = run_distributed(_offload_worker, 2, True, 1, offload_params, 0)
+    got = run_distributed(_offload_worker, 2, True, 1, offload_params, ring)
+    for r in range(2):
+        assert all(got[r][1])
+        for n, t in full[r][0].items():
+            assert torch.equal(got[r][0][n], t), (r, n)

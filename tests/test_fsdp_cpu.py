@@ -156,7 +156,7 @@ def test_hybrid_shard_accumulation_one_replica_allreduce_per_step(offload):
             torch.testing.assert_close(sd[n], ref[n], **TOL, msg=f"rank {r} {n}")
 
 
-def _offload_train(rank, world, batches, overlap, accum, offload=True, offload_params=True):
+def _offload_train(rank, world, batches, overlap, accum, offload=True, offload_params=True, ring=0):
     from dtg.models import build_model
     from dtg.parallel.data_parallel import FlatAdamW
     from dtg.parallel.fsdp import FullyShard
@@ -164,7 +164,7 @@ def _offload_train(rank, world, batches, overlap, accum, offload=True, offload_p
     torch.manual_seed(0)
     model = build_model("llama-tiny", device="cpu", dtype=torch.float32)
     eng = FullyShard(model, cpu_offload=offload, device="cpu", overlap_cpu_step=overlap,
-                     offload_params=offload_params)
+                     offload_params=offload_params, grad_ring=ring)
     opt = FlatAdamW(eng, lr=1e-2, eps=1e-3)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))  # lr changes every step
     stepped_in_bwd = []
@@ -252,3 +252,53 @@ def test_fsdp_overlapped_host_step_guards_misuse():
     assert eng._bwd_stepped and not torch.equal(before, eng.shard_params)
     opt.step()
     assert eng.step_count == 2
+
+
+def test_offload_stats_account_host_update():
+    """CPU offload accounting the 405B runs report: host AdamW seconds and GB/s per step over the
+    log window (14 B per parameter), reset on read.  (D2H / H2D rows need a GPU.)"""
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+
+    m = build_model("llama-tiny", device="cpu", dtype=torch.float32)
+    eng = FullyShard(m, device="cpu", cpu_offload=True)
+    opt = FlatAdamW(eng, lr=1e-3)
+    ids = _batches(512, 2, 16)[0]
+    for _ in range(2):
+        opt.zero_grad()
+        eng.backward(m(input_ids=ids, labels=ids).loss)
+        opt.step()
+    st = eng.offload_stats()
+    assert st["host_adamw_s"] > 0 and st["host_adamw_gbs"] > 0
+    assert "d2h_gb" not in st  # no device copies on a CPU engine
+    assert eng.offload_stats() == {}  # reset after the read
+
+
+@pytest.mark.parametrize("offload_params,ring", [(True, 2), (False, 1), (False, 3)])
+def test_fsdp_offload_grad_ring_bit_identical(offload_params, ring):
+    """The host gradient ring (no whole-model host gradient shard; each unit's gradient staged
+    in one of `ring` slots the host AdamW consumes) == the full host gradient shard, bit for
+    bit; one slot forces every unit to wait for the previous unit's host update."""
+    batches = _batches(512, 4, 32, n=3)
+    full = run_distributed(_offload_train, 2, batches, True, 1, True, offload_params, 0)
+    got = run_distributed(_offload_train, 2, batches, True, 1, True, offload_params, ring)
+    for r in range(2):
+        assert all(got[r][1])
+        for n, t in full[r][0].items():
+            assert torch.equal(got[r][0][n], t), f"rank {r} {n}"
+
+
+def test_fsdp_offload_grad_ring_refuses_accumulation():
+    from dtg.models import build_model
+    from dtg.parallel.data_parallel import FlatAdamW
+    from dtg.parallel.fsdp import FullyShard
+
+    model = build_model("llama-tiny", device="cpu", dtype=torch.float32)
+    eng = FullyShard(model, cpu_offload=True, device="cpu", grad_ring=2)
+    assert eng.shard_grads.numel() == 0 and len(eng._ring) == 2
+    FlatAdamW(eng, lr=1e-3)
+    ids = _batches(512, 2, 16)[0]
+    with pytest.raises(RuntimeError, match="gradient ring"):
+        with eng.no_sync():
+            eng.backward(model(input_ids=ids, labels=ids).loss)
