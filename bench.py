@@ -50,6 +50,9 @@ def parse(argv=None):
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--parallel", default="zero", choices=["ddp", "zero", "fsdp"])
     ap.add_argument("--bucket-mb", type=int, default=256)
+    # ZeRO's bucket collectives: RCCL (default) or copy-engine pulls between the ranks' shared flat
+    # buffers over xGMI (parallel/xgmi_dp.py); the N > 1 sweep times the other one too
+    ap.add_argument("--dp-comm", default="rccl", choices=["rccl", "xgmi-dma"])
     # BASELINE config 06 (Llama-3-8B TP=8 over xGMI): --tp 8 --gpus 8.  Tensor + sequence parallel
     # inside groups of --tp ranks, data parallel (--parallel) across them; a step is dp x B x S
     # tokens (the reference's TP tok/s formula, 06-tensor-parallel/train_llm.py:256).
@@ -83,6 +86,8 @@ def parse(argv=None):
     # N > 1 only, after the timed region: ZeRO/DDP step time rebuilt at each bucket size (MiB)
     ap.add_argument("--bucket-sweep-mb", default="64,128,256,512")
     ap.add_argument("--sweep-steps", type=int, default=3)
+    ap.add_argument("--sweep-other-dp-comm", type=int, default=1,
+                    help="1: the bucket sweep also times ZeRO on the other --dp-comm transport")
     # reference-mode throughput: this many extra steps under the reference's synchronising
     # LocalTimer phases (outside the timed region); 0 = off
     ap.add_argument("--ref-steps", type=int, default=3)
@@ -134,7 +139,7 @@ def loss_in_band(loss: float, vocab: int) -> bool:
     return math.isfinite(loss) and lnv - 3.5 < loss < lnv + 1.5
 
 
-def build_job(args, torch, device, cuda, bucket_mb=None):
+def build_job(args, torch, device, cuda, bucket_mb=None, dp_comm=None):
     """Model + engine + optimizer + scheduler of the flagship step, as the driver's command
     builds them.  `bucket_mb` overrides --bucket-mb (the N > 1 bucket-size sweep)."""
     from dtg.models import build_model, resolve_config
@@ -167,7 +172,8 @@ def build_job(args, torch, device, cuda, bucket_mb=None):
     else:
         engine = DataParallel(model, mode=args.parallel if dp_size > 1 else "single", group=dp_group, tp_group=tp_group,
                               bucket_mb=bucket_mb or args.bucket_mb, broadcast_from_rank0=tp_group is None,
-                              overlap_optimizer=bool(args.overlap_optimizer))
+                              overlap_optimizer=bool(args.overlap_optimizer),
+                              dp_comm=(dp_comm or args.dp_comm) if cuda else "rccl")
     opt = FlatAdamW(engine, lr=args.lr)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=1000, eta_min=args.lr * 1e-2)
     return dict(cfg=cfg, model=model, engine=engine, opt=opt, sched=sched, dp_size=dp_size, dp_rank=dp_rank,
@@ -185,6 +191,10 @@ def close_job(job, torch):
 
         _comm.unregister_xgmi(job["tp_group"])
         job["xgmi"].close()
+    xdp = getattr(eng, "xdp", None)
+    if xdp is not None:
+        torch.cuda.synchronize()
+        xdp.check()
     job.clear()
 
 
@@ -281,6 +291,7 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
                          f"ln({cfg.vocab_size}) = {math.log(cfg.vocab_size):.2f}; refusing to report a throughput")
     res = dict(elapsed=elapsed, peak_gb=peak_gb, loss=loss_val, cfg=cfg, ref_ms=ref_ms,
                mode=getattr(engine, "mode", args.parallel), dp=dp_size, tp_comm=job["tp_comm"],
+               dp_comm=getattr(engine, "dp_comm", "rccl"),
                replica_sum=replica_checksum(engine, torch))
     del model, engine, opt, sched, batches, loss
     close_job(job, torch)
@@ -306,8 +317,16 @@ def bucket_sweep(args, torch, dist, device, world, rank, cuda):
     sizes = [int(x) for x in args.bucket_sweep_mb.split(",") if x.strip()]
     out = []
     B, S = args.batch_size, args.seq_len
-    for mb in sizes:
-        job = build_job(args, torch, device, cuda, bucket_mb=mb)
+    runs = [(mb, args.dp_comm) for mb in sizes]
+    other = "xgmi-dma" if args.dp_comm == "rccl" else "rccl"
+    if cuda and args.parallel == "zero" and args.sweep_other_dp_comm:
+        runs.append((args.bucket_mb, other))  # the other ZeRO transport at the default bucket size
+    for mb, dpc in runs:
+        try:
+            job = build_job(args, torch, device, cuda, bucket_mb=mb, dp_comm=dpc)
+        except Exception as e:  # a diagnostic row: never lose the run's JSON line over it
+            out.append({"bucket_mb": mb, "dp_comm": dpc, "error": repr(e)[:300]})
+            continue
         model, engine, opt = job["model"], job["engine"], job["opt"]
         ids_all = _batches(torch, job["cfg"], B, S, 1 + args.sweep_steps, device, 777 + job["dp_rank"])
 
@@ -327,7 +346,8 @@ def bucket_sweep(args, torch, dist, device, world, rank, cuda):
                           device=device)
         if world > 1:
             dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-        out.append({"bucket_mb": mb, "buckets": len(engine.space.buckets) if hasattr(engine, "space") else None,
+        out.append({"bucket_mb": mb, "dp_comm": getattr(engine, "dp_comm", "rccl"),
+                    "buckets": len(engine.space.buckets) if hasattr(engine, "space") else None,
                     "ms_per_step": round(float(ms.item()), 2)})
         del model, engine, opt, ids_all, step
         close_job(job, torch)
@@ -626,7 +646,8 @@ def main(argv=None):
             "dtype": "bf16",
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": cfg.hf_name or args.model, "global_batch": dp * B, "seq_len": S,
-                       "parallelism": f"dp{dp}-{res['mode']}" + (f"-tp{args.tp}-{tp_comm_label}" if args.tp > 1 else "")},
+                       "parallelism": f"dp{dp}-{res['mode']}" + ("-xgmi-dma" if res["dp_comm"] == "xgmi-dma" else "")
+                                      + (f"-tp{args.tp}-{tp_comm_label}" if args.tp > 1 else "")},
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
             "peak_mem_gb": round(max(r[2] for r in rows), 2),

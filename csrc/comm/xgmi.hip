@@ -176,6 +176,10 @@ struct Comm {
   std::vector<void*> opened;
   uint32_t epoch = 0;
   double timeout_s = 60.0;
+  // shared buffers (alloc_shared): every rank's copy of a buffer with the same layout, mapped
+  // from every peer; shared[slot][r] = rank r's base (own or IPC-mapped)
+  std::vector<std::vector<uint8_t*>> shared;
+  std::vector<void*> shared_opened;
   // copy-engine path: one stream per peer, fork/join events
   hipStream_t peer_st[kMaxRanks] = {};
   hipEvent_t ev_fork = nullptr;
@@ -200,6 +204,7 @@ struct Comm {
       (void)hipEventDestroy(ev_fork);
     }
     for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+    for (void* p : shared_opened) (void)hipIpcCloseMemHandle(p);
     if (base) (void)hipFree(base);
     if (err) (void)hipHostFree(err);
   }
@@ -516,7 +521,149 @@ void all_reduce(int64_t id, const at::Tensor& inout, int64_t offset) {
   barrier(c, 1, st);
 }
 
+// ------------------------------------------------------------------------------------------
+// Shared buffers: data-parallel bucket collectives without staging (parallel/xgmi_dp.py)
+// ------------------------------------------------------------------------------------------
+// A buffer every rank allocates with the same size and layout (ZeRO's flat parameter and
+// gradient buffers), IPC-exported and mapped from every peer.  Collectives on it are copy-engine
+// pulls at arbitrary byte ranges of the peers' copies: a reduce-scatter pulls this rank's slice
+// of a bucket from every peer into a local scratch and sums it; an all-gather pulls every peer's
+// updated slice straight into place.  Only the one-wave barrier kernel and the local reduce
+// touch the shader array.  Memory is ordinary (cached) device memory: a producer kernel's
+// results are written back at its end, before the barrier kernel that follows it on the stream
+// signals the peers.
+
+// Own allocation; the tensor's deleter frees it (peers keep their mapping until they close it).
+at::Tensor alloc_shared(int64_t id, int64_t nbytes) {
+  Comm& c = get(id);
+  TORCH_CHECK(nbytes > 0, "xgmi: alloc_shared needs a positive size");
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c.device));
+  void* p = nullptr;
+  XGMI_CHECK(hipMalloc(&p, (size_t)nbytes));
+  XGMI_CHECK(hipMemset(p, 0, (size_t)nbytes));
+  XGMI_CHECK(hipDeviceSynchronize());
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    c.shared.push_back(std::vector<uint8_t*>(c.world, nullptr));
+    c.shared.back()[c.rank] = static_cast<uint8_t*>(p);
+  }
+  const int dev = c.device;
+  return at::from_blob(p, {nbytes}, [dev](void* q) {
+           c10::DeviceGuard gg(c10::Device(c10::DeviceType::CUDA, dev));
+           (void)hipFree(q);
+         },
+         at::TensorOptions().dtype(at::kByte).device(c10::Device(c10::DeviceType::CUDA, c.device)));
+}
+
+at::Tensor shared_handle(int64_t id, int64_t slot) {
+  Comm& c = get(id);
+  TORCH_CHECK(slot >= 0 && slot < (int64_t)c.shared.size(), "xgmi: bad shared slot");
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c.device));
+  hipIpcMemHandle_t h;
+  XGMI_CHECK(hipIpcGetMemHandle(&h, c.shared[slot][c.rank]));
+  auto t = at::empty({(int64_t)sizeof(h)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), &h, sizeof(h));
+  return t;
+}
+
+void open_shared(int64_t id, int64_t slot, const at::Tensor& handles) {
+  Comm& c = get(id);
+  TORCH_CHECK(slot >= 0 && slot < (int64_t)c.shared.size(), "xgmi: bad shared slot");
+  TORCH_CHECK(handles.device().is_cpu() && handles.scalar_type() == at::kByte && handles.dim() == 2 &&
+                  handles.size(0) == c.world && handles.size(1) == (int64_t)sizeof(hipIpcMemHandle_t),
+              "xgmi: handles must be a CPU uint8 tensor [world, ", sizeof(hipIpcMemHandle_t), "]");
+  auto hc = handles.contiguous();
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c.device));
+  for (int r = 0; r < c.world; ++r) {
+    if (r == c.rank) continue;
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, hc.data_ptr<uint8_t>() + r * sizeof(h), sizeof(h));
+    void* q = nullptr;
+    XGMI_CHECK(hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess));
+    c.shared_opened.push_back(q);
+    c.shared[slot][r] = static_cast<uint8_t*>(q);
+  }
+}
+
+// Everyone's work queued before this point on their stream has finished (signal + wait, bounded).
+void signal_wait(int64_t id) {
+  Comm& c = get(id);
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c.device));
+  ++c.epoch;
+  barrier(c, 0, cur_stream());
+}
+
+// dst[dst_off[p] : + nbytes[p]] = peer p's shared slot [src_off[p] : + nbytes[p]] for every peer
+// p != this rank, one hipMemcpyAsync per peer on that peer's stream (the copy engines, all
+// links at once), forked from and joined back into the caller's stream.  Offsets / sizes: CPU
+// int64 [world].
+void pull(int64_t id, int64_t slot, const at::Tensor& dst, const at::Tensor& src_off, const at::Tensor& nbytes,
+          const at::Tensor& dst_off) {
+  Comm& c = get(id);
+  TORCH_CHECK(slot >= 0 && slot < (int64_t)c.shared.size(), "xgmi: bad shared slot");
+  TORCH_CHECK(dst.is_cuda() && dst.get_device() == c.device && dst.is_contiguous(), "xgmi pull: dst");
+  for (const at::Tensor* t : {&src_off, &nbytes, &dst_off})
+    TORCH_CHECK(t->device().is_cpu() && t->scalar_type() == at::kLong && t->numel() == c.world,
+                "xgmi pull: offsets / sizes must be CPU int64 [world]");
+  const int64_t* so = src_off.data_ptr<int64_t>();
+  const int64_t* nb = nbytes.data_ptr<int64_t>();
+  const int64_t* dof = dst_off.data_ptr<int64_t>();
+  const int64_t cap = dst.numel() * dst.element_size();
+  for (int p = 0; p < c.world; ++p)
+    TORCH_CHECK(nb[p] >= 0 && dof[p] >= 0 && so[p] >= 0 && dof[p] + nb[p] <= cap, "xgmi pull: range of peer ", p);
+  c10::DeviceGuard g(dst.device());
+  hipStream_t st = cur_stream();
+  fork(c, st);
+  auto* d = static_cast<uint8_t*>(dst.data_ptr());
+  for (int k = 1; k < c.world; ++k) {
+    const int p = (c.rank + k) % c.world;
+    TORCH_CHECK(c.shared[slot][p] != nullptr, "xgmi pull: peer ", p, " of slot ", slot, " not opened");
+    if (nb[p] == 0) continue;
+    XGMI_CHECK(hipMemcpyAsync(d + dof[p], c.shared[slot][p] + so[p], (size_t)nb[p], hipMemcpyDeviceToDevice,
+                              c.peer_st[p]));
+  }
+  join(c, st);
+}
+
+// out = own + sum over peers p != rank of scratch[p] (bf16, f32 accumulation in rank order 0 ..
+// world-1, so every rank's result does not depend on which rank computes it).  scratch is
+// [world, n] (the own row unused), own and out are [n].
+__global__ void reduce_rows_kernel(const u32x4* __restrict__ scratch, const u32x4* __restrict__ own,
+                                   u32x4* __restrict__ out, int me, int world, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) {
+      const u32x4 v = r == me ? own[i] : __builtin_nontemporal_load(scratch + (int64_t)r * n16 + i);
+      acc8_bf16(a, v);
+    }
+    out[i] = pack8_bf16(a);
+  }
+}
+
+void reduce_pulled(int64_t id, const at::Tensor& out, const at::Tensor& scratch, const at::Tensor& own) {
+  Comm& c = get(id);
+  for (const at::Tensor* t : {&out, &scratch, &own})
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == at::kBFloat16 &&
+                    reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "xgmi reduce_pulled: bf16, contiguous, 16-byte aligned");
+  const int64_t n = out.numel();
+  TORCH_CHECK(own.numel() == n && scratch.numel() == n * c.world && n % 8 == 0, "xgmi reduce_pulled: shapes");
+  if (n == 0) return;
+  c10::DeviceGuard g(out.device());
+  const int64_t n16 = n / 8;
+  reduce_rows_kernel<<<grid_for(n16), 256, 0, cur_stream()>>>(
+      reinterpret_cast<const u32x4*>(scratch.data_ptr()), reinterpret_cast<const u32x4*>(own.data_ptr()),
+      reinterpret_cast<u32x4*>(out.data_ptr()), c.rank, c.world, n16);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
 TORCH_LIBRARY(dtg_xgmi, m) {
+  m.def("alloc_shared(int id, int nbytes) -> Tensor", &alloc_shared);
+  m.def("shared_handle(int id, int slot) -> Tensor", &shared_handle);
+  m.def("open_shared(int id, int slot, Tensor handles) -> ()", &open_shared);
+  m.def("signal_wait(int id) -> ()", &signal_wait);
+  m.def("pull(int id, int slot, Tensor(a!) dst, Tensor src_off, Tensor nbytes, Tensor dst_off) -> ()", &pull);
+  m.def("reduce_pulled(int id, Tensor(a!) out, Tensor scratch, Tensor own) -> ()", &reduce_pulled);
   m.def("create(int capacity, int rank, int world, int device) -> int", &create);
   m.def("ipc_handle(int id) -> Tensor", &ipc_handle);
   m.def("open_peers(int id, Tensor handles) -> ()", &open_peers);

@@ -32,6 +32,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include <cmath>
+
 namespace dtg {
 namespace fa {
 
@@ -130,6 +132,55 @@ __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * 
 // The lane-independent part: acc_row(reg, h) == acc_row0(reg) + 4h, a compile-time constant, so
 // a mask test against a row becomes one compare with a per-lane threshold.
 constexpr int acc_row0(int reg) { return (reg & 3) + 8 * (reg >> 2); }
+
+// Attention-probability dropout (GPT-2's attn_pdrop), regenerated in the backward
+// instead of stored.  The keep decision of (query q, key k) -- sequence-relative indices of
+// sequence s0 = cu[seq], query head hd -- is byte (k & 3) of word (q & 3) of
+//     Philox4x32-10(counter = {k & ~3, s0 + (q & ~3), hd, offset}, key = seed)
+// compared with thr = round(keep * 256): kept iff byte < thr, so the keep probability is exactly
+// thr / 256 and kept probabilities are scaled by 256 / thr (unbiased).  One Philox call covers a
+// 4 x 4 (query, key) block, which matches both accumulator layouts: a forward / dQ lane owns one
+// query and runs of 4 consecutive keys (one word per call), a dK/dV lane one key and runs of 4
+// consecutive queries (one byte of each word).  The CPU reference (dtg.ops._cpu) implements the
+// same function, so the tests check the kernels' masks bit for bit.
+struct DropCfg {
+  uint32_t k0, k1, off;  // seed (low, high word), per-call offset
+  int thr;               // keep iff random byte < thr (0..256)
+  float scale;           // 256 / thr
+};
+
+__device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
+    const uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+  }
+}
+
+// Forward / dQ layout: lane query q, registers 4g + e = keys key0 + 8g + 4h + e.  Zeroes the
+// dropped entries of x (one 32-key half) and returns nothing else; keep*scale is applied by the
+// caller where it folds into a constant.
+__device__ __forceinline__ void drop_row_half(const DropCfg& dc, int s0, int q, int head, int key0, int h,
+                                              f32x16& x) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint32_t c[4] = {(uint32_t)(key0 + 8 * g + 4 * h), (uint32_t)(s0 + (q & ~3)), (uint32_t)head, dc.off};
+    philox4x32_10(c, dc.k0, dc.k1);
+    const int ws = q & 3;
+    const uint32_t wd = ws == 0 ? c[0] : ws == 1 ? c[1] : ws == 2 ? c[2] : c[3];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[4 * g + e] = (int)((wd >> (8 * e)) & 255u) < dc.thr ? x[4 * g + e] : 0.f;
+  }
+}
 
 // Buffer descriptor over `bytes` bytes at p, built from provably wave-uniform values (T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int bytes) {
@@ -245,6 +296,7 @@ struct FwdParams {
   long long* stamps;  // diagnostic path only (flash_attn_fwd_stamped): 6 words per workgroup
   const int *kstart, *klen;  // optional per-sequence key ranges (see KeyRange)
   int window;  // causal sliding window (Mistral): query i sees keys in (i + off - window, i + off]; 0 = none
+  DropCfg drop;  // DROP instantiations only
 };
 
 // In-kernel timeline stamps (CDNA guide §7 'In-kernel stamps'): constant-rate 100 MHz clock,
@@ -264,7 +316,7 @@ constexpr int kFwdBK = 64;   // keys per K/V tile
 
 // WIN: sliding-window instantiation (only launched with P.window > 0); without it every window
 // term folds to a compile-time 0 and the kernel is the plain causal one.
-template <int D, bool CAUSAL, bool WIDE, bool QLDS, bool WIN = false>
+template <int D, bool CAUSAL, bool WIDE, bool QLDS, bool WIN = false, bool DROP = false>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int TILE = kFwdBK * RB;
@@ -393,7 +445,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
           rs += p;
         }
       }
-      l += rs;
+      l += rs;  // the softmax normaliser counts every probability, dropped or not
+      if constexpr (DROP) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) drop_row_half(P.drop, s0, qrow, head, kt0 + 32 * kt, h, s[kt]);
+      }
       bf16x8 pf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) pf[j] = pack8(s[j >> 1], j & 1);
@@ -426,7 +482,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   fa_stamp(P.stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), 2);
 
   const float lt = pair_sum(l);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const float inv = (lt > 0.f ? 1.f / lt : 0.f) * (DROP ? P.drop.scale : 1.f);
   uint16_t* op = P.o + ((int64_t)(s0 + min(qrow, seqlen - 1)) * P.hq + head) * D;
   if constexpr (WIDE) {
     store_rows_wide<ND>(acc, inv, op, qrow < seqlen);
@@ -471,6 +527,7 @@ struct BwdParams {
   // order by bwd_kv_combine_kernel (deterministic).  nsplit <= 1: bf16 dK / dV written directly.
   float *dk_part, *dv_part;
   int nsplit;
+  DropCfg drop;  // DROP instantiations only
 };
 
 constexpr int kDqBQ = 128;  // query rows per workgroup (4 waves x 32)
@@ -504,7 +561,7 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restri
 
 // dQ = scale * sum_keys dS K, query-stationary (the forward's structure).  Also writes
 // delta = rowsum(dO * O) for its rows, which bwd_dkdv_kernel (launched after it) reads.
-template <int D, bool CAUSAL, int OCC, bool WIN = false, bool PRE_DELTA = false>
+template <int D, bool CAUSAL, int OCC, bool WIN = false, bool PRE_DELTA = false, bool DROP = false>
 __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   constexpr int RB = 2 * D;
   constexpr int TILE = kDqBK * RB;
@@ -623,8 +680,15 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) > lim || acc_row0(i) < llim) ? 0.f : s[i];
     }
+    if constexpr (DROP) {  // dS = P o (M dP_dropped / keep - delta); delta = rowsum(dO o O) still holds
+      f32x16 z = dp;
+      drop_row_half(P.drop, s0, qrow, head, key0, h, z);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s[i] *= dp[i] - delta;  // dS^T / scale
+      for (int i = 0; i < 16; ++i) s[i] *= z[i] * P.drop.scale - delta;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] *= dp[i] - delta;  // dS^T / scale
+    }
     dsf[0] = pack8(s, 0);
     dsf[1] = pack8(s, 1);
   };
@@ -706,7 +770,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 // pipeline (S/dP MFMAs of half 1 under the softmax VALU of half 0, dK/dV MFMAs of half 0 under
 // the softmax of half 1): at one wave per SIMD there is no partner wave to fill the matrix pipe
 // while a wave does its VALU, so the overlap has to come from the wave's own instruction stream.
-template <int D, bool CAUSAL, int PF, bool WIN = false, int QB = kKvBQ>
+template <int D, bool CAUSAL, int PF, bool WIN = false, int QB = kKvBQ, bool DROP = false>
 __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
   static_assert(QB == 32 || QB == 64, "query rows per item");
   constexpr int RB = 2 * D;
@@ -793,6 +857,25 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
       rowc[buf * 2 * QB + threadIdx.x] = (threadIdx.x & QB) ? -dl : -l * inv_scale;
     }
   };
+  // Dropout in the key-stationary layout (DROP): s holds P, dp holds dO.V^T (started from 0, not
+  // -delta), cnd the rows' -delta; afterwards s = the dropped, rescaled probabilities (dV's
+  // operand) and dp = dS / scale.
+  auto drop_cols = [&](int qsu, int hqi, f32x16& s, f32x16& dp, const float* cnd) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint32_t c[4] = {(uint32_t)(key & ~3), (uint32_t)(s0 + qsu + 8 * g + 4 * h), (uint32_t)hqi, P.drop.off};
+      philox4x32_10(c, P.drop.k0, P.drop.k1);
+      const int sh = 8 * (key & 3);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e;
+        const bool keep = (int)((c[e] >> sh) & 255u) < P.drop.thr;
+        const float p = s[i];
+        dp[i] = p * ((keep ? dp[i] * P.drop.scale : 0.f) + cnd[acc_row(i, h)]);
+        s[i] = keep ? p * P.drop.scale : 0.f;
+      }
+    }
+  };
   auto compute = [&](int it, int buf) {
     const int qs = (first_slice + it % per_head) * QB;
     // No skip of the (at most 3 per head) slices whose queries all precede this wave's keys:
@@ -806,7 +889,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         s[i] = c0[acc_row(i, h)];
-        dp[i] = c0[QB + acc_row(i, h)];
+        dp[i] = DROP ? 0.f : c0[QB + acc_row(i, h)];
       }
       __builtin_amdgcn_sched_barrier(0);
       {
@@ -831,8 +914,12 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[i] = (acc_row0(i) < lim || acc_row0(i) > ulim) ? 0.f : s[i];
       }
+      if constexpr (DROP) {
+        drop_cols(qs, kvh * group + it / per_head, s, dp, c0 + QB);
+      } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dp[i] *= s[i];  // dS / scale
+        for (int i = 0; i < 16; ++i) dp[i] *= s[i];  // dS / scale
+      }
       const bf16x8 pf[2] = {pack8(s, 0), pack8(s, 1)};
       const bf16x8 dsf[2] = {pack8(dp, 0), pack8(dp, 1)};
       __builtin_amdgcn_sched_barrier(0);
@@ -868,7 +955,8 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
 #pragma unroll
     for (int c = 0; c < NC; ++c) dp = mfma(g[c], vf[c], dp);
   };
-  auto softmax_half = [&](int qsu, f32x16& s, f32x16& dp, bf16x8 (&pf)[2], bf16x8 (&dsf)[2]) {
+  auto softmax_half = [&](int qsu, int hqi, const float* cnd, f32x16& s, f32x16& dp, bf16x8 (&pf)[2],
+                          bf16x8 (&dsf)[2]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
     if constexpr (CAUSAL) {
@@ -876,8 +964,12 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = acc_row0(i) < lim ? 0.f : s[i];
     }
+    if constexpr (DROP) {
+      drop_cols(qsu, hqi, s, dp, cnd);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dp[i] *= s[i];
+      for (int i = 0; i < 16; ++i) dp[i] *= s[i];
+    }
     pf[0] = pack8(s, 0);
     pf[1] = pack8(s, 1);
     dsf[0] = pack8(dp, 0);
@@ -908,9 +1000,9 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       s0[i] = c0[acc_row(i, h)];
-      dp0[i] = c0[QB + acc_row(i, h)];
+      dp0[i] = DROP ? 0.f : c0[QB + acc_row(i, h)];
       s1[i] = c0[32 + acc_row(i, h)];
-      dp1[i] = c0[QB + 32 + acc_row(i, h)];
+      dp1[i] = DROP ? 0.f : c0[QB + 32 + acc_row(i, h)];
     }
     __builtin_amdgcn_sched_barrier(0);
     sd_mfma(Ql, dOl, s0, dp0);
@@ -918,10 +1010,11 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     __builtin_amdgcn_sched_barrier(0);
     bf16x8 pf0[2], dsf0[2], pf1[2], dsf1[2];
     sd_mfma(Ql + 32 * RB, dOl + 32 * RB, s1, dp1);  // || softmax of half 0
-    softmax_half(qs, s0, dp0, pf0, dsf0);
+    const int hqi = kvh * group + it / per_head;
+    softmax_half(qs, hqi, c0 + QB, s0, dp0, pf0, dsf0);
     __builtin_amdgcn_sched_barrier(0);
     kv_mfma(Ql, dOl, pf0, dsf0);  // || softmax of half 1
-    softmax_half(qs + 32, s1, dp1, pf1, dsf1);
+    softmax_half(qs + 32, hqi, c0 + QB + 32, s1, dp1, pf1, dsf1);
     __builtin_amdgcn_sched_barrier(0);
     kv_mfma(Ql + 32 * RB, dOl + 32 * RB, pf1, dsf1);
     pipeline_reads<4 * ND, 2, 3>();
@@ -1040,6 +1133,19 @@ __global__ __launch_bounds__(256) void bwd_kv_combine_kernel(const float* __rest
 
 }  // namespace fa
 
+// p -> keep threshold / scale (fa::DropCfg), and the Philox key / offset of this call.
+static fa::DropCfg make_drop(double p, int64_t seed, int64_t offset) {
+  DTG_CHECK(p >= 0.0 && p < 1.0, "flash_attn dropout: p must be in [0, 1)");
+  fa::DropCfg d{};
+  d.k0 = (uint32_t)((uint64_t)seed & 0xffffffffu);
+  d.k1 = (uint32_t)((uint64_t)seed >> 32);
+  d.off = (uint32_t)((uint64_t)offset & 0xffffffffu);
+  d.thr = (int)std::lround((1.0 - p) * 256.0);
+  d.thr = std::max(1, std::min(256, d.thr));
+  d.scale = 256.f / (float)d.thr;
+  return d;
+}
+
 // Dynamic LDS above 64 KiB must be opted into per kernel (MI355X: 160 KiB per CU).
 static void set_lds_limit(const void* fn, size_t bytes) {
   if (bytes > 65536) C10_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
@@ -1068,7 +1174,8 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
                                                               const at::Tensor& v, const at::Tensor& cu_seqlens,
                                                               int64_t max_seqlen, double scale, bool causal,
                                                               at::Tensor* stamps, const at::Tensor* k_start = nullptr,
-                                                              const at::Tensor* k_len = nullptr, int64_t window = 0) {
+                                                              const at::Tensor* k_len = nullptr, int64_t window = 0,
+                                                              const fa::DropCfg* drop = nullptr) {
   const int64_t T = q.size(0), hq = q.size(1), D = q.size(2), hkv = k.size(1);
   check_qkv(q, "q", hq, D);
   check_qkv(k, "k", hkv, D);
@@ -1108,7 +1215,16 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
 #define DTG_FWD_W(DD, C)                                                                  \
   do { if (!wide) DTG_FWD(DD, C, false, false); else if (!qlds) DTG_FWD(DD, C, true, false);   \
        else DTG_FWD(DD, C, true, true); } while (0)
-  if (P.window > 0) {  // sliding window (causal only): the WIN instantiation of the default variant
+  if (drop != nullptr) {  // attention dropout: the default variant's DROP instantiation
+    DTG_CHECK(P.window == 0 && P.kstart == nullptr, "flash_attn dropout: no sliding window / key ranges");
+    P.drop = *drop;
+#define DTG_FWD_DROP(DD, C)                                                                           \
+  do { set_lds_limit((const void*)&fa::fwd_kernel<DD, C, true, true, false, true>, lds);                 \
+       hipLaunchKernelGGL((fa::fwd_kernel<DD, C, true, true, false, true>), grid, dim3(256), lds, stream(), P); } while (0)
+    if (D == 128) { if (causal) DTG_FWD_DROP(128, true); else DTG_FWD_DROP(128, false); }
+    else { if (causal) DTG_FWD_DROP(64, true); else DTG_FWD_DROP(64, false); }
+#undef DTG_FWD_DROP
+  } else if (P.window > 0) {  // sliding window (causal only): the WIN instantiation of the default variant
     if (D == 128) { set_lds_limit((const void*)&fa::fwd_kernel<128, true, true, true, true>, lds);
                     hipLaunchKernelGGL((fa::fwd_kernel<128, true, true, true, true>), grid, dim3(256), lds, stream(), P); }
     else { set_lds_limit((const void*)&fa::fwd_kernel<64, true, true, true, true>, lds);
@@ -1139,9 +1255,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_fwd_stamped(const at::
 }
 
 static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen, int64_t hq, int nseq,
-                          hipStream_t st, bool pre_delta);
+                          hipStream_t st, bool pre_delta, bool drop = false);
 static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
-                            int nseq, hipStream_t st, const at::Tensor& dk_t, const at::Tensor& dv_t);
+                            int nseq, hipStream_t st, const at::Tensor& dk_t, const at::Tensor& dv_t, bool drop = false);
 
 // Shared backward driver: outputs are [T, H, D] views (contiguous heads, any token stride).
 static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, const at::Tensor& k,
@@ -1150,7 +1266,7 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
                                 bool causal, const at::Tensor& dq, const at::Tensor& dk,
                                 const at::Tensor& dv, const at::Tensor* k_start = nullptr,
                                 const at::Tensor* k_len = nullptr, int64_t max_seqlen_k = -1,
-                                int64_t window = 0) {
+                                int64_t window = 0, const fa::DropCfg* drop = nullptr) {
   auto dout = dout_.contiguous();
   const int64_t T = q.size(0), hq = q.size(1), D = q.size(2), hkv = k.size(1);
   check_qkv(q, "q", hq, D);
@@ -1187,6 +1303,13 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   DTG_CHECK(window >= 0 && window < (1ll << 30), "flash_attn: window must be >= 0 (0 = full causal)");
   P.window = causal ? (int)window : 0;
   if (max_seqlen_k < 0) max_seqlen_k = max_seqlen;
+  if (drop != nullptr) {
+    DTG_CHECK(P.window == 0 && P.kstart == nullptr, "flash_attn dropout: no sliding window / key ranges");
+    P.drop = *drop;
+    launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, stream(), false, true);
+    launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, stream(), dk, dv, true);
+    return;
+  }
   // Concurrent backward (DTG_FA_BWD_CONC=1; off by default): delta comes from its own small
   // kernel, then the dQ kernel runs on a side stream WHILE the dK/dV kernel runs on the
   // caller's stream, co-resident on every CU (99 KB of LDS for the pair).  The idea: each alone
@@ -1225,7 +1348,7 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
 }
 
 static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen, int64_t hq, int nseq,
-                          hipStream_t st, bool pre_delta) {
+                          hipStream_t st, bool pre_delta, bool drop) {
   static const int occ = [] {  // waves per SIMD of the dq kernel at head_dim 128 (DTG_FA_OCC=1|2)
     const char* e = std::getenv("DTG_FA_OCC");
     return (e != nullptr && e[0] == '2') ? 2 : 1;
@@ -1236,7 +1359,10 @@ static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_
 #define DTG_BWD_DQ(DD, C, O, ...)                                                         \
   do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>, lds);         \
        hipLaunchKernelGGL((fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>), grid, dim3(256), lds, st, P); } while (0)
-    if (P.window > 0) {  // sliding window (causal only)
+    if (drop) {  // attention dropout (no window, delta computed here)
+      if (D == 128) { if (causal) DTG_BWD_DQ(128, true, 1, false, false, true); else DTG_BWD_DQ(128, false, 1, false, false, true); }
+      else { if (causal) DTG_BWD_DQ(64, true, 2, false, false, true); else DTG_BWD_DQ(64, false, 2, false, false, true); }
+    } else if (P.window > 0) {  // sliding window (causal only)
       if (D == 128) DTG_BWD_DQ(128, true, 1, true); else DTG_BWD_DQ(64, true, 2, true);
     } else if (pre_delta) {
       if (D == 128) { if (causal) DTG_BWD_DQ(128, true, 1, false, true); else DTG_BWD_DQ(128, false, 1, false, true); }
@@ -1251,7 +1377,7 @@ static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_
 }
 
 static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
-                            int nseq, hipStream_t st, const at::Tensor& dk_t, const at::Tensor& dv_t) {
+                            int nseq, hipStream_t st, const at::Tensor& dk_t, const at::Tensor& dv_t, bool drop) {
   // Items the dK/dV kernel stages ahead (DTG_FA_KV_PF=1|2).  Equal on MI355X once the kernel's
   // false vmcnt waits were gone (bwd 0.767 vs 0.768 ms at the 8B shape, profiles/r1_s51_*), so
   // the single-set form with fewer registers is the default.
@@ -1264,12 +1390,13 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
   // >= 2 workgroups per CU.  DTG_FA_KV_SPLIT = N forces N (1 = off); read per call (A/B).
   const int nkb = (int)((max_seqlen_k + fa::kKvBK - 1) / fa::kKvBK);
   const int64_t wgs = (int64_t)hkv * nseq * nkb;
+  const int kv_pf_eff = drop ? 1 : kv_pf;  // dropout: the single-set, 64-row-item instantiation
   int nsplit = 1;
   const char* se = std::getenv("DTG_FA_KV_SPLIT");
   if (se != nullptr && std::atoi(se) > 0) nsplit = std::min(8, std::atoi(se));
   else if (wgs > 0 && wgs < 512) nsplit = (int)std::min<int64_t>(4, (512 + wgs - 1) / wgs);
   at::Tensor dk_part, dv_part;
-  if (nsplit > 1 && P.kstart == nullptr && P.window == 0 && kv_pf == 1) {
+  if (nsplit > 1 && P.kstart == nullptr && P.window == 0 && kv_pf_eff == 1) {
     dk_part = at::empty({nsplit, P.T, hkv, D}, dk_t.options().dtype(at::kFloat));
     dv_part = at::empty({nsplit, P.T, hkv, D}, dk_t.options().dtype(at::kFloat));
     P.dk_part = dk_part.data_ptr<float>();
@@ -1285,12 +1412,15 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
     // pipeline) is the default: backward 2-4 % faster on every benchmarked shape, -1.9 ms per 8B
     // step (profiles/r3_s39).  Sliding windows and the two-item prefetch keep 32.
     const char* qe = std::getenv("DTG_FA_KV_QB");
-    const int qb = ((qe == nullptr || std::atoi(qe) != 32) && P.window == 0 && kv_pf == 1) ? 64 : 32;
+    const int qb = drop || ((qe == nullptr || std::atoi(qe) != 32) && P.window == 0 && kv_pf == 1) ? 64 : 32;
     const size_t lds = 4 * (size_t)qb * D * 2 + 2 * 2 * qb * 4;
 #define DTG_BWD_KV(DD, C, PF, ...)                                                        \
   do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>, lds);      \
        hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>), grid, dim3(256), lds, st, P); } while (0)
-    if (P.window > 0) {  // sliding window (causal only)
+    if (drop) {
+      if (D == 128) { if (causal) DTG_BWD_KV(128, true, 1, false, 64, true); else DTG_BWD_KV(128, false, 1, false, 64, true); }
+      else { if (causal) DTG_BWD_KV(64, true, 1, false, 64, true); else DTG_BWD_KV(64, false, 1, false, 64, true); }
+    } else if (P.window > 0) {  // sliding window (causal only)
       if (D == 128) DTG_BWD_KV(128, true, 1, true); else DTG_BWD_KV(64, true, 1, true);
     } else if (kv_pf == 2) {
       if (D == 128) { if (causal) DTG_BWD_KV(128, true, 2); else DTG_BWD_KV(128, false, 2); }
@@ -1371,7 +1501,51 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_varlen_bwd(
   return {dq, dk, dv};
 }
 
+// Attention-probability dropout (GPT-2 attn_pdrop): p, Philox seed and per-call offset; the
+// backward regenerates the same keep mask (see fa::DropCfg).
+std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_drop(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                       const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale,
+                                                       bool causal, double p, int64_t seed, int64_t offset) {
+  const fa::DropCfg d = make_drop(p, seed, offset);
+  return flash_attn_fwd_impl(q, k, v, cu_seqlens, max_seqlen, scale, causal, nullptr, nullptr, nullptr, 0, &d);
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd_drop(
+    const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+    const at::Tensor& lse, const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale, bool causal, double p,
+    int64_t seed, int64_t offset) {
+  const fa::DropCfg d = make_drop(p, seed, offset);
+  auto dq = at::empty(q.sizes(), q.options());
+  auto dk = at::empty(k.sizes(), k.options());
+  auto dv = at::empty(v.sizes(), v.options());
+  flash_attn_bwd_impl(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, dq, dk, dv, nullptr, nullptr, -1, 0,
+                      &d);
+  return {dq, dk, dv};
+}
+
+at::Tensor flash_attn_bwd_qkv_drop(const at::Tensor& dout, const at::Tensor& qkv, int64_t nq, int64_t nkv,
+                                   int64_t head_dim, const at::Tensor& o, const at::Tensor& lse,
+                                   const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale, bool causal,
+                                   double p, int64_t seed, int64_t offset) {
+  DTG_CHECK_CUDA_BF16(qkv);
+  const fa::DropCfg d = make_drop(p, seed, offset);
+  const int64_t T = qkv.size(0), D = head_dim;
+  DTG_CHECK(qkv.dim() == 2 && qkv.size(1) == (nq + 2 * nkv) * D && qkv.stride(1) == 1,
+            "flash_attn_bwd_qkv_drop: qkv must be [T, (nq + 2 nkv) * D]");
+  auto dqkv = at::empty({T, (nq + 2 * nkv) * D}, qkv.options());
+  auto view3 = [&](const at::Tensor& t, int64_t h0, int64_t nh) {
+    return t.as_strided({T, nh, D}, {t.stride(0), D, 1}, t.storage_offset() + h0 * D);
+  };
+  flash_attn_bwd_impl(dout, view3(qkv, 0, nq), view3(qkv, nq, nkv), view3(qkv, nq + nkv, nkv), o, lse, cu_seqlens,
+                      max_seqlen, scale, causal, view3(dqkv, 0, nq), view3(dqkv, nq, nkv), view3(dqkv, nq + nkv, nkv),
+                      nullptr, nullptr, -1, 0, &d);
+  return dqkv;
+}
+
 TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
+  m.impl("flash_attn_fwd_drop", &flash_attn_fwd_drop);
+  m.impl("flash_attn_bwd_drop", &flash_attn_bwd_drop);
+  m.impl("flash_attn_bwd_qkv_drop", &flash_attn_bwd_qkv_drop);
   m.impl("flash_attn_varlen_fwd", &flash_attn_varlen_fwd);
   m.impl("flash_attn_varlen_bwd", &flash_attn_varlen_bwd);
   m.impl("flash_attn_fwd", &flash_attn_fwd);

@@ -59,46 +59,12 @@ class GPT2Block(nn.Module):
         p_attn = self.cfg.attn_pdrop if self.training else 0.0
         p_res = self.cfg.resid_pdrop if self.training else 0.0
         qkv = self.c_attn(self.ln_1(x))
-        if p_attn > 0:
-            # attention-probability dropout is not fused into the flash kernel; GPT-2 (the
-            # plumbing model) keeps its reference semantics through an explicit math path.
-            a = _attn_with_dropout(qkv, self.nh, self.d, cu, p_attn, dense)
-        else:
-            a = ops.attention(qkv, self.nh, self.nh, self.d, cu, max_seqlen)
+        # attention-probability dropout (attn_pdrop, 0.1 in training) runs inside the flash
+        # kernels: Philox keep mask drawn in the forward, regenerated in the backward
+        a = ops.attention(qkv, self.nh, self.nh, self.d, cu, max_seqlen, dropout_p=p_attn)
         x = x + F.dropout(self.c_proj(a), p_res, self.training)
         m = self.mlp_proj(F.gelu(self.c_fc(self.ln_2(x)), approximate="tanh"))
         return x + F.dropout(m, p_res, self.training)
-
-
-def _math_attention(q, k, v, p):
-    """Causal softmax(q k^T / sqrt(d)) with attention-probability dropout, then @ v.
-    q, k, v: [..., S, d].  GEMMs are hipBLASLt, softmax / dropout the native ATen kernels
-    (f32 softmax); used only when attention dropout is active (GPT-2 in train mode)."""
-    S = q.shape[-2]
-    s = torch.matmul(q, k.transpose(-1, -2)).float() * (q.shape[-1] ** -0.5)
-    s.masked_fill_(torch.ones(S, S, dtype=torch.bool, device=s.device).triu_(1), float("-inf"))
-    pr = F.dropout(torch.softmax(s, dim=-1), p, True)
-    return torch.matmul(pr.to(v.dtype), v)
-
-
-def _attn_with_dropout(qkv, nh, d, cu, p, dense=None):
-    """GPT-2 attention with dropout on the probabilities (reference semantics, attn_pdrop 0.1).
-    The flash kernels have no dropout, so this path materialises the [S, S] scores per head:
-    batched for dense [B, S] batches, one sequence at a time for packed ones."""
-    T = qkv.shape[0]
-    if dense is not None:
-        B, S = dense
-        q, k, v = qkv.view(B, S, 3, nh, d).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, d] each
-        return _math_attention(q, k, v, p).permute(0, 2, 1, 3).reshape(T, nh * d)
-    q, k, v = qkv.view(T, 3, nh, d).unbind(1)
-    bounds = cu.tolist()
-    outs = []
-    for i in range(len(bounds) - 1):
-        a, b = bounds[i], bounds[i + 1]
-        qs, ks, vs = (t[a:b].transpose(0, 1) for t in (q, k, v))
-        outs.append(_math_attention(qs, ks, vs, p).transpose(0, 1))
-    out = torch.cat(outs, 0) if outs else torch.empty(T, nh, d, dtype=qkv.dtype, device=qkv.device)
-    return out.reshape(T, nh * d)
 
 
 class GPT2LMHeadModel(nn.Module):

@@ -208,6 +208,126 @@ def flash_attn_fwd(q, k, v, cu_seqlens, max_seqlen, scale, causal, window=0):
     return o.to(q.dtype), lse
 
 
+# ---- attention dropout: the kernels' counter-based keep mask (csrc/kernels/flash_attn.hip DropCfg)
+_PHILOX_M = (0xD2511F53, 0xCD9E8D57)
+_PHILOX_W = (0x9E3779B9, 0xBB67AE85)
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 on numpy uint64 arrays holding 32-bit values (Random123's round function)."""
+    import numpy as np
+
+    m32 = np.uint64(0xFFFFFFFF)
+    c = [np.asarray(x, dtype=np.uint64) & m32 for x in (c0, c1, c2, c3)]
+    k0, k1 = np.uint64(k0) & m32, np.uint64(k1) & m32
+    for r in range(10):
+        if r:
+            k0 = (k0 + np.uint64(_PHILOX_W[0])) & m32
+            k1 = (k1 + np.uint64(_PHILOX_W[1])) & m32
+        p0 = np.uint64(_PHILOX_M[0]) * c[0]
+        p1 = np.uint64(_PHILOX_M[1]) * c[2]
+        c = [(p1 >> np.uint64(32)) ^ c[1] ^ k0, p1 & m32, (p0 >> np.uint64(32)) ^ c[3] ^ k1, p0 & m32]
+    return c
+
+
+def dropout_threshold(p):
+    """(thr, scale): keep iff random byte < thr; keep probability thr / 256, scale 256 / thr."""
+    thr = max(1, min(256, int(round((1.0 - p) * 256.0))))
+    return thr, 256.0 / thr
+
+
+def dropout_keep(seed, offset, head, s0, nq, nk, p):
+    """bool [nq, nk]: the keep decision of (query q, key k) of the sequence starting at token s0
+    (sequence-relative q, k) for query head `head` -- byte (k & 3) of word (q & 3) of
+    Philox4x32-10({k & ~3, s0 + (q & ~3), head, offset}, seed)."""
+    import numpy as np
+
+    thr, _ = dropout_threshold(p)
+    q = np.arange(nq, dtype=np.uint64)[:, None]
+    k = np.arange(nk, dtype=np.uint64)[None, :]
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    w = philox4x32_10(k & ~np.uint64(3), np.uint64(s0) + (q & ~np.uint64(3)), np.full_like(q, head),
+                      np.full_like(q, int(offset) & 0xFFFFFFFF), seed & 0xFFFFFFFF, seed >> 32)
+    sel = (q & np.uint64(3)).astype(np.int64)
+    word = np.choose(np.broadcast_to(sel, (nq, nk)), [np.broadcast_to(x, (nq, nk)) for x in w])
+    byte = (word >> (np.uint64(8) * (k & np.uint64(3)))) & np.uint64(255)
+    return torch.from_numpy(byte.astype(np.int64) < thr)
+
+
+def _drop_masks(cu_seqlens, hq, p, seed, offset):
+    out = []
+    for a, b, _, _ in _key_ranges(cu_seqlens):
+        out.append(torch.stack([dropout_keep(seed, offset, h, a, b - a, b - a, p) for h in range(hq)]) if b > a else None)
+    return out
+
+
+def flash_attn_fwd_drop(q, k, v, cu_seqlens, max_seqlen, scale, causal, p, seed, offset):
+    """o = (M o softmax(S) * 256/thr) V per sequence; lse of the undropped softmax."""
+    _check_attn_inputs(q, k, v)
+    T, hq, d = q.shape
+    rep = hq // k.shape[1]
+    _, sc_keep = dropout_threshold(p)
+    o = torch.zeros(T, hq, d, dtype=torch.float32)
+    lse = torch.full((hq, T), float("-inf"), dtype=torch.float32)
+    for (a, b, _, _), m in zip(_key_ranges(cu_seqlens), _drop_masks(cu_seqlens, hq, p, seed, offset)):
+        if b <= a:
+            continue
+        qs = q[a:b].float().transpose(0, 1)
+        ks = k[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        vs = v[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        s = qs @ ks.transpose(1, 2) * scale
+        if causal:
+            s = s.masked_fill(_mask(b - a, b - a), float("-inf"))
+        l_ = torch.logsumexp(s, -1)
+        pr = torch.exp(s - l_[..., None]) * m * sc_keep
+        o[a:b] = (pr @ vs).transpose(0, 1)
+        lse[:, a:b] = l_
+    return o.to(q.dtype), lse
+
+
+def flash_attn_bwd_drop(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, p, seed, offset):
+    _check_attn_inputs(q, k, v)
+    T, hq, d = q.shape
+    hkv = k.shape[1]
+    rep = hq // hkv
+    _, sc_keep = dropout_threshold(p)
+    dq = torch.zeros(T, hq, d, dtype=torch.float32)
+    dk = torch.zeros(T, hkv, d, dtype=torch.float32)
+    dv = torch.zeros(T, hkv, d, dtype=torch.float32)
+    for (a, b, _, _), m in zip(_key_ranges(cu_seqlens), _drop_masks(cu_seqlens, hq, p, seed, offset)):
+        if b <= a:
+            continue
+        qs = q[a:b].float().transpose(0, 1)
+        ks = k[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        vs = v[a:b].float().transpose(0, 1).repeat_interleave(rep, 0)
+        dos = dout[a:b].float().transpose(0, 1)
+        os_ = o[a:b].float().transpose(0, 1)
+        s = qs @ ks.transpose(1, 2) * scale
+        if causal:
+            s = s.masked_fill(_mask(b - a, b - a), float("-inf"))
+        pr = torch.exp(s - lse[:, a:b].float()[..., None])
+        z = pr * m * sc_keep
+        dvh = z.transpose(1, 2) @ dos
+        dpr = (dos @ vs.transpose(1, 2)) * m * sc_keep
+        delta = (dos * os_).sum(-1, keepdim=True)
+        ds = pr * (dpr - delta)
+        dq[a:b] = (ds @ ks * scale).transpose(0, 1)
+        dk[a:b] += (ds.transpose(1, 2) @ qs * scale).view(hkv, rep, b - a, d).sum(1).transpose(0, 1)
+        dv[a:b] += dvh.view(hkv, rep, b - a, d).sum(1).transpose(0, 1)
+    return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
+
+
+def flash_attn_bwd_qkv_drop(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal, p, seed,
+                            offset):
+    T = qkv.shape[0]
+    d = head_dim
+    q = qkv[:, : nq * d].reshape(T, nq, d)
+    k = qkv[:, nq * d : (nq + nkv) * d].reshape(T, nkv, d)
+    v = qkv[:, (nq + nkv) * d :].reshape(T, nkv, d)
+    dq, dk, dv = flash_attn_bwd_drop(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, p, seed, offset)
+    return torch.cat([dq.reshape(T, -1), dk.reshape(T, -1), dv.reshape(T, -1)], dim=1)
+
+
 def flash_attn_varlen_fwd(q, k, v, cu_seqlens_q, k_start, k_len, max_seqlen_q, max_seqlen_k, scale, causal):
     _check_attn_inputs(q, k, v)
     o, lse = _attn_ref(q, k, v, cu_seqlens_q, scale, causal, k_start, k_len)
@@ -299,6 +419,6 @@ for _name, _fn in list(globals().items()):
         "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "adamw_t_", "flash_attn_fwd", "flash_attn_bwd",
         "flash_attn_bwd_qkv", "transpose2d", "transpose_mats_", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
-        "flash_attn_varlen_bwd",
+        "flash_attn_varlen_bwd", "flash_attn_fwd_drop", "flash_attn_bwd_drop", "flash_attn_bwd_qkv_drop",
     ):
         LIB.impl(_name, _fn, "CPU")

@@ -37,6 +37,13 @@ _DEFS = [
     "int max_seqlen, float scale, bool causal, int window=0) -> (Tensor, Tensor, Tensor)",
     "flash_attn_bwd_qkv(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
     "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, int window=0) -> Tensor",
+    # attention-probability dropout regenerated from Philox(seed, offset) in the backward
+    "flash_attn_fwd_drop(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, bool causal, "
+    "float p, int seed, int offset) -> (Tensor, Tensor)",
+    "flash_attn_bwd_drop(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor cu_seqlens, "
+    "int max_seqlen, float scale, bool causal, float p, int seed, int offset) -> (Tensor, Tensor, Tensor)",
+    "flash_attn_bwd_qkv_drop(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
+    "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, float p, int seed, int offset) -> Tensor",
     "transpose2d(Tensor x) -> Tensor",
     # many matrices of a flat buffer transposed in one launch: rows of `mats` (int64 [n, 5]:
     # source offset, rows, cols, destination offset, first 64 x 64 tile); `mats_host` = its CPU copy

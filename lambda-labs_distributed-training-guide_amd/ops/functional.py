@@ -225,6 +225,40 @@ class _AttentionQKV(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
 
 
+class _AttentionQKVDrop(torch.autograd.Function):
+    """Attention with dropout on the probabilities, inside the flash kernels: the keep mask is a
+    counter-based (Philox) function of (seed, offset, head, query, key), drawn in the forward and
+    regenerated in the backward -- nothing [S, S] is stored."""
+
+    @staticmethod
+    def forward(ctx, qkv, cu_seqlens, max_seqlen, nq, nkv, head_dim, scale, causal, p, seed, offset):
+        T = qkv.shape[0]
+        d = head_dim
+        q = qkv.as_strided((T, nq, d), (qkv.stride(0), d, 1), qkv.storage_offset())
+        k = qkv.as_strided((T, nkv, d), (qkv.stride(0), d, 1), qkv.storage_offset() + nq * d)
+        v = qkv.as_strided((T, nkv, d), (qkv.stride(0), d, 1), qkv.storage_offset() + (nq + nkv) * d)
+        o, lse = ops.flash_attn_fwd_drop(q, k, v, cu_seqlens, max_seqlen, scale, causal, p, seed, offset)
+        ctx.save_for_backward(qkv, o, lse, cu_seqlens)
+        ctx.meta = (max_seqlen, nq, nkv, d, scale, causal, p, seed, offset)
+        return o.view(T, nq * d)
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, cu = ctx.saved_tensors
+        max_seqlen, nq, nkv, d, scale, causal, p, seed, offset = ctx.meta
+        T = qkv.shape[0]
+        dqkv = ops.flash_attn_bwd_qkv_drop(do.contiguous().view(T, nq, d), qkv, nq, nkv, d, o, lse, cu, max_seqlen,
+                                           scale, causal, p, seed, offset)
+        return dqkv, None, None, None, None, None, None, None, None, None, None
+
+
+def dropout_seed_offset(generator=None):
+    """(seed, offset) of one dropout call, from torch's CPU generator (host only, no device sync;
+    reproducible under torch.manual_seed and checkpointed with the RNG state)."""
+    r = torch.randint(0, 2**62, (2,), generator=generator)
+    return int(r[0]), int(r[1] % (2**31))
+
+
 class _Rope(torch.autograd.Function):
     """Out-of-place RoPE on the q and k heads of a fused QKV activation (v untouched)."""
 
@@ -276,13 +310,22 @@ def _attention_padded(qkv, nq, nkv, d, cu_seqlens, max_seqlen, cos, sin, pos, ca
 
 
 def attention(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos=None, sin=None, pos=None, causal=True, scale=None,
-              window=0):
+              window=0, dropout_p=0.0):
     """Causal (varlen) GQA attention on a fused [T, (nq+2nkv)*d] QKV activation -> [T, nq*d].
 
     If cos/sin/pos are given, RoPE is applied to q and k first (in place on qkv).  window > 0:
-    sliding-window attention (query i sees keys i - window < j <= i; Mistral)."""
+    sliding-window attention (query i sees keys i - window < j <= i; Mistral).  dropout_p > 0:
+    dropout on the attention probabilities inside the flash kernels (GPT-2 training)."""
     if scale is None:
         scale = 1.0 / math.sqrt(head_dim)
+    if dropout_p > 0.0:
+        if cos is not None or window:
+            raise ValueError("attention dropout is supported without RoPE / sliding windows (GPT-2)")
+        if qkv.is_cuda and head_dim not in FA_HEAD_DIMS:
+            raise ValueError(f"attention dropout: head_dim {head_dim} needs a kernel instantiation {FA_HEAD_DIMS}")
+        seed, offset = dropout_seed_offset()
+        return _AttentionQKVDrop.apply(qkv, cu_seqlens, int(max_seqlen), nq, nkv, head_dim, float(scale), causal,
+                                       float(dropout_p), seed, offset)
     if qkv.is_cuda and head_dim not in FA_HEAD_DIMS:  # the CPU reference takes any width
         return _attention_padded(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos, sin, pos, causal, scale, window)
     rope = cos is not None

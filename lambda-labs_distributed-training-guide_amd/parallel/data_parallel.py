@@ -57,8 +57,12 @@ class DataParallel:
                  bucket_mb: int = 256, broadcast_from_rank0: bool = True, state_dtype=torch.bfloat16,
                  master_weights: bool = False, overlap_param_gather: bool = True,
                  overlap_optimizer: bool = False, grad_divisor: Optional[int] = None,
-                 force_collectives: bool = False, weight_t: Optional[bool] = None):
+                 force_collectives: bool = False, weight_t: Optional[bool] = None, dp_comm: str = "rccl"):
+        """dp_comm: "rccl" (default; also the inter-node path) or "xgmi-dma": ZeRO's gradient
+        reduce-scatter and parameter all-gather as copy-engine pulls between the ranks' shared
+        flat buffers over xGMI (parallel/xgmi_dp.py; one node, no CU time in the overlap)."""
         assert mode in ("single", "ddp", "zero")
+        assert dp_comm in ("rccl", "xgmi-dma"), dp_comm
         self.module = model
         self.group = group
         self.tp_group = tp_group
@@ -74,9 +78,16 @@ class DataParallel:
         for n, p in named:
             p._dtg_name = n
         tp_on = tp_group is not None and comm.world(tp_group) > 1
+        self.xdp = None
+        if dp_comm == "xgmi-dma" and self.mode == "zero" and self.world > 1 and dev.type == "cuda":
+            from .xgmi_dp import XgmiZero
+
+            self.xdp = XgmiZero(group, dev)
+        self.dp_comm = "xgmi-dma" if self.xdp is not None else "rccl"
         self.space = FlatSpace(named, dev, world=self.world if self.mode == "zero" else 1,
                                bucket_bytes=bucket_mb << 20, dtype=named[0][1].dtype,
-                               trailing=(lambda p: getattr(p, "_dtg_sequence_parallel", False)) if tp_on else None)
+                               trailing=(lambda p: getattr(p, "_dtg_sequence_parallel", False)) if tp_on else None,
+                               alloc=self.xdp.alloc if self.xdp is not None else None)
         self._sp_bucket = next((b for b in self.space.buckets if b.trailing), None)
         self._sp_reduced = False
         self.params = rebind_parameters(model, self.space, copy_data=True, notify=self._on_grad)
@@ -306,7 +317,11 @@ class DataParallel:
             i = b.index
             o = self.shard_offsets[i]
             s, e = self.shard_ranges[i]
-            b.work = comm.reduce_scatter_into(self.grad_shard[o:o + (e - s)], view, group=self.group, async_op=True)
+            if self.xdp is not None:
+                ranges = [self.space.shard_range(b, r) for r in range(self.world)]
+                b.work = self.xdp.reduce_scatter(self.space.grad_buf, ranges, self.grad_shard[o:o + (e - s)])
+            else:
+                b.work = comm.reduce_scatter_into(self.grad_shard[o:o + (e - s)], view, group=self.group, async_op=True)
         self._inflight.append(b)
         if self.overlap_optimizer:
             self._step_bucket_in_backward(b)
@@ -441,8 +456,11 @@ class DataParallel:
         b = self.space.buckets[i]
         s, e = self.shard_ranges[i]
         src = buf[s:e]
-        self._pending_ag[i] = comm.all_gather_into(buf[b.start:b.end], src.clone() if gloo else src,
-                                                   group=self.group, async_op=True)
+        if self.xdp is not None:
+            self._pending_ag[i] = self.xdp.all_gather(buf, [self.space.shard_range(b, r) for r in range(self.world)])
+        else:
+            self._pending_ag[i] = comm.all_gather_into(buf[b.start:b.end], src.clone() if gloo else src,
+                                                       group=self.group, async_op=True)
         self._transpose_bucket(i, self._pending_ag[i])
 
     def wait_param_gather(self, buckets=None):

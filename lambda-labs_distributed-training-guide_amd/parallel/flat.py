@@ -48,10 +48,12 @@ class FlatSpace:
 
     def __init__(self, named_params: Sequence[Tuple[str, nn.Parameter]], device, world: int = 1,
                  bucket_bytes: int = 256 << 20, dtype=torch.bfloat16, grad_dtype=None, reverse=True,
-                 alloc_params=True, trailing: Optional[Callable] = None):
+                 alloc_params=True, trailing: Optional[Callable] = None, alloc: Optional[Callable] = None):
         """`trailing(p)`: parameters moved into one extra bucket after all others (tensor-
         parallel replicated norm weights: their gradients are summed over TP with ONE
-        all-reduce of that bucket instead of one per parameter)."""
+        all-reduce of that bucket instead of one per parameter).  `alloc(numel, dtype, kind)`
+        (kind "param" | "grad") provides the flat buffers instead of torch.zeros (IPC-shared
+        memory for the xGMI copy-engine collectives, parallel/xgmi_dp.py)."""
         self.world = world
         self.device = torch.device(device)
         self.dtype = dtype
@@ -87,8 +89,10 @@ class FlatSpace:
         self.numel = cur
         self.shapes = [tuple(p.shape) for _, p in items]
         self.params_src = [p for _, p in items]
-        self.param_buf = torch.zeros(self.numel, dtype=dtype, device=self.device) if alloc_params else None
-        self.grad_buf = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
+        if alloc is None:
+            alloc = lambda n, dt, kind: torch.zeros(n, dtype=dt, device=self.device)  # noqa: E731
+        self.param_buf = alloc(self.numel, dtype, "param") if alloc_params else None
+        self.grad_buf = alloc(self.numel, self.grad_dtype, "grad")
         self.buckets = [Bucket(i, s, e, ps, trailing=bool(tail) and i == len(buckets_spec) - 1)
                         for i, (s, e, ps) in enumerate(buckets_spec)]
         self.param_bucket = []

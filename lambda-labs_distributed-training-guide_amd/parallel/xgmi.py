@@ -128,6 +128,34 @@ class XgmiCommunicator:
         torch.ops.dtg_xgmi.all_reduce(self.id, t, self._offset(t))
         return t
 
+    # ------------------------------------------------------------------ shared buffers
+    def alloc_shared(self, nbytes: int) -> tuple:
+        """(uint8 tensor, slot): a buffer of `nbytes` that every rank of the group allocates in
+        the same call, IPC-exported and mapped from every peer (collective)."""
+        x = torch.ops.dtg_xgmi
+        t = x.alloc_shared(self.id, int(nbytes))
+        slot = getattr(self, "_nshared", 0)
+        self._nshared = slot + 1
+        mine = bytes(x.shared_handle(self.id, slot).tolist())
+        handles = [None] * self.world
+        dist.all_gather_object(handles, mine, group=self.group)
+        x.open_shared(self.id, slot, torch.tensor([list(h) for h in handles], dtype=torch.uint8))
+        return t, slot
+
+    def signal_wait(self):
+        """Stream-ordered barrier: returns (on the device) once every peer's stream reached it."""
+        if self._skip():
+            return
+        torch.ops.dtg_xgmi.signal_wait(self.id)
+
+    def pull(self, slot: int, dst: torch.Tensor, src_off, nbytes, dst_off):
+        """Copy-engine pulls from every peer's copy of shared `slot` into `dst` (byte ranges)."""
+        lt = lambda v: torch.tensor(v, dtype=torch.long)  # noqa: E731
+        torch.ops.dtg_xgmi.pull(self.id, slot, dst, lt(src_off), lt(nbytes), lt(dst_off))
+
+    def reduce_pulled(self, out: torch.Tensor, scratch: torch.Tensor, own: torch.Tensor):
+        torch.ops.dtg_xgmi.reduce_pulled(self.id, out, scratch, own)
+
     # ------------------------------------------------------------------ zero-copy slots
     def rs_input_buffer(self, shape, dtype, stage_bytes: int = 0):
         """A workspace view of `shape` for a producer to write a reduce-scatter input into, or

@@ -226,7 +226,10 @@ def _build(args, chapter, device, world):
         engine = DataParallel(model, mode=mode, group=dp_group if pp > 1 else (None if seq is not None else dp_group),
                               tp_group=tp_group,
                               bucket_mb=args.bucket_mb, broadcast_from_rank0=tp_group is None,
-                              grad_divisor=dp_size if seq is not None else None)
+                              grad_divisor=dp_size if seq is not None else None,
+                              dp_comm=getattr(args, "dp_comm", "rccl") if device.type == "cuda" else "rccl")
+        if getattr(engine, "xdp", None) is not None:
+            LOGGER.info("ZeRO collectives: copy-engine pulls over xGMI between the ranks' shared flat buffers")
         style = "full" if mode == "single" and chapter in ("01", "rime") else ("dp" if chapter == "02" else "sharded")
         if pp > 1:
             style = "sharded"  # no rank holds the whole model: no model.pt

@@ -37,11 +37,20 @@ def unregister_xgmi(group):
     return _XGMI.pop(group, None)
 
 
+# Communicators that carry no TP/SP traffic but must be health-checked too (the data-parallel
+# copy-engine path, parallel/xgmi_dp.py).
+_XGMI_HEALTH = []
+
+
+def register_xgmi_health(communicator):
+    _XGMI_HEALTH.append(communicator)
+
+
 def check_xgmi():
     """Raise XgmiError if any registered direct-peer communicator saw a barrier time out (a
     peer died or fell out of step).  Synchronises the device.  Called by the trainer at every
     log step, checkpoint and exit."""
-    for c in list(_XGMI.values()):
+    for c in list(_XGMI.values()) + [c for c in _XGMI_HEALTH if getattr(c, "id", None) is not None]:
         c.check()
 
 
@@ -49,7 +58,7 @@ def poll_xgmi():
     """Like check_xgmi() but without synchronising the device: reads each communicator's
     host-pinned error word (written by a barrier kernel that timed out).  Cheap enough for
     every training step."""
-    for c in list(_XGMI.values()):
+    for c in list(_XGMI.values()) + [c for c in _XGMI_HEALTH if getattr(c, "id", None) is not None]:
         c.check(sync=False)
 
 

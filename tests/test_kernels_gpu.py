@@ -362,6 +362,67 @@ def _attn_case(cuda, seqlens, hq, hkv, D, causal, stride_extra=0, qscale=1.0, wi
     return qkv, cu
 
 
+@pytest.mark.parametrize("D,hq,hkv,seqlens", [(64, 12, 12, [1024, 1024]), (64, 4, 4, [100, 257, 3, 667]),
+                                               (128, 8, 2, [300, 131]), (128, 2, 1, [2048])])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_flash_attn_dropout_matches_masked_reference(cuda, D, hq, hkv, seqlens, causal, p, monkeypatch):
+    """Attention-probability dropout inside the kernels (GPT-2's attn_pdrop) against the f32
+    reference that applies the SAME Philox keep mask (dtg.ops._cpu.dropout_keep): forward, and
+    the backward that regenerates the mask in both the query-stationary dQ kernel and the
+    key-stationary dK/dV kernel (also with its query items split over workgroups).  A mask that
+    differed in even a few elements per row would move the outputs far beyond the tolerance."""
+    torch.manual_seed(1)
+    T = sum(seqlens)
+    cu = torch.tensor([0] + list(torch.tensor(seqlens).cumsum(0).tolist()), dtype=torch.int32)
+    q = torch.randn(T, hq, D).bfloat16()
+    k = torch.randn(T, hkv, D).bfloat16()
+    v = torch.randn(T, hkv, D).bfloat16()
+    do = torch.randn(T, hq, D).bfloat16()
+    scale = 1 / math.sqrt(D)
+    seed, off = 0x123456789AB, 77
+    o_ref, lse_ref = dops.flash_attn_fwd_drop(q, k, v, cu, max(seqlens), scale, causal, p, seed, off)
+    o, lse = dops.flash_attn_fwd_drop(q.to(cuda), k.to(cuda), v.to(cuda), cu.to(cuda), max(seqlens), scale, causal, p,
+                                      seed, off)
+    _close(o, o_ref, 3e-2, 2e-2, "attn out (dropout)")
+    _close(lse, lse_ref, 2e-3, 1e-3, "lse")
+    ref = dops.flash_attn_bwd_drop(do, q, k, v, o_ref, lse_ref, cu, max(seqlens), scale, causal, p, seed, off)
+    for split in ("1", "3"):
+        monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
+        got = dops.flash_attn_bwd_drop(do.to(cuda), q.to(cuda), k.to(cuda), v.to(cuda), o, lse, cu.to(cuda),
+                                       max(seqlens), scale, causal, p, seed, off)
+        for a, b, n in zip(got, ref, ("dq", "dk", "dv")):
+            assert _rel(a, b) < 2e-2, f"{n} (split {split}) rel err {_rel(a, b)}"
+    # another offset is another mask
+    o2, _ = dops.flash_attn_fwd_drop(q.to(cuda), k.to(cuda), v.to(cuda), cu.to(cuda), max(seqlens), scale, causal, p,
+                                     seed, off + 1)
+    assert _rel(o2, o_ref) > 5e-2
+
+
+def test_gpt2_trains_through_the_dropout_kernels(cuda):
+    """GPT-2 in train mode (attn_pdrop 0.1) runs its attention through the flash kernels
+    (no [S, S] materialisation) and its loss decreases on a repeated batch."""
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    torch.manual_seed(0)
+    cfg = resolve_config("gpt2")
+    m = build_model(cfg, device=cuda)
+    m.train()
+    eng = DataParallel(m, mode="single")
+    opt = FlatAdamW(eng, lr=1e-3)
+    ids = torch.randint(0, cfg.vocab_size, (4, 1024), device=cuda)
+    losses = []
+    for _ in range(6):
+        opt.zero_grad()
+        out = m(input_ids=ids, labels=ids)
+        eng.backward(out.loss)
+        opt.step()
+        losses.append(out.loss.item())
+    torch.cuda.synchronize()
+    assert all(math.isfinite(x) for x in losses) and losses[-1] < losses[0] - 0.5, losses
+
+
 @pytest.mark.parametrize("seqlens", [[1024], [100, 257, 667], [64, 1, 129, 130]])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attn_d128_gqa(cuda, seqlens, causal):

@@ -1,5 +1,7 @@
 """T1: owned models vs HF transformers (installed 5.x) on tiny configs with identical weights."""
 import pytest
+import math
+
 import torch
 
 import dtg  # noqa: F401
@@ -149,21 +151,38 @@ def test_resize_token_embeddings_mean_rows(name):
     assert torch.isfinite(out.loss)
 
 
-def test_gpt2_attention_dropout_path_matches_flash_semantics():
-    """The explicit dropout path (GPT-2 train mode) == the flash op at p=0, dense and packed."""
+def test_gpt2_attention_dropout_in_the_flash_op():
+    """GPT-2's attention-probability dropout goes through the flash op (the kernels' Philox keep
+    mask): p = 0 is the plain op; at p > 0 the output equals the explicit masked softmax with the
+    op's own keep mask, the same torch seed reproduces it, and gradients flow."""
     from dtg import ops
-    from dtg.models.gpt2 import _attn_with_dropout
+    from dtg.ops import _cpu
+    from dtg.ops.functional import dropout_seed_offset
 
     torch.manual_seed(0)
     B, S, nh, d = 2, 24, 3, 16
     T = B * S
     qkv = torch.randn(T, 3 * nh * d)
-    cu = torch.tensor([0, S, T], dtype=torch.int32)
-    ref = ops.attention(qkv, nh, nh, d, cu, S)
-    torch.testing.assert_close(_attn_with_dropout(qkv, nh, d, cu, 0.0, dense=(B, S)), ref, atol=1e-5, rtol=1e-4)
-    cu2 = torch.tensor([0, 10, 30, T], dtype=torch.int32)
-    ref2 = ops.attention(qkv, nh, nh, d, cu2, 20)
-    torch.testing.assert_close(_attn_with_dropout(qkv, nh, d, cu2, 0.0), ref2, atol=1e-5, rtol=1e-4)
+    cu = torch.tensor([0, 10, 30, T], dtype=torch.int32)
+    torch.testing.assert_close(ops.attention(qkv, nh, nh, d, cu, 20, dropout_p=1e-9), ops.attention(qkv, nh, nh, d, cu, 20))
+    torch.manual_seed(5)
+    got = ops.attention(qkv, nh, nh, d, cu, 20, dropout_p=0.25)
+    torch.manual_seed(5)
+    again = ops.attention(qkv, nh, nh, d, cu, 20, dropout_p=0.25)
+    assert torch.equal(got, again)
+    torch.manual_seed(5)
+    seed, off = dropout_seed_offset()
+    q, k, v = qkv.view(T, 3, nh, d).unbind(1)
+    _, sc = _cpu.dropout_threshold(0.25)
+    want = torch.zeros(T, nh, d)
+    for a_, b_ in ((0, 10), (10, 30), (30, T)):
+        m = torch.stack([_cpu.dropout_keep(seed, off, h, a_, b_ - a_, b_ - a_, 0.25) for h in range(nh)])
+        s = (q[a_:b_].transpose(0, 1) @ k[a_:b_].transpose(0, 1).transpose(1, 2)) / math.sqrt(d)
+        s = s.masked_fill(torch.ones(b_ - a_, b_ - a_, dtype=torch.bool).triu(1), float("-inf"))
+        want[a_:b_] = ((torch.softmax(s, -1) * m * sc) @ v[a_:b_].transpose(0, 1)).transpose(0, 1)
+    torch.testing.assert_close(got, want.reshape(T, nh * d), atol=1e-5, rtol=1e-4)
+    frac = torch.cat([_cpu.dropout_keep(seed, off, 0, 0, 256, 256, 0.1).flatten()]).float().mean()
+    assert abs(frac - 230 / 256) < 0.01  # keep probability thr / 256
     x = qkv.clone().requires_grad_()
-    _attn_with_dropout(x, nh, d, cu, 0.1, dense=(B, S)).sum().backward()
+    ops.attention(x, nh, nh, d, cu, 20, dropout_p=0.1).sum().backward()
     assert torch.isfinite(x.grad).all()
