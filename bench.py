@@ -168,7 +168,7 @@ def build_job(args, torch, device, cuda, bucket_mb=None, dp_comm=None):
     if args.parallel == "fsdp":
         from dtg.parallel.fsdp import FullyShard
 
-        engine = FullyShard(model, group=dp_group, tp_group=tp_group)
+        engine = FullyShard(model, group=dp_group, tp_group=tp_group, dp_comm=(dp_comm or args.dp_comm) if cuda else "rccl")
     else:
         engine = DataParallel(model, mode=args.parallel if dp_size > 1 else "single", group=dp_group, tp_group=tp_group,
                               bucket_mb=bucket_mb or args.bucket_mb, broadcast_from_rank0=tp_group is None,

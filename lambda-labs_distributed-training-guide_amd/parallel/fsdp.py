@@ -135,7 +135,7 @@ class FullyShard:
                  state_dtype=torch.bfloat16, init_fn: Optional[Callable] = None, seed: int = 0,
                  prefetch: bool = True, max_inflight_rs: int = 2, tp_group=None, replicate_group=None,
                  overlap_cpu_step: bool = True, force_collectives: bool = False, offload_params: bool = True,
-                 grad_ring: int = 0):
+                 grad_ring: int = 0, dp_comm: str = "rccl"):
         self.module = model
         self.group = group
         # HYBRID_SHARD (ZeRO++-style): shard inside `group` (one node's xGMI island), replicate
@@ -204,7 +204,19 @@ class FullyShard:
         # parameter of host RAM (101 GB per rank for Llama-3.1-405B at W = 8: the difference
         # between fitting eight ranks' offloaded state in one node's 3 TB or not).
         self.grad_ring = int(grad_ring) if cpu_offload else 0
-        if pin:  # exact-size page-locked buffers (the caching host allocator rounds to 2^k)
+        # dp_comm="xgmi-dma": unit all-gathers / reduce-scatters as copy-engine pulls between the
+        # ranks' shared shard buffers and gradient pools over xGMI (parallel/xgmi_dp.py; one node)
+        self.xdp = None
+        if (dp_comm == "xgmi-dma" and self._coll and self.world > 1 and self.device.type == "cuda"
+                and (not cpu_offload or self.resident)):
+            from .xgmi_dp import XgmiFsdp
+
+            self.xdp = XgmiFsdp(group, self.device, nslots=max_inflight_rs + 3)  # + root + current + 1 spare
+        self.dp_comm = "xgmi-dma" if self.xdp is not None else "rccl"
+        if self.xdp is not None and not cpu_offload:
+            self.shard_params = self.xdp.alloc_shards(total, self.dtype)
+            self.shard_grads = torch.zeros(total, dtype=self.dtype, device=home)
+        elif pin:  # exact-size page-locked buffers (the caching host allocator rounds to 2^k)
             from ..utils.pinned import pinned_zeros
 
             self.shard_params = pinned_zeros(total, self.dtype)
@@ -215,7 +227,10 @@ class FullyShard:
         self.exp_avg = torch.zeros(total, dtype=state_dtype, device=home)
         self.exp_avg_sq = torch.zeros(total, dtype=state_dtype, device=home)
         # resident mode: the GPU copy every gather reads (the host shard_params is the master)
-        self.gpu_params = torch.zeros(total, dtype=self.dtype, device=self.device) if self.resident else None
+        self.gpu_params = None
+        if self.resident:
+            self.gpu_params = (self.xdp.alloc_shards(total, self.dtype) if self.xdp is not None
+                               else torch.zeros(total, dtype=self.dtype, device=self.device))
         self._h2d_stream = torch.cuda.Stream(device=self.device) if (self.resident and self.device.type == "cuda") else None
         self._d2h_stream = torch.cuda.Stream(device=self.device) if (cpu_offload and self.device.type == "cuda") else None
         self._d2h_events = []
@@ -228,6 +243,8 @@ class FullyShard:
             u.shard_off = o
             o += u.shard_numel
         self.all_units = all_units
+        if self.xdp is not None:
+            self.xdp.alloc_grad_pool(max(u.numel for u in all_units), self.dtype)
         self._ring, self._ring_busy, self._ring_next = [], [], 0
         if self.grad_ring:
             from ..utils.pinned import pinned_zeros
@@ -335,6 +352,10 @@ class FullyShard:
                 u.gather_work = None
                 u.gathered = True
                 return
+            if self.xdp is not None:
+                u.gather_work = self.xdp.gather(u.full, u.shard_off, u.shard_numel, shard)
+                u._gather_src = shard
+                return
             if comm.backend_of(self.group) == "gloo":
                 dist.all_gather_into_tensor(u.full, shard.contiguous(), group=self.group)
                 u.gathered = True
@@ -415,7 +436,10 @@ class FullyShard:
     def _prepare_grads(self, u: _Unit):
         if u.full_grad is not None:
             return
-        u.full_grad = torch.empty(u.numel, dtype=self.dtype, device=self.device)
+        if self.xdp is not None:  # a slot of the shared gradient pool the peers pull from
+            u.full_grad, u.grad_slot = self.xdp.grad_buffer(u.numel)
+        else:
+            u.full_grad = torch.empty(u.numel, dtype=self.dtype, device=self.device)
         # a fresh (uninitialised) full gradient per micro-batch: the first write of every param
         # must overwrite, not accumulate (micro-batches are summed in the gradient shard)
         reset_grad_state(u.params)
@@ -452,6 +476,8 @@ class FullyShard:
         if not self._coll:
             out.copy_(u.full_grad)
             work = None
+        elif self.xdp is not None:
+            work = self.xdp.reduce_scatter(u.grad_slot, u.shard_numel, out)
         else:
             work = comm.reduce_scatter_into(out, u.full_grad, group=self.group, async_op=True)
         self._rs_inflight.append((u, work, out, first, direct))

@@ -117,3 +117,96 @@ class XgmiZero:
     def close(self):
         self.rs.close()
         self.ag.close()
+
+
+class XgmiFsdp:
+    """FSDP (ZeRO-3) unit collectives on the copy engines (`FullyShard(dp_comm="xgmi-dma")`).
+
+    * all-gather of a unit: after a barrier, pull every peer's shard of the unit from its shared
+      parameter-shard buffer straight into this rank's gathered unit buffer (own shard: a local
+      copy on the same side stream);
+    * reduce-scatter of a unit's gradient: the backward writes the unit's full gradient into one of
+      `nslots` slots of a shared gradient pool; after a barrier every rank pulls its slice of the
+      slot from each peer and sums it locally; a second barrier ("every peer has pulled from this
+      slot") releases the slot, and the backward that next writes into it waits for that event.
+
+    A parameter shard needs no release barrier (its owner next updates it only after the unit's
+    reduce-scatter barrier, which every rank reaches after its own gathers of the unit)."""
+
+    def __init__(self, group, device, nslots: int = 4, timeout_s: float = None):
+        self.device = torch.device(device)
+        self.ag = XgmiCommunicator(group, capacity_bytes=4096, device=self.device, gather_engine="dma",
+                                   timeout_s=timeout_s)
+        self.rs = XgmiCommunicator(group, capacity_bytes=4096, device=self.device, gather_engine="dma",
+                                   timeout_s=timeout_s)
+        from ..utils import comm as _comm
+
+        _comm.register_xgmi_health(self.ag)
+        _comm.register_xgmi_health(self.rs)
+        self.world, self.rank = self.ag.world, self.ag.rank
+        self.ag_stream = torch.cuda.Stream(device=self.device)
+        self.rs_stream = torch.cuda.Stream(device=self.device)
+        self.nslots = nslots
+        self._shard_slot = None
+        self._pool = None
+
+    def alloc_shards(self, numel: int, dtype) -> torch.Tensor:
+        esz = torch.empty((), dtype=dtype).element_size()
+        raw, self._shard_slot = self.ag.alloc_shared(max(16, numel * esz))
+        return raw[: numel * esz].view(dtype)
+
+    def alloc_grad_pool(self, slot_numel: int, dtype):
+        esz = torch.empty((), dtype=dtype).element_size()
+        self.slot_numel = (slot_numel + 7) // 8 * 8
+        raw, self._pool_slot = self.rs.alloc_shared(self.nslots * self.slot_numel * esz)
+        self._pool = raw[: self.nslots * self.slot_numel * esz].view(dtype)
+        self._free = [None] * self.nslots  # event: every peer pulled from the slot
+        self._next = 0
+
+    def grad_buffer(self, numel: int):
+        """(view of the next pool slot, slot index); the current stream waits until every peer has
+        finished pulling the slot's previous contents."""
+        k = self._next
+        self._next = (k + 1) % self.nslots
+        ev = self._free[k]
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            self._free[k] = None
+        o = k * self.slot_numel
+        return self._pool[o:o + numel], k
+
+    def gather(self, full: torch.Tensor, shard_off: int, n: int, own: torch.Tensor) -> _EventWork:
+        esz = full.element_size()
+        st = self.ag_stream
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            self.ag.signal_wait()
+            full[self.rank * n:(self.rank + 1) * n].copy_(own)
+            nbytes = [0 if r == self.rank else n * esz for r in range(self.world)]
+            self.ag.pull(self._shard_slot, full, [shard_off * esz] * self.world, nbytes,
+                         [r * n * esz for r in range(self.world)])
+            ev = torch.cuda.Event()
+            ev.record(st)
+        return _EventWork(ev, self.device)
+
+    def reduce_scatter(self, k: int, n: int, out: torch.Tensor) -> _EventWork:
+        esz = self._pool.element_size()
+        base = k * self.slot_numel
+        st = self.rs_stream
+        st.wait_stream(torch.cuda.current_stream(self.device))  # the unit's gradient is written
+        with torch.cuda.stream(st):
+            self.rs.signal_wait()
+            scratch = torch.empty(self.world * n, dtype=self._pool.dtype, device=self.device)
+            nbytes = [0 if r == self.rank else n * esz for r in range(self.world)]
+            self.rs.pull(self._pool_slot, scratch, [(base + self.rank * n) * esz] * self.world, nbytes,
+                         [r * n * esz for r in range(self.world)])
+            self.rs.reduce_pulled(out, scratch, self._pool[base + self.rank * n:base + (self.rank + 1) * n])
+            self.rs.signal_wait()  # every peer has pulled from this slot: it may be rewritten
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self._free[k] = ev
+        return _EventWork(ev, self.device)
+
+    def check(self, sync: bool = True):
+        self.ag.check(sync)
+        self.rs.check(sync)

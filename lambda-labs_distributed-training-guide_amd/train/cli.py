@@ -99,10 +99,11 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                    help="debugging: log the tensors holding NaN/inf -- gradients after every backward (grad), "
                         "parameters after every update (param) or both (on); each check syncs the device")
     g.add_argument("--bucket-mb", default=256, type=int, help="gradient bucket size for DDP/ZeRO")
-    if chapter == "02":
+    if chapter in ("02", "04", "05", "07"):
         g.add_argument("--dp-comm", default="rccl", choices=["rccl", "xgmi-dma"],
-                       help="ZeRO bucket collectives: RCCL, or copy-engine pulls between the ranks' shared flat "
-                            "buffers over xGMI (one node; no CU time under the overlapped backward/forward)")
+                       help="ZeRO / FSDP collectives: RCCL, or copy-engine pulls between the ranks' shared shard / "
+                            "gradient buffers over xGMI (one node; no CU time under the overlapped compute)")
+    if chapter == "02":
         g.add_argument("--dp-mode", default="zero", choices=["ddp", "zero"],
                        help="zero: sharded optimizer (reference's ZeroRedundancyOptimizer); ddp: replicated")
     g.add_argument("--activation-checkpointing", default="on" if chapter == "05" else "off", choices=["on", "off"])

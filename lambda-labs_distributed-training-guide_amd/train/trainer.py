@@ -206,7 +206,10 @@ def _build(args, chapter, device, world):
                             min_num_params=getattr(args, "numel_to_wrap", 100_000_000), device=device,
                             reshard_after_forward=args.reshard_after_forward == "on",
                             cpu_offload=cpu_offload, offload_params=offload_params, seed=args.seed,
-                            replicate_group=replicate_group, grad_ring=ring)
+                            replicate_group=replicate_group, grad_ring=ring,
+                            dp_comm=getattr(args, "dp_comm", "rccl") if device.type == "cuda" else "rccl")
+        if getattr(engine, "xdp", None) is not None:
+            LOGGER.info("FSDP collectives: copy-engine pulls over xGMI (shared shard buffers, gradient pool)")
         style = "sharded"
     else:
         if world == 1 or (pp > 1 and dp_size == 1):
