@@ -959,7 +959,9 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
                           bf16x8 (&dsf)[2]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
-    if constexpr (CAUSAL) {
+    // causal: only a half where some query precedes this wave's last key needs the mask (the
+    // mask used to run on every half of every item: 16 v_cmp + 16 v_cndmask + 16 s_nop each)
+    if (CAUSAL && wkey0 + 31 > qsu + koff_c) {
       const int lim = key - koff_c - qsu - 4 * h;  // query row qsu + acc_row < key - koff_c is masked
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = acc_row0(i) < lim ? 0.f : s[i];
@@ -1020,6 +1022,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     pipeline_reads<4 * ND, 2, 3>();
     __builtin_amdgcn_sched_barrier(0);
   };
+
   auto run_item = [&](int it, int buf) {
     if constexpr (QB == 64) compute64(it, buf);
     else compute(it, buf);
