@@ -88,6 +88,11 @@ def parse(argv=None):
     ap.add_argument("--sweep-steps", type=int, default=3)
     ap.add_argument("--sweep-other-dp-comm", type=int, default=1,
                     help="1: the bucket sweep also times ZeRO on the other --dp-comm transport")
+    # The xGMI diagnostics (the direct-peer library's collective rows and ZeRO over the copy
+    # engines) run in a CHILD job launched by rank 0 after the timed region: a first contact of
+    # IPC-mapped peer memory with a machine must not be able to take the measured run down.
+    ap.add_argument("--xgmi-child", type=int, default=1)
+    ap.add_argument("--diag-only", default="", choices=["", "xgmi"], help=argparse.SUPPRESS)
     # reference-mode throughput: this many extra steps under the reference's synchronising
     # LocalTimer phases (outside the timed region); 0 = off
     ap.add_argument("--ref-steps", type=int, default=3)
@@ -319,7 +324,7 @@ def bucket_sweep(args, torch, dist, device, world, rank, cuda):
     B, S = args.batch_size, args.seq_len
     runs = [(mb, args.dp_comm) for mb in sizes]
     other = "xgmi-dma" if args.dp_comm == "rccl" else "rccl"
-    if cuda and args.parallel == "zero" and args.sweep_other_dp_comm:
+    if cuda and args.parallel == "zero" and args.sweep_other_dp_comm and (other == "rccl" or not args.xgmi_child):
         runs.append((args.bucket_mb, other))  # the other ZeRO transport at the default bucket size
     for mb, dpc in runs:
         try:
@@ -401,7 +406,7 @@ def fsdp_mem_one_rank(args):
     """Valley / peak of ONE rank of an --fsdp-mem-world-rank FSDP job on this GPU: a child process
     (tools/fsdp_mem_one_rank.py) runs rank 0 with a fake process group for the other ranks --
     exact allocations, meaningless numerics (validated against real W = 1/2/4 runs,
-    profiles/r3_s22/).  Returns the child's JSON record, or None if it failed."""
+    profiles/r3/s22/).  Returns the child's JSON record, or None if it failed."""
     cmd = [sys.executable, os.path.join(ROOT, "tools", "fsdp_mem_one_rank.py"), "--world", str(args.fsdp_mem_world),
            "--model", args.fsdp_mem_model, "--batch", str(args.fsdp_mem_batch), "--seq", str(args.fsdp_mem_seq),
            "--numel-to-wrap", str(args.numel_to_wrap), "--steps", str(max(2, args.fsdp_mem_steps))]
@@ -449,7 +454,7 @@ def collective_sweep(args, torch, dist, device, world, cuda):
             out.append({"op": op, "mib": mib, "us": round(dt * 1e6, 1),
                         "busbw_gbs": round((n * esz) / dt / 1e9 * factor, 4)})
         del x, shard, full
-    if cuda and 1 < world <= 8:
+    if cuda and 1 < world <= 8 and not args.xgmi_child:
         out.extend(_xgmi_sweep(torch, dist, device, world, cuda, [s for s in sizes if s <= 256]))
     return out
 
@@ -495,6 +500,46 @@ def _xgmi_sweep(torch, dist, device, world, cuda, sizes):
             except Exception:
                 pass
     return rows
+
+
+def xgmi_child_diag(args, world):
+    """Rank 0: `torchrun --nproc-per-node world bench.py --diag-only xgmi ...` as a child job on the
+    same GPUs; returns its JSON record (or an error record).  The child times the xGMI library's
+    all-gather / reduce-scatter (pull kernels and copy engines) and a ZeRO step over the copy
+    engines at this run's config."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+           "--gpus", str(world), "--diag-only", "xgmi", "--model", args.model, "--batch-size", str(args.batch_size),
+           "--seq-len", str(args.seq_len), "--bucket-mb", str(args.bucket_mb), "--coll-sweep-mb", args.coll_sweep_mb,
+           "--sweep-steps", str(args.sweep_steps), "--tunableop", args.tunableop, "--parallel", args.parallel]
+    if args.backend:
+        cmd += ["--backend", args.backend]
+    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+            "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE", "NCCL_DEBUG", "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "xgmi diagnostic child timed out (420 s)"}
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"xgmi diagnostic child exited {r.returncode}", "stderr_tail": r.stderr[-600:]}
+    return json.loads(lines[-1])
+
+
+def xgmi_diag_main(args, torch, dist, device, world, rank, cuda):
+    """--diag-only xgmi (the child job): xGMI collective rows + a ZeRO step on the copy engines."""
+    out = {"collectives": _xgmi_sweep(torch, dist, device, world, cuda,
+                                      [int(s) for s in args.coll_sweep_mb.split(",") if s.strip() and int(s) <= 256])}
+    if args.parallel == "zero":
+        a2 = argparse.Namespace(**vars(args))
+        a2.bucket_sweep_mb, a2.sweep_other_dp_comm, a2.dp_comm = str(args.bucket_mb), 0, "xgmi-dma"
+        out["zero_step"] = bucket_sweep(a2, torch, dist, device, world, rank, cuda)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
 
 
 def _load_rccl_module():
@@ -580,6 +625,8 @@ def main(argv=None):
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     pg_world = dist.get_world_size() if dist.is_initialized() else 1
     torch.manual_seed(0)
+    if args.diag_only == "xgmi":
+        return xgmi_diag_main(args, torch, dist, device, world, rank, cuda)
 
     res = throughput_phase(args, torch, dist, device, world, rank, cuda)
     gc.collect()
@@ -590,6 +637,14 @@ def main(argv=None):
     sweep = None
     if multi and args.bucket_sweep_mb and args.parallel in ("ddp", "zero") and args.tp == 1:
         sweep = bucket_sweep(args, torch, dist, device, world, rank, cuda)
+    xgmi_diag = None
+    if multi and cuda and args.xgmi_child and world <= 8:
+        gc.collect()
+        torch.cuda.empty_cache()
+        dist.barrier()
+        if rank == 0:
+            xgmi_diag = xgmi_child_diag(args, world)
+        dist.barrier()
     mem = None
     if args.fsdp_mem_steps > 0:
         mem = fsdp_memory_phase(args, torch, dist, device, world, rank, cuda)
@@ -679,6 +734,8 @@ def main(argv=None):
             rec["collectives"] = coll
         if sweep is not None:
             rec["bucket_sweep"] = sweep
+        if xgmi_diag is not None:
+            rec["xgmi_diag"] = xgmi_diag
         if multi and backend == "nccl":
             rec["rccl"] = _load_rccl_module().diagnose(rccl_log)
             rec["rccl"]["preset_applied"] = rccl_applied

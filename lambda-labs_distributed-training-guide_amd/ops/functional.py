@@ -26,8 +26,8 @@ ops = torch.ops.dtg
 # DTG_LINEAR_BWD=tn the backward hands hipBLASLt explicit transposed copies (one streaming
 # pass each through csrc/kernels/transpose.hip); "native" keeps the strided forms; "auto"
 # transposes W for every dX and dY, X only for dW of layers whose output is at least as wide as
-# their input.  Measured on MI355X (Llama-3-8B, b16 x s1024, profiles/r1_s15_*): native 24.0k,
-# auto 25.4k, tn 25.4k tok/s; round 2 with every layout's shapes tuned (profiles/r2_s32/bench_*.log):
+# their input.  Measured on MI355X (Llama-3-8B, b16 x s1024, profiles/r1/s15_*): native 24.0k,
+# auto 25.4k, tn 25.4k tok/s; round 2 with every layout's shapes tuned (profiles/r2/s32/bench_*.log):
 # native 24.3k, auto 27.0k, tn 27.0-27.1k -- "tn" is the default.
 _LINEAR_BWD = os.environ.get("DTG_LINEAR_BWD", "tn")
 _TN_MIN_TOKENS = 4096

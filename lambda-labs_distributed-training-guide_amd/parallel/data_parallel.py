@@ -156,7 +156,7 @@ class DataParallel:
         import math
 
         sp = self.space
-        # adamw_t_ tile width (64 x TC tiles; DTG_ADAMT_TC = 64 | 128 | 256; 128 measured fastest, profiles/r3_s07)
+        # adamw_t_ tile width (64 x TC tiles; DTG_ADAMT_TC = 64 | 128 | 256; 128 measured fastest, profiles/r3/s07)
         self._wt_tc = int(os.environ.get("DTG_ADAMT_TC", "128"))
         rows_desc, slots, toff, tile0 = [], {}, 0, 0
         for i in range(len(sp.names)):
@@ -174,7 +174,7 @@ class DataParallel:
             # No W^T (norm weights, a vocabulary that is not a multiple of 8): updated as full
             # [*, TC] rows plus one short row (within the flat buffer's 16-element padding), so
             # every tile is full -- one [1, n] row would leave 63 of a tile's 64 rows idle
-            # (a 157k x 3072 embedding took the update from 8 to 16 ms, profiles/r3_s10).
+            # (a 157k x 3072 embedding took the update from 8 to 16 ms, profiles/r3/s10).
             n8 = (n + 7) // 8 * 8
             full, rem = divmod(n8, self._wt_tc)
             if full:

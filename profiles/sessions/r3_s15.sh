@@ -12,7 +12,7 @@ grep "done" $O/tune.log
 cp tunableop/tunableop_results_partial.csv $O/table_cold_all.csv
 python tools/merge_tunableop.py $O/table_cold_all.csv $O/cold_all.csv || exit 1
 cp tunableop/tunableop_results_partial.csv $O/table_cold3.csv
-python tools/merge_tunableop.py $O/table_cold3.csv profiles/r3_s14/cold.csv || exit 1
+python tools/merge_tunableop.py $O/table_cold3.csv profiles/r3/s14/cold.csv || exit 1
 for i in 1 2; do
   for v in base cold3 cold_all; do
     if [ $v = base ]; then unset DTG_TUNABLEOP_TABLE; else export DTG_TUNABLEOP_TABLE=$O/table_$v.csv; fi

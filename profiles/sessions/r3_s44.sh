@@ -1,6 +1,6 @@
 #!/bin/bash
 # colsum (RMSNorm weight-gradient column sums) on a 256-workgroup grid: norm tests, then the
-# kernel's time in a profiled bench step (compare profiles/r3_s40: 65 launches, 1.17 ms).
+# kernel's time in a profiled bench step (compare profiles/r3/s40: 65 launches, 1.17 ms).
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=$GRAFT_REPO_ROOT/gpurun_out/r3_s44
 mkdir -p $O

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Embedding-backward (dtg::embedding_bwd_) timing at the 8B shapes: TP 1, TP 8 (7/8 of the ids
-out of shard, -1), and one token covering 3/4 of the batch (profiles/r2_s39/emb_bench.jsonl)."""
+out of shard, -1), and one token covering 3/4 of the batch (profiles/r2/s39/emb_bench.jsonl)."""
 import json
 import os
 import sys

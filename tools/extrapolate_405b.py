@@ -57,7 +57,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--net-gbs", type=float, default=50.0, help="ASSUMED inter-node bandwidth per GPU (GB/s)")
     ap.add_argument("--xgmi-gbs", type=float, default=300.0, help="ASSUMED RCCL intra-node bus bandwidth (GB/s)")
-    ap.add_argument("--host-gbs", type=float, default=347.0, help="host AdamW GB/s (profiles/r2_s15_host_adamw.log)")
+    ap.add_argument("--host-gbs", type=float, default=347.0, help="host AdamW GB/s (profiles/r2/s15_host_adamw.log)")
     ap.add_argument("--world", type=int, default=64)
     ap.add_argument("--per-node", type=int, default=8)
     a = ap.parse_args()

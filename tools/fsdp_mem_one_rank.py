@@ -9,7 +9,7 @@ same allocations and frees in the same order as on a real W-GPU node -- and garb
 which this tool never reports.  It fills the reference's W = 8 memory row
 (`/root/reference/04-fully-sharded-data-parallel/README.md:271-333`) with a measurement instead
 of the planner's prediction, and is checked against the real multi-rank runs at W = 1, 2, 4
-(`profiles/r2_fsdp_memory_and_host_adamw.md`, `profiles/r3_s07/`).
+(`profiles/r2/fsdp_memory_and_host_adamw.md`, `profiles/r3/s07/`).
 
     python tools/fsdp_mem_one_rank.py --world 8 [--model llama-2-7b --batch 10 --seq 1024]
 """

@@ -57,7 +57,7 @@ def _worker(shapes_file, results_file, max_tuning_ms, rotating_mb=0):
     # Compare every candidate's output with the default kernel's and drop the ones that differ:
     # without this TunableOp ranks on time alone, and one hipBLASLt solution for GPT-2's batched
     # attention-score GEMM (tn_1024_1024_64_B_96) returned values of order 1e33 -- NaN losses
-    # (found by tools/check_tunableop.py, profiles/r2_s35/).
+    # (found by tools/check_tunableop.py, profiles/r2/s35/).
     # format "atol_rtol" (PyTorch 2.10): bf16 outputs of two correct kernels differ by rounding
     # (a few ulps of values ~sqrt(K)); a broken one is off by orders of magnitude
     os.environ.setdefault("PYTORCH_TUNABLEOP_NUMERICAL_CHECK", "1e-1_5e-2")
