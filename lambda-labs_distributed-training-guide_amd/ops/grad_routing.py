@@ -7,7 +7,35 @@ Functions compute a weight gradient straight into `main_grad` -- the first contr
 step writes (`out=`), later ones (tied embeddings, gradient accumulation) add -- and return
 None to autograd.  Parameters without `main_grad` get an ordinary gradient.
 """
+import os
+
 import torch
+
+# Weight-gradient GEMMs on a side stream (DTG_DW_STREAM=1).  In a backward the dX GEMMs and the
+# streaming kernels between them (norm / SwiGLU / attention backward, transposes) form the
+# critical path; every dW GEMM hangs off it and is needed only by the gradient collective or the
+# optimizer.  Issued on a second stream, the dW GEMMs can fill the chip while the critical path
+# runs bandwidth-bound kernels.  Operands are recorded on the side stream (the caching allocator
+# does not reuse them early); consumers of the gradients join the stream first (join_dw).
+_DW_STREAM = os.environ.get("DTG_DW_STREAM", "0") == "1"
+_dw_streams = {}
+
+
+def dw_stream(device):
+    s = _dw_streams.get(device)
+    if s is None:
+        s = _dw_streams[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def join_dw(device=None):
+    """The current stream waits for every weight-gradient GEMM issued so far."""
+    if not _dw_streams:
+        return
+    for dev, s in _dw_streams.items():
+        if device is None or torch.device(device) == dev:
+            torch.cuda.current_stream(dev).wait_stream(s)
+
 
 # When an engine owns the loss (it back-propagates the loss with an implicit gradient of 1 and
 # folds any scaling into the optimizer's grad_scale), the fused loss head writes the lm_head
@@ -106,7 +134,17 @@ def route_weight_grad_mm(param, a, b, a_t=None, b_t=None):
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return lhs @ rhs
-    if _fresh(param):
+    if _DW_STREAM and mg.is_cuda:
+        s = dw_stream(mg.device)
+        s.wait_stream(torch.cuda.current_stream(mg.device))
+        with torch.cuda.stream(s):
+            if _fresh(param):
+                torch.mm(lhs, rhs, out=mg)
+            else:
+                mg.addmm_(lhs, rhs)
+        for t in (lhs, rhs):
+            t.record_stream(s)
+    elif _fresh(param):
         torch.mm(lhs, rhs, out=mg)
     else:
         mg.addmm_(lhs, rhs)

@@ -40,7 +40,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.adamw import adamw_step
-from ..ops.grad_routing import reset_grad_state, set_direct_loss_grad
+from ..ops.grad_routing import join_dw, reset_grad_state, set_direct_loss_grad
 from ..utils import comm
 
 ALIGN = 16
@@ -459,6 +459,7 @@ class FullyShard:
         if u.rs_launched:
             return
         u.rs_launched = True
+        join_dw(self.device)  # weight-gradient GEMMs on the side stream (DTG_DW_STREAM)
         # zero the padding / never-written params so the reduce-scatter sums only real grads
         for i, p in enumerate(u.params):
             if not getattr(p, "_dtg_grad_written", False):
@@ -644,6 +645,7 @@ class FullyShard:
         ok = False
         try:
             loss.backward()
+            join_dw(self.device)
             self.accum_count += 1
             self.finish_grad_sync()
             ok = True

@@ -2,7 +2,7 @@
 
 TunableOp ranks candidates on time; one pinned hipBLASLt solution for GPT-2's batched
 attention-score GEMM returned values of order 1e33 and turned chapter 01's loss into NaN
-(profiles/r2_s35/).  tools/check_tunableop.py rebuilds each row's operands and compares the
+(profiles/r2/s35/).  tools/check_tunableop.py rebuilds each row's operands and compares the
 table's kernel with an f32 product.  It runs in a child process so that enabling TunableOp does
 not change the GEMM solutions of the other tests in this session.
 """
