@@ -1,0 +1,233 @@
+// Weight-gradient GEMM with both operands token-major: C[M, N] = A^T B (+ C), A = dY [K, M],
+// B = X [K, N], K = tokens.  (SURVEY K-list: the Linear backward; VERDICT r3 "next round" #6.)
+//
+// Why it exists: a Linear layer's dW = dY^T X reduces over the token dimension, which is the
+// STRIDED dimension of both row-major activations.  hipBLASLt runs this "NT" layout 25-40 %
+// slower than the K-contiguous "TN" one (csrc/kernels/transpose.hip), so the default backward
+// transposes dY and X first (12.7 ms/step of transposes at the 8B shape, plus the transposed
+// writes of swiglu_bwd_t; profiles/r3/s46/step_roofline.md).  gfx950 reads an MN-major LDS
+// tile straight into MFMA operand order with ds_read_b64_tr_b16, so this kernel consumes the
+// token-major tiles as they are: no transpose pass, no transposed copies.
+//
+// Structure (one 256 x 256 output tile per 512-thread workgroup, 8 waves as 2 (M) x 4 (N),
+// 128 x 64 outputs per wave = 4 x 2 accumulators of v_mfma_f32_32x32x16_bf16):
+//  * K-tiles of 64 token rows.  Each K-tile of A and of B is a [64][256] bf16 image (512-B
+//    rows, 32 KB) filled by global_load_lds_dwordx4 -- LDS-DMA, no VGPR staging -- two stages
+//    (128 KB of the 160 KB LDS), the load of tile t+1 in flight while tile t is consumed;
+//  * the image is XOR-swizzled in 64-B units by (row & 3) (written through a pre-swizzled
+//    global SOURCE address: the DMA's LDS destination is lane-linear), so one tr-read's
+//    half-wave (4 rows x 64 B) covers all 64 banks once;
+//  * operand fragments by two ds_read_b64_tr_b16 each (k-order {4h..4h+3, 8+4h..}: the same
+//    permutation on both operands, so the dot product is unchanged);
+//  * raw s_barrier + explicit counted waits (a __syncthreads() would drain the DMA in flight);
+//    all LDS in one __shared__ array (a second object makes hipcc wait vmcnt(0) per ds_read);
+//  * workgroup -> tile map: XCD-bijective remap, then bands of GM tile rows so the 32
+//    workgroups resident on one XCD share A and B panels in its L2.
+//  * epilogue: f32 accumulators -> C (bf16 or f32), optionally C += (addmm_ semantics).
+#include "common.h"
+
+namespace dtg {
+namespace dwg {
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int ROWB = 512;                 // bytes per k-row of a tile image (BM == BN == 256)
+constexpr int TILE_BYTES = BK * ROWB;     // 32 KB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;  // 128 KB
+constexpr int GM = 4;                     // tile rows per band of the workgroup order
+
+// Byte offset of logical 16-byte chunk `ch` (0..31) of k-row `row` in a tile image.
+__device__ __forceinline__ int img_off(int row, int ch) { return row * ROWB + 16 * (ch ^ ((row & 3) << 2)); }
+
+__device__ __forceinline__ bf16x8 tr_frag(const char* base, int oa) {
+  const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + oa));
+  const i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + oa + 8 * ROWB));
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const i16x8 ab = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, ab);
+}
+
+// Lane offset (k-step 0) of the transposed fragment of columns cb .. cb+31 of an image.
+__device__ __forceinline__ int frag_off(int cb) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane & 15, g = lane >> 4;
+  const int q = i >> 2, p = i & 3;
+  const int ch = ((cb + 16 * (g & 1)) >> 3) + (p >> 1);
+  return img_off(4 * (g >> 1) + q, ch) + 8 * (p & 1);
+}
+
+// One 16-byte-per-lane LDS-DMA: lane l's 16 bytes from `gsrc` land at LDS byte lds_dst + 16 l.
+// Inline asm, so that hipcc does not see an LDS write in flight: with the builtin it waits
+// vmcnt(0) before the first ds_read of every K-tile (it cannot tell the staged buffer from the
+// one being read) and the prefetch never overlaps the MFMAs.  The waits are counted by hand.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+// Issue the LDS-DMA of one K-tile (rows k0 .. k0+63, columns c0 .. c0+255) of a token-major
+// operand into the image at `img`: 32 wave-instructions of 1 KB (two k-rows), 4 per wave.
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ src, int64_t ld, int64_t k0, int64_t c0,
+                                      uint32_t img) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 4 * w + i;
+    const int row = 2 * j + (lane >> 5);
+    const int lc = (lane & 31) ^ ((row & 3) << 2);  // logical chunk this lane's 16 B belong to
+    const uint16_t* g = src + (k0 + row) * ld + c0 + 8 * lc;
+    glds16(g, __builtin_amdgcn_readfirstlane(img + 1024 * j));
+  }
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Workgroup id -> (tile row, tile col): XCD-bijective remap (consecutive ids land on one XCD),
+// then bands of GM tile rows walked column by column.
+__device__ __forceinline__ void tile_of(int tm_n, int tn_n, int& tm, int& tn) {
+  const int nwg = tm_n * tn_n, orig = blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  const int per_band = GM * tn_n;
+  const int band = wgid / per_band;
+  const int first = band * GM;
+  const int rows = tm_n - first < GM ? tm_n - first : GM;
+  const int in = wgid - band * per_band;
+  tm = first + in % rows;
+  tn = in / rows;
+}
+
+template <bool OUT_F32, bool ACCUM>
+__global__ __launch_bounds__(512) void dw_gemm_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                      const uint16_t* __restrict__ B, int64_t ldb,
+                                                      void* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  int tm, tn;
+  tile_of(M / BM, N / BN, tm, tn);
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;  // 2 (M) x 4 (N)
+
+  int oa[4], ob[2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) oa[mt] = frag_off(128 * wr + 32 * mt);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) ob[nt] = frag_off(64 * wc + 32 * nt);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+
+  const int nk = K / BK;
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
+  stage(A, lda, 0, m0, lds0);
+  stage(B, ldb, 0, n0, lds0 + TILE_BYTES);
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) {
+      const uint32_t nxt = lds0 + ((t + 1) & 1) * STAGE_BYTES;
+      stage(A, lda, (int64_t)(t + 1) * BK, m0, nxt);
+      stage(B, ldb, (int64_t)(t + 1) * BK, n0, nxt + TILE_BYTES);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's DMA of tile t has landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();  // ... and every wave's
+    const char* ia = cur;
+    const char* ib = cur + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 fa[4], fb[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) fb[nt] = tr_frag(ib + 16 * s * ROWB, ob[nt]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) fa[mt] = tr_frag(ia + 16 * s * ROWB, oa[mt]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(fa[mt], fb[nt], acc[mt][nt]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();  // every wave is done reading `cur`: the next DMA may refill it
+  }
+
+  // epilogue: acc[mt][nt][r] = C[m0 + 128 wr + 32 mt + row(r)][n0 + 64 wc + 32 nt + (lane & 31)]
+  const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + 128 * wr + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t n = n0 + 64 * wc + 32 * nt + col;
+        float v = acc[mt][nt][r];
+        if constexpr (OUT_F32) {
+          float* c = reinterpret_cast<float*>(C) + m * ldc + n;
+          if constexpr (ACCUM) v += *c;
+          *c = v;
+        } else {
+          uint16_t* c = reinterpret_cast<uint16_t*>(C) + m * ldc + n;
+          if constexpr (ACCUM) v += bf2f(*c);
+          *c = f2bf(v);
+        }
+      }
+}
+
+}  // namespace dwg
+
+// c (=|+=) a^T @ b;  a: [K, M], b: [K, N] (token-major, unit column stride), c: [M, N].
+// Shapes must be tile multiples (M, N % 256, K % 64); callers fall back to hipBLASLt otherwise.
+void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool accumulate) {
+  DTG_CHECK_CUDA_BF16(a);
+  DTG_CHECK_CUDA_BF16(b);
+  DTG_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
+            "dw_gemm_: c must be a bf16 or f32 GPU tensor");
+  DTG_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "dw_gemm_: 2-D operands");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  DTG_CHECK(b.size(0) == K && c.size(0) == M && c.size(1) == N, "dw_gemm_: shape mismatch");
+  DTG_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "dw_gemm_: unit column stride required");
+  DTG_CHECK(M % dwg::BM == 0 && N % dwg::BN == 0 && K % dwg::BK == 0 && K > 0,
+            "dw_gemm_: M, N must be multiples of 256 and K of 64 (got ", M, ", ", N, ", ", K, ")");
+  DTG_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+            "dw_gemm_: operands must be 16-byte aligned rows");
+  DTG_CHECK(K < (int64_t(1) << 31) && M * N < (int64_t(1) << 40), "dw_gemm_: too large");
+  const int64_t tiles = (M / dwg::BM) * (N / dwg::BN);
+  DTG_CHECK(tiles < (int64_t(1) << 31), "dw_gemm_: too many tiles");
+  const c10::DeviceGuard g(a.device());
+  const dim3 grid((unsigned)tiles), block(512);
+  const bool f32 = c.scalar_type() == at::kFloat;
+#define DTG_DWG_LAUNCH(F, ACC)                                                                              \
+  dwg::dw_gemm_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b), b.stride(0), \
+                                                            c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K)
+  if (f32) {
+    if (accumulate) DTG_DWG_LAUNCH(true, true); else DTG_DWG_LAUNCH(true, false);
+  } else {
+    if (accumulate) DTG_DWG_LAUNCH(false, true); else DTG_DWG_LAUNCH(false, false);
+  }
+#undef DTG_DWG_LAUNCH
+  DTG_LAUNCH_CHECK();
+}
+
+TORCH_LIBRARY_IMPL(dtg, CUDA, m) { m.impl("dw_gemm_", &dw_gemm_); }
+
+}  // namespace dtg

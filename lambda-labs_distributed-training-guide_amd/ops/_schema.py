@@ -49,6 +49,8 @@ _DEFS = [
     # source offset, rows, cols, destination offset, first 64 x 64 tile); `mats_host` = its CPU copy
     "transpose_mats_(Tensor x, Tensor(a!) out, Tensor mats, Tensor mats_host, int ntiles) -> ()",
     "embedding_bwd_(Tensor(a!) out, Tensor ids, Tensor dy) -> ()",
+    # weight-gradient GEMM over token-major operands: c (=|+=) a^T @ b, a [K, M], b [K, N]
+    "dw_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()",
     # FlashAttention-2-style varlen with explicit per-sequence key ranges (disjoint), causal mask
     # bottom-right aligned: context parallelism's local query chunks over gathered key prefixes
     "flash_attn_varlen_fwd(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens_q, Tensor k_start, Tensor k_len, "
