@@ -396,6 +396,15 @@ def swiglu_bwd_t(dh, gu):
     return dgu, dgu.t().contiguous(), swiglu_fwd(gu).t().contiguous()
 
 
+def swiglu_bwd_h(dh, gu):
+    return swiglu_bwd(dh, gu), swiglu_fwd(gu)
+
+
+def dw_gemm_(a, b, c, accumulate):
+    r = a.float().t() @ b.float()
+    c.copy_((r + c.float()) if accumulate else r)
+
+
 def transpose2d(x):
     return x.t().contiguous()
 
@@ -420,5 +429,6 @@ for _name, _fn in list(globals().items()):
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "adamw_t_", "flash_attn_fwd", "flash_attn_bwd",
         "flash_attn_bwd_qkv", "transpose2d", "transpose_mats_", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
         "flash_attn_varlen_bwd", "flash_attn_fwd_drop", "flash_attn_bwd_drop", "flash_attn_bwd_qkv_drop",
+        "swiglu_bwd_h", "dw_gemm_",
     ):
         LIB.impl(_name, _fn, "CPU")

@@ -51,6 +51,8 @@ _DEFS = [
     "embedding_bwd_(Tensor(a!) out, Tensor ids, Tensor dy) -> ()",
     # weight-gradient GEMM over token-major operands: c (=|+=) a^T @ b, a [K, M], b [K, N]
     "dw_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()",
+    # SwiGLU backward that also returns h = silu(g) * u (token-major operand of dW_down)
+    "swiglu_bwd_h(Tensor dh, Tensor gu) -> (Tensor, Tensor)",
     # FlashAttention-2-style varlen with explicit per-sequence key ranges (disjoint), causal mask
     # bottom-right aligned: context parallelism's local query chunks over gathered key prefixes
     "flash_attn_varlen_fwd(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens_q, Tensor k_start, Tensor k_len, "

@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import grad_routing as _gr
-from .grad_routing import route_embedding_grad, route_param_grad, route_weight_grad_mm
+from .grad_routing import route_embedding_grad, route_param_grad, route_weight_grad_hand, route_weight_grad_mm
 
 ops = torch.ops.dtg
 
@@ -31,6 +31,17 @@ ops = torch.ops.dtg
 # native 24.3k, auto 27.0k, tn 27.0-27.1k -- "tn" is the default.
 _LINEAR_BWD = os.environ.get("DTG_LINEAR_BWD", "tn")
 _TN_MIN_TOKENS = 4096
+# DTG_DW_GEMM=1: weight gradients by the hand-written token-major GEMM (csrc/kernels/dw_gemm.hip)
+# on dY and X as they are -- no transposes, and the MLP backward writes dgu and h row-major
+# (swiglu_bwd_h) instead of dgu, dgu^T and h^T.  Shapes that are not 256 x 256 x 64 tile
+# multiples keep the hipBLASLt path.
+_DW_GEMM = os.environ.get("DTG_DW_GEMM", "0") == "1"
+
+
+def _dw_hand_ok(w, *ts):
+    return (_DW_GEMM and w.shape[0] % 256 == 0 and w.shape[1] % 256 == 0
+            and all(t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.shape[0] % 64 == 0
+                    and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in ts))
 
 
 def _tn_ok(*ts):
@@ -75,7 +86,9 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy, _wt(w).t()) if dx_tn else torch.mm(dy, w)
         if ctx.needs_input_grad[1]:
-            if dw_tn and _tn_ok(dy):
+            if _dw_hand_ok(w, dy, x):
+                dw = route_weight_grad_hand(w, dy, x)
+            elif dw_tn and _tn_ok(dy):
                 dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
             else:
                 dw = route_weight_grad_mm(w, dy, x)
@@ -105,7 +118,9 @@ class _LinearBias(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy, _wt(w).t()) if dx_tn else torch.mm(dy, w)
         if ctx.needs_input_grad[1]:
-            if dw_tn and _tn_ok(dy):
+            if _dw_hand_ok(w, dy, x):
+                dw = route_weight_grad_hand(w, dy, x)
+            elif dw_tn and _tn_ok(dy):
                 dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
             else:
                 dw = route_weight_grad_mm(w, dy, x)
@@ -378,7 +393,16 @@ class _SwiGLUMLP(torch.autograd.Function):
         dy = dy.contiguous()
         dx_tn, dw_tn = _bwd_layout(x, w_gu)
         fused = dw_tn and _tn_ok(dy, gu) and gu.stride(0) == gu.shape[1]
+        hand = _dw_hand_ok(w_down, dy, x, gu) and _dw_hand_ok(w_gu)
         dh = torch.mm(dy, _wt(w_down).t()) if dx_tn else torch.mm(dy, w_down)
+        if hand:
+            dgu, h = ops.swiglu_bwd_h(dh, gu)
+            del dh
+            dw_down = route_weight_grad_hand(w_down, dy, h)
+            del h
+            dx = torch.mm(dgu, _wt(w_gu).t()) if dx_tn else torch.mm(dgu, w_gu)
+            dw_gu = route_weight_grad_hand(w_gu, dgu, x)
+            return dx, dw_gu, dw_down, None
         if fused:
             dgu, dgu_t, h_t = ops.swiglu_bwd_t(dh, gu)
             del dh

@@ -121,6 +121,28 @@ def notify_param(param):
     _mark(param)
 
 
+def route_weight_grad_hand(param, a, b):
+    """Weight gradient a^T @ b by the token-major hand GEMM (torch.ops.dtg.dw_gemm_, no
+    transposes), straight into main_grad (accumulating after the first micro-batch)."""
+    mg = getattr(param, "main_grad", None)
+    if mg is None:
+        out = torch.empty(a.shape[1], b.shape[1], dtype=a.dtype, device=a.device)
+        torch.ops.dtg.dw_gemm_(a, b, out, False)
+        return out
+    acc = not _fresh(param)
+    if _DW_STREAM and mg.is_cuda:
+        s = dw_stream(mg.device)
+        s.wait_stream(torch.cuda.current_stream(mg.device))
+        with torch.cuda.stream(s):
+            torch.ops.dtg.dw_gemm_(a, b, mg, acc)
+        for t in (a, b):
+            t.record_stream(s)
+    else:
+        torch.ops.dtg.dw_gemm_(a, b, mg, acc)
+    _mark(param)
+    return None
+
+
 def route_weight_grad_mm(param, a, b, a_t=None, b_t=None):
     """Weight gradient a^T @ b (a: [T, out], b: [T, in]) into main_grad without a temporary.
 

@@ -55,3 +55,55 @@ def test_dw_gemm_rejects_untiled_shapes(cuda):
     c = torch.empty(300, 256, device="cuda", dtype=torch.bfloat16)
     with pytest.raises(RuntimeError, match="multiples of 256"):
         torch.ops.dtg.dw_gemm_(a, b, c, False)
+
+
+def _train(hand, accum=2):
+    from dtg.models import build_model, resolve_config
+    from dtg.ops import functional as F_
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+
+    F_._DW_GEMM = hand
+    real = F_.route_weight_grad_hand
+    calls = [0]
+
+    def counting(*a, **k):
+        calls[0] += 1
+        return real(*a, **k)
+
+    F_.route_weight_grad_hand = counting
+    try:
+        cfg = resolve_config("llama-tiny-d128")
+        torch.manual_seed(0)
+        model = build_model(cfg, device=torch.device("cuda"))
+        eng = DataParallel(model, mode="single")
+        opt = FlatAdamW(eng, lr=1e-3)
+        g = torch.Generator().manual_seed(0)
+        losses = []
+        for _ in range(3):
+            ids = torch.randint(0, cfg.vocab_size, (8, 128), generator=g).cuda()
+            opt.zero_grad()
+            for j, mb in enumerate(ids.chunk(accum)):
+                ctx = eng.no_sync() if j < accum - 1 else torch.enable_grad()
+                with ctx:
+                    out = model(input_ids=mb, labels=mb)
+                    eng.backward(out.loss)
+            opt.step()
+            losses.append(out.loss.item())
+        torch.cuda.synchronize()
+        return {n: p.detach().float().cpu() for n, p in model.named_parameters()}, losses, calls[0]
+    finally:
+        F_._DW_GEMM = False
+        F_.route_weight_grad_hand = real
+
+
+def test_dw_gemm_in_llama_backward(cuda):
+    """DTG_DW_GEMM path (hand dW GEMM + swiglu_bwd_h) trains like the hipBLASLt TN path:
+    every projection's dW goes through the hand kernel, with gradient accumulation."""
+    ref, ref_losses, n0 = _train(False)
+    got, losses, n1 = _train(True)
+    assert n0 == 0 and n1 > 0
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) < 2e-2 * abs(b), (losses, ref_losses)
+    for n, v in ref.items():
+        rel = ((got[n] - v).norm() / v.norm().clamp_min(1e-12)).item()
+        assert rel < 1e-2, (n, rel)
