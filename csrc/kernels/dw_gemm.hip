@@ -111,6 +111,33 @@ __device__ __forceinline__ void tile_of(int tm_n, int tn_n, int& tm, int& tn) {
   tn = in / rows;
 }
 
+// acc[mt][nt][r] = C[m0 + 128 wr + 32 mt + row(r)][n0 + 64 wc + 32 nt + (lane & 31)]
+template <bool OUT_F32, bool ACCUM>
+__device__ __forceinline__ void store_tile(const f32x16 (&acc)[4][2], void* __restrict__ C, int64_t ldc, int64_t m0,
+                                           int64_t n0, int wr, int wc) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + 128 * wr + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t n = n0 + 64 * wc + 32 * nt + col;
+        float v = acc[mt][nt][r];
+        if constexpr (OUT_F32) {
+          float* c = reinterpret_cast<float*>(C) + m * ldc + n;
+          if constexpr (ACCUM) v += *c;
+          *c = v;
+        } else {
+          uint16_t* c = reinterpret_cast<uint16_t*>(C) + m * ldc + n;
+          if constexpr (ACCUM) v += bf2f(*c);
+          *c = f2bf(v);
+        }
+      }
+}
+
 template <bool OUT_F32, bool ACCUM>
 __global__ __launch_bounds__(512) void dw_gemm_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                       const uint16_t* __restrict__ B, int64_t ldb,
@@ -169,27 +196,93 @@ __global__ __launch_bounds__(512) void dw_gemm_kernel(const uint16_t* __restrict
     barrier();  // every wave is done reading `cur`: the next DMA may refill it
   }
 
-  // epilogue: acc[mt][nt][r] = C[m0 + 128 wr + 32 mt + row(r)][n0 + 64 wc + 32 nt + (lane & 31)]
-  const int h = lane >> 5, col = lane & 31;
+  store_tile<OUT_F32, ACCUM>(acc, C, ldc, m0, n0, wr, wc);
+}
+
+// Variant 2: the same tile, images and fragments, pipelined by k-step ("phase") instead of by
+// K-tile.  A K-tile's 64 rows are four quarters of 16 rows (A 8 KB + B 8 KB, one LDS-DMA
+// wave-instruction of each per wave).  Phase (t, s), s = 0..3:
+//   1. read the fragments of k-step s of tile t (retired by the previous phase's wait+barrier);
+//   2. issue the DMA of quarter s of tile t+1 into the other buffer (its rows were last read
+//      four phases ago, before that phase's barrier);
+//   3. s_waitcnt vmcnt(6): this wave's DMA of the quarter the NEXT phase reads has landed (three
+//      quarters stay in flight);
+//   4. barrier (every wave's has), lgkmcnt(0), 8 MFMAs of k-step s.
+// The fragment reads of a phase issue behind the previous phase's MFMAs, so the matrix pipe
+// never waits on LDS at a K-tile seam (variant 1 drains it twice per K-tile).
+__device__ __forceinline__ void stage_quarter(const uint16_t* __restrict__ src, int64_t ld, int64_t k0, int64_t c0,
+                                              uint32_t img, int q) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = 8 * q + w;  // wave-instruction j of the tile: rows 2j, 2j + 1
+  const int row = 2 * j + (lane >> 5);
+  const int lc = (lane & 31) ^ ((row & 3) << 2);
+  glds16(src + (k0 + row) * ld + c0 + 8 * lc, __builtin_amdgcn_readfirstlane(img + 1024 * j));
+}
+
+template <bool OUT_F32, bool ACCUM>
+__global__ __launch_bounds__(512) void dw_gemm_v2_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                         const uint16_t* __restrict__ B, int64_t ldb,
+                                                         void* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  int tm, tn;
+  tile_of(M / BM, N / BN, tm, tn);
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;
+
+  int oa[4], ob[2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) oa[mt] = frag_off(128 * wr + 32 * mt);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) ob[nt] = frag_off(64 * wc + 32 * nt);
+
+  f32x16 acc[4][2];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + 128 * wr + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int64_t n = n0 + 64 * wc + 32 * nt + col;
-        float v = acc[mt][nt][r];
-        if constexpr (OUT_F32) {
-          float* c = reinterpret_cast<float*>(C) + m * ldc + n;
-          if constexpr (ACCUM) v += *c;
-          *c = v;
-        } else {
-          uint16_t* c = reinterpret_cast<uint16_t*>(C) + m * ldc + n;
-          if constexpr (ACCUM) v += bf2f(*c);
-          *c = f2bf(v);
-        }
+      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+
+  const int nk = K / BK;
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    stage_quarter(A, lda, 0, m0, lds0, q);
+    stage_quarter(B, ldb, 0, n0, lds0 + TILE_BYTES, q);
+  }
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // quarter 0 of tile 0
+  barrier();
+  for (int t = 0; t < nk; ++t) {
+    const char* ia = smem + (t & 1) * STAGE_BYTES;
+    const char* ib = ia + TILE_BYTES;
+    const uint32_t nxt = lds0 + ((t + 1) & 1) * STAGE_BYTES;
+    const bool more = t + 1 < nk;
+    const int64_t k1 = (int64_t)(t + 1) * BK;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 fa[4], fb[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) fb[nt] = tr_frag(ib + 16 * s * ROWB, ob[nt]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) fa[mt] = tr_frag(ia + 16 * s * ROWB, oa[mt]);
+      if (more) {
+        stage_quarter(A, lda, k1, m0, nxt, s);
+        stage_quarter(B, ldb, k1, n0, nxt + TILE_BYTES, s);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(fa[mt], fb[nt], acc[mt][nt]);
+    }
+  }
+  store_tile<OUT_F32, ACCUM>(acc, C, ldc, m0, n0, wr, wc);
 }
 
 }  // namespace dwg
@@ -216,9 +309,19 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const c10::DeviceGuard g(a.device());
   const dim3 grid((unsigned)tiles), block(512);
   const bool f32 = c.scalar_type() == at::kFloat;
-#define DTG_DWG_LAUNCH(F, ACC)                                                                              \
-  dwg::dw_gemm_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b), b.stride(0), \
-                                                            c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K)
+  // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline); read per call (A/B knob)
+  const char* ve = std::getenv("DTG_DWG_VARIANT");
+  const int variant = ve ? std::atoi(ve) : 2;
+#define DTG_DWG_LAUNCH(F, ACC)                                                                                    \
+  do {                                                                                                            \
+    if (variant == 1)                                                                                             \
+      dwg::dw_gemm_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b), b.stride(0), \
+                                                                c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K); \
+    else                                                                                                          \
+      dwg::dw_gemm_v2_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),          \
+                                                                   b.stride(0), c.data_ptr(), c.stride(0), (int)M, \
+                                                                   (int)N, (int)K);                                \
+  } while (0)
   if (f32) {
     if (accumulate) DTG_DWG_LAUNCH(true, true); else DTG_DWG_LAUNCH(true, false);
   } else {

@@ -14,8 +14,11 @@ def _ref(a, b):
 
 @pytest.mark.parametrize("K,M,N", [(64, 256, 256), (1024, 512, 768), (4096, 1024, 256), (192, 2560, 512)])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
-def test_dw_gemm_matches_f32(cuda, K, M, N, out_dtype):
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_dw_gemm_matches_f32(cuda, K, M, N, out_dtype, variant, monkeypatch):
     import dtg.ops  # noqa: F401
+
+    monkeypatch.setenv("DTG_DWG_VARIANT", variant)
 
     g = torch.Generator(device="cuda").manual_seed(K + M + N)
     a = torch.randn(K, M, device="cuda", generator=g).to(torch.bfloat16)

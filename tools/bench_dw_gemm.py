@@ -3,7 +3,8 @@
 Linear backward runs today, on the Llama-3-8B decoder's dW shapes.
 
 Variants per shape (dW = dY^T X, dY [T, out], X [T, in], bf16, f32 accumulation):
-  * hand          dtg::dw_gemm_ on the token-major operands as they are (no transposes);
+  * hand          dtg::dw_gemm_ on the token-major operands as they are (no transposes),
+                  k-step pipeline (variant 2); hand_v1 the K-tile pipeline (variant 1);
   * hand_acc      the same, accumulating into the gradient (addmm_ semantics);
   * tn_gemm       hipBLASLt on pre-transposed, K-contiguous operands (the GEMM alone);
   * tn_total      transpose dY + transpose X + tn_gemm (what the default backward pays);
@@ -70,17 +71,29 @@ def main():
         x = torch.randn(T, n_in, device=dev, dtype=torch.bfloat16, generator=g)
         dyt, xt = dy.t().contiguous(), x.t().contiguous()
         out = torch.empty(n_out, n_in, device=dev, dtype=torch.bfloat16)
-        torch.ops.dtg.dw_gemm_(dy, x, out, False)
         ref = dy.float().t() @ x.float()
-        err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
+        errs = {}
+        for v in ("1", "2"):
+            os.environ["DTG_DWG_VARIANT"] = v
+            out.fill_(float("nan"))
+            torch.ops.dtg.dw_gemm_(dy, x, out, False)
+            errs[v] = ((out.float() - ref).abs().max() / ref.abs().max()).item()
+        err = max(errs.values())
         out2 = out.clone()
         torch.ops.dtg.dw_gemm_(dy, x, out2, True)
         err_acc = ((out2.float() - 2 * ref).abs().max() / (2 * ref).abs().max()).item()
         del ref
         flop = 2.0 * T * n_out * n_in
+        def hand(v, acc=False):
+            def fn():
+                os.environ["DTG_DWG_VARIANT"] = v
+                torch.ops.dtg.dw_gemm_(dy, x, out, acc)
+            return fn
+
         variants = {
-            "hand": lambda: torch.ops.dtg.dw_gemm_(dy, x, out, False),
-            "hand_acc": lambda: torch.ops.dtg.dw_gemm_(dy, x, out, True),
+            "hand": hand("2"),
+            "hand_v1": hand("1"),
+            "hand_acc": hand("2", True),
             "tn_gemm": lambda: torch.mm(dyt, xt.t(), out=out),
             "tn_total": lambda: torch.mm(torch.ops.dtg.transpose2d(dy), torch.ops.dtg.transpose2d(x).t(), out=out),
             "nt": lambda: torch.mm(dy.t(), x, out=out),
