@@ -220,7 +220,13 @@ __device__ __forceinline__ void stage_quarter(const uint16_t* __restrict__ src, 
   glds16(src + (k0 + row) * ld + c0 + 8 * lc, __builtin_amdgcn_readfirstlane(img + 1024 * j));
 }
 
-template <bool OUT_F32, bool ACCUM>
+// PP (variant 3): the 8-phase GEMM template's ping-pong on top -- two barriers per phase
+// (reads + DMA | barrier | MFMAs at raised priority | barrier) and the M-half wave group wr = 1
+// one barrier behind wr = 0, so on every SIMD (waves w and w + 4) one wave issues its MFMAs
+// while the other reads its fragments.  Data hazards are still covered: a quarter is retired
+// (vmcnt + barrier) two barriers before any wave of either group reads it, and a buffer row is
+// refilled >= 6 barriers after its last read completed.
+template <bool OUT_F32, bool ACCUM, bool PP>
 __global__ __launch_bounds__(512) void dw_gemm_v2_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          void* __restrict__ C, int64_t ldc, int M, int N, int K) {
@@ -254,6 +260,7 @@ __global__ __launch_bounds__(512) void dw_gemm_v2_kernel(const uint16_t* __restr
   }
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // quarter 0 of tile 0
   barrier();
+  if (PP && wr == 1) barrier();  // the stagger (wave-uniform branch)
   for (int t = 0; t < nk; ++t) {
     const char* ia = smem + (t & 1) * STAGE_BYTES;
     const char* ib = ia + TILE_BYTES;
@@ -276,12 +283,18 @@ __global__ __launch_bounds__(512) void dw_gemm_v2_kernel(const uint16_t* __restr
       }
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (PP) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(fa[mt], fb[nt], acc[mt][nt]);
+      if constexpr (PP) {
+        __builtin_amdgcn_s_setprio(0);
+        barrier();
+      }
     }
   }
+  if (PP && wr == 0) barrier();  // equal barrier counts for both groups
   store_tile<OUT_F32, ACCUM>(acc, C, ldc, m0, n0, wr, wc);
 }
 
@@ -309,7 +322,7 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const c10::DeviceGuard g(a.device());
   const dim3 grid((unsigned)tiles), block(512);
   const bool f32 = c.scalar_type() == at::kFloat;
-  // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline); read per call (A/B knob)
+  // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline) | 3 (k-step + ping-pong); read per call
   const char* ve = std::getenv("DTG_DWG_VARIANT");
   const int variant = ve ? std::atoi(ve) : 2;
 #define DTG_DWG_LAUNCH(F, ACC)                                                                                    \
@@ -317,10 +330,14 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
     if (variant == 1)                                                                                             \
       dwg::dw_gemm_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b), b.stride(0), \
                                                                 c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K); \
+    else if (variant == 3)                                                                                        \
+      dwg::dw_gemm_v2_kernel<F, ACC, true><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
+                                                                         b.stride(0), c.data_ptr(), c.stride(0),   \
+                                                                         (int)M, (int)N, (int)K);                  \
     else                                                                                                          \
-      dwg::dw_gemm_v2_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),          \
-                                                                   b.stride(0), c.data_ptr(), c.stride(0), (int)M, \
-                                                                   (int)N, (int)K);                                \
+      dwg::dw_gemm_v2_kernel<F, ACC, false><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),   \
+                                                                          b.stride(0), c.data_ptr(), c.stride(0),  \
+                                                                          (int)M, (int)N, (int)K);                 \
   } while (0)
   if (f32) {
     if (accumulate) DTG_DWG_LAUNCH(true, true); else DTG_DWG_LAUNCH(true, false);
