@@ -17,6 +17,11 @@ import torch
 # optimizer.  Issued on a second stream, the dW GEMMs can fill the chip while the critical path
 # runs bandwidth-bound kernels.  Operands are recorded on the side stream (the caching allocator
 # does not reuse them early); consumers of the gradients join the stream first (join_dw).
+# Only PRIVATE operands may be read there -- the TN path's fresh transposed copies: dY itself is
+# also the residual stream's gradient, into which autograd later accumulates the norm branch's
+# contribution IN PLACE on the main stream (InputBuffer steals the buffer), so a delayed GEMM
+# reading dY directly sees the sum (tests/test_dw_stream_gpu.py caught exactly that with a spin
+# ahead of every side-stream GEMM).  Shared operands keep the GEMM on the main stream.
 _DW_STREAM = os.environ.get("DTG_DW_STREAM", "0") == "1"
 _dw_streams = {}
 
@@ -129,16 +134,8 @@ def route_weight_grad_hand(param, a, b):
         out = torch.empty(a.shape[1], b.shape[1], dtype=a.dtype, device=a.device)
         torch.ops.dtg.dw_gemm_(a, b, out, False)
         return out
-    acc = not _fresh(param)
-    if _DW_STREAM and mg.is_cuda:
-        s = dw_stream(mg.device)
-        s.wait_stream(torch.cuda.current_stream(mg.device))
-        with torch.cuda.stream(s):
-            torch.ops.dtg.dw_gemm_(a, b, mg, acc)
-        for t in (a, b):
-            t.record_stream(s)
-    else:
-        torch.ops.dtg.dw_gemm_(a, b, mg, acc)
+    # main stream only: a and b are the shared dY / X (see the side-stream note above)
+    torch.ops.dtg.dw_gemm_(a, b, mg, not _fresh(param))
     _mark(param)
     return None
 
@@ -156,7 +153,7 @@ def route_weight_grad_mm(param, a, b, a_t=None, b_t=None):
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return lhs @ rhs
-    if _DW_STREAM and mg.is_cuda:
+    if _DW_STREAM and mg.is_cuda and a_t is not None and b_t is not None:
         s = dw_stream(mg.device)
         s.wait_stream(torch.cuda.current_stream(mg.device))
         with torch.cuda.stream(s):

@@ -3,12 +3,12 @@
 Every dW GEMM is issued on a second stream; the engines join it before a bucket / unit gradient
 collective, at the end of each backward and so before the optimizer.  With a ~1 ms spin
 enqueued on the side stream ahead of EVERY dW GEMM, a consumer that skipped the join would read
-gradients the GEMM has not written yet: results must stay BIT-identical to the same side-stream
-run without the spins, for the single-device DP engine, DDP and ZeRO over a real RCCL
-communicator (world of one, forced collectives) and FSDP -- and match the in-order run to
-GEMM-solution rounding (the first, bitwise version of this test found a 1e-4 loss difference
-against the in-order run; comparing spin vs no spin on the side stream tells a race from a
-different hipBLASLt solution on the second stream).
+gradients the GEMM has not written yet: results must stay BIT-identical to the in-order run and
+to the side-stream run without spins, for the single-device DP engine, DDP and ZeRO over a real
+RCCL communicator (world of one, forced collectives) and FSDP.  The first version of this test
+found a real race (profiles/r4/s12): GEMMs that read dY directly saw autograd's later in-place
+accumulation of the residual gradient; only private (transposed-copy) operands go to the side
+stream now.
 """
 import pytest
 import torch
@@ -23,10 +23,12 @@ SPIN = 2_000_000
 
 def _train(kind, side, force=False, accum=2, spin=True):
     from dtg.models import build_model, resolve_config
+    from dtg.ops import functional as F_
     from dtg.ops import grad_routing as gr
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
 
     gr._DW_STREAM = side
+    tn_min, F_._TN_MIN_TOKENS = F_._TN_MIN_TOKENS, 0  # the bench's TN path at this small token count
     calls = [0]
     real = gr.dw_stream
     if side:
@@ -76,6 +78,7 @@ def _train(kind, side, force=False, accum=2, spin=True):
     finally:
         gr._DW_STREAM = False
         gr.dw_stream = real
+        F_._TN_MIN_TOKENS = tn_min
 
 
 def _worker(rank, world, kind, spin):
@@ -90,28 +93,18 @@ def _same(a, b):
         assert torch.equal(pb[n], v), n
 
 
-def _close(a, b):
-    pa, la, _ = a
-    pb, lb, _ = b
-    for x, y in zip(la, lb):
-        assert abs(x - y) <= 1e-3 * abs(y), (la, lb)
-    for n, v in pa.items():
-        rel = ((pb[n].float() - v.float()).norm() / v.float().norm().clamp_min(1e-12)).item()
-        assert rel < 1e-2, (n, rel)
-
-
 @pytest.mark.parametrize("kind", ["single", "fsdp"])
 def test_dw_side_stream_race_free(cuda, kind):
-    """A spin ahead of every side-stream GEMM leaves the result bit-identical (a consumer that
-    skipped the join would read unwritten gradients); the side-stream run matches the in-order
-    one to GEMM-solution rounding (hipBLASLt may pick another solution on the second stream)."""
+    """A spin ahead of every side-stream GEMM leaves the result bit-identical to the in-order run
+    (a consumer that skipped the join would read unwritten gradients, an operand mutated on the
+    main stream would be read late)."""
     torch.cuda.set_device(0)
     ref = _train(kind, False)
     fast = _train(kind, True, spin=False)
     slow = _train(kind, True, spin=True)
     assert slow[2] > 0
     _same(fast, slow)
-    _close(ref, slow)
+    _same(ref, slow)
 
 
 @pytest.mark.parametrize("kind", ["ddp", "zero"])
@@ -122,4 +115,4 @@ def test_dw_side_stream_rccl_engines_race_free(cuda, kind):
     slow, = run_distributed(_worker, 1, kind, True, backend="nccl")
     assert slow[2] > 0
     _same(fast, slow)
-    _close(ref, slow)
+    _same(ref, slow)

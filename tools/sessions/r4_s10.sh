@@ -2,7 +2,7 @@
 # r4_s10: weight-gradient GEMMs on a side stream (DTG_DW_STREAM=1): bitwise tests, then an
 # interleaved same-box bench A/B (flagship 1-GPU step, off/on twice).  Kept only if >= 1% faster.
 set -o pipefail
-out=gpurun_out/r4_s12
+out=gpurun_out/r4_s13
 mkdir -p "$out"
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
