@@ -161,13 +161,24 @@ class XgmiFsdp:
         raw, self._pool_slot = self.rs.alloc_shared(self.nslots * self.slot_numel * esz)
         self._pool = raw[: self.nslots * self.slot_numel * esz].view(dtype)
         self._free = [None] * self.nslots  # event: every peer pulled from the slot
+        self._held = [False] * self.nslots  # acquired by a unit whose reduce-scatter is not issued yet
         self._next = 0
 
     def grad_buffer(self, numel: int):
-        """(view of the next pool slot, slot index); the current stream waits until every peer has
-        finished pulling the slot's previous contents."""
-        k = self._next
-        self._next = (k + 1) % self.nslots
+        """(view of the next free pool slot, slot index); the current stream waits until every
+        peer has finished pulling the slot's previous contents.  Slots still held by a unit whose
+        reduce-scatter has not been issued (the root unit holds one from its forward to the end of
+        the backward) are skipped; the choice depends only on program order, so every rank picks
+        the same slot for the same unit."""
+        for _ in range(self.nslots):
+            k = self._next
+            self._next = (k + 1) % self.nslots
+            if not self._held[k]:
+                break
+        else:
+            raise RuntimeError(f"XgmiFsdp: all {self.nslots} gradient-pool slots are held by units whose "
+                               "reduce-scatter has not been issued")
+        self._held[k] = True
         ev = self._free[k]
         if ev is not None:
             torch.cuda.current_stream(self.device).wait_event(ev)
@@ -190,6 +201,7 @@ class XgmiFsdp:
         return _EventWork(ev, self.device)
 
     def reduce_scatter(self, k: int, n: int, out: torch.Tensor) -> _EventWork:
+        self._held[k] = False  # released to the ring; reuse waits for this call's release event
         esz = self._pool.element_size()
         base = k * self.slot_numel
         st = self.rs_stream

@@ -88,7 +88,9 @@ def _fsdp_train(rank, world, dp_comm, resident=False):
 
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    cfg = resolve_config(MODEL)
+    # 6 layers: more units than gradient-pool slots (max_inflight_rs + 3 = 5), so the ring wraps
+    # while the root unit still holds its slot
+    cfg = resolve_config(MODEL, num_hidden_layers=6)
     torch.manual_seed(0)
     model = build_model(cfg, device=dev)
     eng = FullyShard(model, device=dev, dp_comm=dp_comm, cpu_offload=resident, offload_params=not resident)
