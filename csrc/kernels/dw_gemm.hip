@@ -26,6 +26,8 @@
 //  * epilogue: f32 accumulators -> C (bf16 or f32), optionally C += (addmm_ semantics).
 #include "common.h"
 
+#include <type_traits>
+
 namespace dtg {
 namespace dwg {
 
@@ -298,6 +300,114 @@ __global__ __launch_bounds__(512) void dw_gemm_v2_kernel(const uint16_t* __restr
   store_tile<OUT_F32, ACCUM>(acc, C, ldc, m0, n0, wr, wc);
 }
 
+// Variant 4: variant 2's k-step pipeline on a deep ring.  The 160 KB LDS holds 10 quarter
+// slots (A 8 KB + B 8 KB each); quarter Q (global k-rows 16Q .. 16Q+15) lives in slot Q % 10 and
+// its DMA is issued 8 phases before it is read, so 7 quarters stay in flight across every
+// barrier (vmcnt(14)) instead of 3 -- the counters of variant 2 (profiles/r4/s13: 25-33 % of wave
+// cycles in s_waitcnt, matrix pipe 58 % busy) say HBM/L2 latency is not covered.  The DMA uses
+// the saddr form: a wave-uniform 64-bit base in SGPRs (advanced per quarter) plus a per-lane
+// 32-bit offset computed once, instead of 64-bit per-lane address arithmetic per instruction.
+// Hazards: slot (Q + 8) % 10 was last read in phase Q - 2, whose reads every wave retired
+// (lgkmcnt(0)) before barrier Q - 1, which precedes the refill in phase Q; quarter Q + 1 is
+// retired by every wave's vmcnt before barrier Q and read after it.
+constexpr int RING = 10, AHEAD = 8, QBYTES = 16 * ROWB;  // slot: A quarter, then B quarter
+
+__device__ __forceinline__ void glds16_s(uint32_t voff, const void* sbase, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_dst)
+               : "memory");
+}
+
+__device__ __forceinline__ const uint16_t* uniform_ptr(const uint16_t* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  return reinterpret_cast<const uint16_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+template <bool OUT_F32, bool ACCUM>
+__global__ __launch_bounds__(512) void dw_gemm_v4_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                         const uint16_t* __restrict__ B, int64_t ldb,
+                                                         void* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char smem[RING * 2 * QBYTES];  // 160 KB
+  int tm, tn;
+  tile_of(M / BM, N / BN, tm, tn);
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 2, wc = w & 3;
+
+  int oa[4], ob[2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) oa[mt] = frag_off(128 * wr + 32 * mt);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) ob[nt] = frag_off(64 * wc + 32 * nt);
+
+  // this lane's 16 bytes of its wave's DMA instruction of a quarter: quarter row 2w + (lane >> 5)
+  const int qrow = 2 * w + (lane >> 5);
+  const int lc = (lane & 31) ^ ((qrow & 3) << 2);
+  const uint32_t va = (uint32_t)(qrow * lda * 2 + lc * 16);
+  const uint32_t vb = (uint32_t)(qrow * ldb * 2 + lc * 16);
+  const uint16_t* abase = A + m0;  // + 16 Q lda per quarter
+  const uint16_t* bbase = B + n0;
+  const int64_t astep = 16 * lda, bstep = 16 * ldb;
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
+  auto issue = [&](int q) {
+    const uint32_t slot = lds0 + (uint32_t)(q % RING) * (2 * QBYTES) + 1024 * w;
+    glds16_s(va, uniform_ptr(abase + (int64_t)q * astep), __builtin_amdgcn_readfirstlane(slot));
+    glds16_s(vb, uniform_ptr(bbase + (int64_t)q * bstep), __builtin_amdgcn_readfirstlane(slot + QBYTES));
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+
+  const int nq = K / 16;
+  const int pre = nq < AHEAD ? nq : AHEAD;
+  for (int q = 0; q < pre; ++q) issue(q);
+  if (nq > AHEAD) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // quarter 0 (of 8 issued)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  barrier();
+  auto phase = [&](int q, auto steady) {
+    const char* ia = smem + (q % RING) * (2 * QBYTES);
+    const char* ib = ia + QBYTES;
+    bf16x8 fa[4], fb[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) fb[nt] = tr_frag(ib, ob[nt]);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) fa[mt] = tr_frag(ia, oa[mt]);
+    if constexpr (decltype(steady)::value) {
+      issue(q + AHEAD);
+      asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // quarter q + 1 has landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(fa[mt], fb[nt], acc[mt][nt]);
+  };
+  // branch-free steady state (unrolled by two so the next phase's reads can issue behind this
+  // phase's MFMAs), then the drain of the last AHEAD quarters
+  const int steady_end = nq - AHEAD > 0 ? nq - AHEAD : 0;
+  int q = 0;
+  for (; q + 1 < steady_end; q += 2) {
+    phase(q, std::true_type{});
+    phase(q + 1, std::true_type{});
+  }
+  for (; q < steady_end; ++q) phase(q, std::true_type{});
+  for (; q < nq; ++q) phase(q, std::false_type{});
+  store_tile<OUT_F32, ACCUM>(acc, C, ldc, m0, n0, wr, wc);
+}
+
 }  // namespace dwg
 
 // c (=|+=) a^T @ b;  a: [K, M], b: [K, N] (token-major, unit column stride), c: [M, N].
@@ -322,7 +432,8 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const c10::DeviceGuard g(a.device());
   const dim3 grid((unsigned)tiles), block(512);
   const bool f32 = c.scalar_type() == at::kFloat;
-  // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline) | 3 (k-step + ping-pong); read per call
+  // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline) | 3 (k-step + ping-pong) | 4 (k-step,
+  // 10-slot ring, 8 quarters ahead); read per call
   const char* ve = std::getenv("DTG_DWG_VARIANT");
   const int variant = ve ? std::atoi(ve) : 2;
 #define DTG_DWG_LAUNCH(F, ACC)                                                                                    \
@@ -330,6 +441,10 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
     if (variant == 1)                                                                                             \
       dwg::dw_gemm_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b), b.stride(0), \
                                                                 c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K); \
+    else if (variant == 4)                                                                                        \
+      dwg::dw_gemm_v4_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),          \
+                                                                   b.stride(0), c.data_ptr(), c.stride(0),         \
+                                                                   (int)M, (int)N, (int)K);                        \
     else if (variant == 3)                                                                                        \
       dwg::dw_gemm_v2_kernel<F, ACC, true><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
                                                                          b.stride(0), c.data_ptr(), c.stride(0),   \
