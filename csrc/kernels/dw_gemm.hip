@@ -310,7 +310,7 @@ __global__ __launch_bounds__(512) void dw_gemm_v2_kernel(const uint16_t* __restr
 // Hazards: slot (Q + 8) % 10 was last read in phase Q - 2, whose reads every wave retired
 // (lgkmcnt(0)) before barrier Q - 1, which precedes the refill in phase Q; quarter Q + 1 is
 // retired by every wave's vmcnt before barrier Q and read after it.
-constexpr int RING = 10, AHEAD = 8, QBYTES = 16 * ROWB;  // slot: A quarter, then B quarter
+constexpr int QBYTES = 16 * ROWB;  // slot: A quarter, then B quarter
 
 __device__ __forceinline__ void glds16_s(uint32_t voff, const void* sbase, uint32_t lds_dst) {
   unsigned keep;
@@ -327,11 +327,22 @@ __device__ __forceinline__ const uint16_t* uniform_ptr(const uint16_t* p) {
   return reinterpret_cast<const uint16_t*>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 
-template <bool OUT_F32, bool ACCUM>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// KS k-steps (quarters) per phase and barrier; AHEAD quarters in flight; ring of
+// AHEAD + 2 KS slots (the refill of phase p targets the slots read in phase p - 2).
+template <bool OUT_F32, bool ACCUM, int KS, int AHEAD>
 __global__ __launch_bounds__(512) void dw_gemm_v4_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          void* __restrict__ C, int64_t ldc, int M, int N, int K) {
-  __shared__ __attribute__((aligned(1024))) char smem[RING * 2 * QBYTES];  // 160 KB
+  constexpr int RING = AHEAD + 2 * KS;
+  static_assert(RING * 2 * QBYTES <= 160 * 1024, "LDS");
+  static_assert(AHEAD % KS == 0, "whole phases in flight");
+  __shared__ __attribute__((aligned(1024))) char smem[RING * 2 * QBYTES];
   int tm, tn;
   tile_of(M / BM, N / BN, tm, tn);
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
@@ -368,43 +379,49 @@ __global__ __launch_bounds__(512) void dw_gemm_v4_kernel(const uint16_t* __restr
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
-  const int nq = K / 16;
+  const int nq = K / 16;  // a multiple of 4 (K % 64 == 0), so of KS
   const int pre = nq < AHEAD ? nq : AHEAD;
   for (int q = 0; q < pre; ++q) issue(q);
-  if (nq > AHEAD) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // quarter 0 (of 8 issued)
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nq > AHEAD) wait_vm<2 * (AHEAD - KS)>();  // the first phase's quarters have landed
+  else wait_vm<0>();
   barrier();
   auto phase = [&](int q, auto steady) {
-    const char* ia = smem + (q % RING) * (2 * QBYTES);
-    const char* ib = ia + QBYTES;
-    bf16x8 fa[4], fb[2];
+    bf16x8 fa[KS][4], fb[KS][2];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) fb[nt] = tr_frag(ib, ob[nt]);
+    for (int k = 0; k < KS; ++k) {
+      const char* ia = smem + ((q + k) % RING) * (2 * QBYTES);
+      const char* ib = ia + QBYTES;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) fa[mt] = tr_frag(ia, oa[mt]);
+      for (int nt = 0; nt < 2; ++nt) fb[k][nt] = tr_frag(ib, ob[nt]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) fa[k][mt] = tr_frag(ia, oa[mt]);
+    }
     if constexpr (decltype(steady)::value) {
-      issue(q + AHEAD);
-      asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // quarter q + 1 has landed
+#pragma unroll
+      for (int k = 0; k < KS; ++k) issue(q + AHEAD + k);
+      wait_vm<2 * (AHEAD - KS)>();  // the next phase's quarters have landed
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wait_vm<0>();
     }
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int k = 0; k < KS; ++k)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(fa[mt], fb[nt], acc[mt][nt]);
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(fa[k][mt], fb[k][nt], acc[mt][nt]);
   };
-  // branch-free steady state (unrolled by two so the next phase's reads can issue behind this
-  // phase's MFMAs), then the drain of the last AHEAD quarters
-  const int steady_end = nq - AHEAD > 0 ? nq - AHEAD : 0;
+  // branch-free steady state (unrolled by two phases so the next phase's reads can issue behind
+  // this phase's MFMAs), then the drain of the last AHEAD quarters
+  const int steady_end = nq - AHEAD > 0 ? nq - AHEAD : 0;  // a multiple of KS
   int q = 0;
-  for (; q + 1 < steady_end; q += 2) {
+  for (; q + KS < steady_end; q += 2 * KS) {
     phase(q, std::true_type{});
-    phase(q + 1, std::true_type{});
+    phase(q + KS, std::true_type{});
   }
-  for (; q < steady_end; ++q) phase(q, std::true_type{});
-  for (; q < nq; ++q) phase(q, std::false_type{});
+  for (; q < steady_end; q += KS) phase(q, std::true_type{});
+  for (; q < nq; q += KS) phase(q, std::false_type{});
   store_tile<OUT_F32, ACCUM>(acc, C, ldc, m0, n0, wr, wc);
 }
 
@@ -433,7 +450,7 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const dim3 grid((unsigned)tiles), block(512);
   const bool f32 = c.scalar_type() == at::kFloat;
   // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline) | 3 (k-step + ping-pong) | 4 (k-step,
-  // 10-slot ring, 8 quarters ahead); read per call
+  // 10-slot ring, 8 quarters ahead) | 5 (2 k-steps per barrier, 6 quarters ahead); read per call
   const char* ve = std::getenv("DTG_DWG_VARIANT");
   const int variant = ve ? std::atoi(ve) : 2;
 #define DTG_DWG_LAUNCH(F, ACC)                                                                                    \
@@ -442,9 +459,13 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
       dwg::dw_gemm_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b), b.stride(0), \
                                                                 c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K); \
     else if (variant == 4)                                                                                        \
-      dwg::dw_gemm_v4_kernel<F, ACC><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),          \
-                                                                   b.stride(0), c.data_ptr(), c.stride(0),         \
-                                                                   (int)M, (int)N, (int)K);                        \
+      dwg::dw_gemm_v4_kernel<F, ACC, 1, 8><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
+                                                                         b.stride(0), c.data_ptr(), c.stride(0),   \
+                                                                         (int)M, (int)N, (int)K);                  \
+    else if (variant == 5)                                                                                        \
+      dwg::dw_gemm_v4_kernel<F, ACC, 2, 6><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
+                                                                         b.stride(0), c.data_ptr(), c.stride(0),   \
+                                                                         (int)M, (int)N, (int)K);                  \
     else if (variant == 3)                                                                                        \
       dwg::dw_gemm_v2_kernel<F, ACC, true><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
                                                                          b.stride(0), c.data_ptr(), c.stride(0),   \

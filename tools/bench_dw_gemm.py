@@ -6,7 +6,8 @@ Variants per shape (dW = dY^T X, dY [T, out], X [T, in], bf16, f32 accumulation)
   * hand          dtg::dw_gemm_ on the token-major operands as they are (no transposes),
                   k-step pipeline (variant 2); hand_v1 the K-tile pipeline (variant 1); hand_v3
                   the k-step pipeline with the 8-phase template's wave-group ping-pong; hand_v4
-                  the k-step pipeline on a 10-slot LDS ring, 8 quarters in flight;
+                  the k-step pipeline on a 10-slot LDS ring, 8 quarters in flight; hand_v5 the
+                  same ring with 2 k-steps per barrier, 6 quarters in flight;
   * hand_acc      the same, accumulating into the gradient (addmm_ semantics);
   * tn_gemm       hipBLASLt on pre-transposed, K-contiguous operands (the GEMM alone);
   * tn_total      transpose dY + transpose X + tn_gemm (what the default backward pays);
@@ -75,7 +76,7 @@ def main():
         out = torch.empty(n_out, n_in, device=dev, dtype=torch.bfloat16)
         ref = dy.float().t() @ x.float()
         errs = {}
-        for v in ("1", "2", "3", "4"):
+        for v in ("1", "2", "3", "4", "5"):
             os.environ["DTG_DWG_VARIANT"] = v
             out.fill_(float("nan"))
             torch.ops.dtg.dw_gemm_(dy, x, out, False)
@@ -97,6 +98,7 @@ def main():
             "hand_v1": hand("1"),
             "hand_v3": hand("3"),
             "hand_v4": hand("4"),
+            "hand_v5": hand("5"),
             "hand_acc": hand("2", True),
             "tn_gemm": lambda: torch.mm(dyt, xt.t(), out=out),
             "tn_total": lambda: torch.mm(torch.ops.dtg.transpose2d(dy), torch.ops.dtg.transpose2d(x).t(), out=out),
