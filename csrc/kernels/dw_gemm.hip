@@ -113,6 +113,33 @@ __device__ __forceinline__ void tile_of(int tm_n, int tn_n, int& tm, int& tn) {
   tn = in / rows;
 }
 
+// Generic form: wave tile of MT x NT 32x32 accumulators at (row0, col0) of the output.
+template <bool OUT_F32, bool ACCUM, int MT, int NT>
+__device__ __forceinline__ void store_wave(const f32x16 (&acc)[MT][NT], void* __restrict__ C, int64_t ldc, int64_t row0,
+                                           int64_t col0) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = row0 + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t n = col0 + 32 * nt + col;
+        float v = acc[mt][nt][r];
+        if constexpr (OUT_F32) {
+          float* c = reinterpret_cast<float*>(C) + m * ldc + n;
+          if constexpr (ACCUM) v += *c;
+          *c = v;
+        } else {
+          uint16_t* c = reinterpret_cast<uint16_t*>(C) + m * ldc + n;
+          if constexpr (ACCUM) v += bf2f(*c);
+          *c = f2bf(v);
+        }
+      }
+}
+
 // acc[mt][nt][r] = C[m0 + 128 wr + 32 mt + row(r)][n0 + 64 wc + 32 nt + (lane & 31)]
 template <bool OUT_F32, bool ACCUM>
 __device__ __forceinline__ void store_tile(const f32x16 (&acc)[4][2], void* __restrict__ C, int64_t ldc, int64_t m0,
@@ -425,6 +452,101 @@ __global__ __launch_bounds__(512) void dw_gemm_v4_kernel(const uint16_t* __restr
   store_tile<OUT_F32, ACCUM>(acc, C, ldc, m0, n0, wr, wc);
 }
 
+// Variant 6: hipBLASLt's TN geometry on the ring -- 4 waves (2 x 2), one per SIMD, each owning a
+// 128 x 128 sub-tile (4 x 4 accumulators = 256 f32 registers, which the compiler keeps in the
+// accumulation registers): 16 MFMAs per 8 fragments (1 tr-read per MFMA instead of 1.5) and
+// half as many waves meeting at each barrier.  Each wave issues two DMA instructions per operand
+// and quarter (rows 2j, 2j + 1 for j = w, w + 4).
+template <bool OUT_F32, bool ACCUM, int AHEAD>
+__global__ __launch_bounds__(256) void dw_gemm_w4_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                         const uint16_t* __restrict__ B, int64_t ldb,
+                                                         void* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  constexpr int KS = 1, RING = AHEAD + 2 * KS;
+  static_assert(RING * 2 * QBYTES <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[RING * 2 * QBYTES];
+  int tm, tn;
+  tile_of(M / BM, N / BN, tm, tn);
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+
+  int oa[4], ob[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) oa[mt] = frag_off(128 * wr + 32 * mt);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) ob[nt] = frag_off(128 * wc + 32 * nt);
+
+  uint32_t va[2], vb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int qrow = 2 * (w + 4 * i) + (lane >> 5);
+    const int lc = (lane & 31) ^ ((qrow & 3) << 2);
+    va[i] = (uint32_t)(qrow * lda * 2 + lc * 16);
+    vb[i] = (uint32_t)(qrow * ldb * 2 + lc * 16);
+  }
+  const uint16_t* abase = A + m0;
+  const uint16_t* bbase = B + n0;
+  const int64_t astep = 16 * lda, bstep = 16 * ldb;
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
+  auto issue = [&](int q) {
+    const uint32_t slot = lds0 + (uint32_t)(q % RING) * (2 * QBYTES);
+    const uint16_t* ap = uniform_ptr(abase + (int64_t)q * astep);
+    const uint16_t* bp = uniform_ptr(bbase + (int64_t)q * bstep);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t d = slot + 1024 * (w + 4 * i);
+      glds16_s(va[i], ap, __builtin_amdgcn_readfirstlane(d));
+      glds16_s(vb[i], bp, __builtin_amdgcn_readfirstlane(d + QBYTES));
+    }
+  };
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+
+  const int nq = K / 16;
+  const int pre = nq < AHEAD ? nq : AHEAD;
+  for (int q = 0; q < pre; ++q) issue(q);
+  if (nq > AHEAD) wait_vm<4 * (AHEAD - KS)>();
+  else wait_vm<0>();
+  barrier();
+  auto phase = [&](int q, auto steady) {
+    const char* ia = smem + (q % RING) * (2 * QBYTES);
+    const char* ib = ia + QBYTES;
+    bf16x8 fa[4], fb[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) fb[nt] = tr_frag(ib, ob[nt]);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) fa[mt] = tr_frag(ia, oa[mt]);
+    if constexpr (decltype(steady)::value) {
+      issue(q + AHEAD);
+      wait_vm<4 * (AHEAD - KS)>();
+    } else {
+      wait_vm<0>();
+    }
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma(fa[mt], fb[nt], acc[mt][nt]);
+  };
+  const int steady_end = nq - AHEAD > 0 ? nq - AHEAD : 0;
+  int q = 0;
+  for (; q + 1 < steady_end; q += 2) {
+    phase(q, std::true_type{});
+    phase(q + 1, std::true_type{});
+  }
+  for (; q < steady_end; ++q) phase(q, std::true_type{});
+  for (; q < nq; ++q) phase(q, std::false_type{});
+  store_wave<OUT_F32, ACCUM, 4, 4>(acc, C, ldc, m0 + 128 * wr, n0 + 128 * wc);
+}
+
 }  // namespace dwg
 
 // c (=|+=) a^T @ b;  a: [K, M], b: [K, N] (token-major, unit column stride), c: [M, N].
@@ -450,7 +572,8 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const dim3 grid((unsigned)tiles), block(512);
   const bool f32 = c.scalar_type() == at::kFloat;
   // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline) | 3 (k-step + ping-pong) | 4 (k-step,
-  // 10-slot ring, 8 quarters ahead) | 5 (2 k-steps per barrier, 6 quarters ahead); read per call
+  // 10-slot ring, 8 quarters ahead) | 5 (2 k-steps per barrier, 6 quarters ahead)
+  // | 6 (4 waves x 128 x 128, ring 8 ahead); read per call
   const char* ve = std::getenv("DTG_DWG_VARIANT");
   const int variant = ve ? std::atoi(ve) : 2;
 #define DTG_DWG_LAUNCH(F, ACC)                                                                                    \
@@ -462,6 +585,10 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
       dwg::dw_gemm_v4_kernel<F, ACC, 1, 8><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
                                                                          b.stride(0), c.data_ptr(), c.stride(0),   \
                                                                          (int)M, (int)N, (int)K);                  \
+    else if (variant == 6)                                                                                        \
+      dwg::dw_gemm_w4_kernel<F, ACC, 8><<<grid, dim3(256), 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),   \
+                                                                          b.stride(0), c.data_ptr(), c.stride(0),  \
+                                                                          (int)M, (int)N, (int)K);                 \
     else if (variant == 5)                                                                                        \
       dwg::dw_gemm_v4_kernel<F, ACC, 2, 6><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
                                                                          b.stride(0), c.data_ptr(), c.stride(0),   \
