@@ -457,11 +457,12 @@ __global__ __launch_bounds__(512) void dw_gemm_v4_kernel(const uint16_t* __restr
 // accumulation registers): 16 MFMAs per 8 fragments (1 tr-read per MFMA instead of 1.5) and
 // half as many waves meeting at each barrier.  Each wave issues two DMA instructions per operand
 // and quarter (rows 2j, 2j + 1 for j = w, w + 4).
-template <bool OUT_F32, bool ACCUM, int AHEAD>
+template <bool OUT_F32, bool ACCUM, int KS, int AHEAD>
 __global__ __launch_bounds__(256) void dw_gemm_w4_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          void* __restrict__ C, int64_t ldc, int M, int N, int K) {
-  constexpr int KS = 1, RING = AHEAD + 2 * KS;
+  constexpr int RING = AHEAD + 2 * KS;
+  static_assert(AHEAD % KS == 0, "whole phases in flight");
   static_assert(RING * 2 * QBYTES <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[RING * 2 * QBYTES];
   int tm, tn;
@@ -516,15 +517,19 @@ __global__ __launch_bounds__(256) void dw_gemm_w4_kernel(const uint16_t* __restr
   else wait_vm<0>();
   barrier();
   auto phase = [&](int q, auto steady) {
-    const char* ia = smem + (q % RING) * (2 * QBYTES);
-    const char* ib = ia + QBYTES;
-    bf16x8 fa[4], fb[4];
+    bf16x8 fa[KS][4], fb[KS][4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) fb[nt] = tr_frag(ib, ob[nt]);
+    for (int k = 0; k < KS; ++k) {
+      const char* ia = smem + ((q + k) % RING) * (2 * QBYTES);
+      const char* ib = ia + QBYTES;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) fa[mt] = tr_frag(ia, oa[mt]);
+      for (int nt = 0; nt < 4; ++nt) fb[k][nt] = tr_frag(ib, ob[nt]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) fa[k][mt] = tr_frag(ia, oa[mt]);
+    }
     if constexpr (decltype(steady)::value) {
-      issue(q + AHEAD);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) issue(q + AHEAD + k);
       wait_vm<4 * (AHEAD - KS)>();
     } else {
       wait_vm<0>();
@@ -532,18 +537,20 @@ __global__ __launch_bounds__(256) void dw_gemm_w4_kernel(const uint16_t* __restr
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int k = 0; k < KS; ++k)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma(fa[mt], fb[nt], acc[mt][nt]);
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma(fa[k][mt], fb[k][nt], acc[mt][nt]);
   };
   const int steady_end = nq - AHEAD > 0 ? nq - AHEAD : 0;
   int q = 0;
-  for (; q + 1 < steady_end; q += 2) {
+  for (; q + KS < steady_end; q += 2 * KS) {
     phase(q, std::true_type{});
-    phase(q + 1, std::true_type{});
+    phase(q + KS, std::true_type{});
   }
-  for (; q < steady_end; ++q) phase(q, std::true_type{});
-  for (; q < nq; ++q) phase(q, std::false_type{});
+  for (; q < steady_end; q += KS) phase(q, std::true_type{});
+  for (; q < nq; q += KS) phase(q, std::false_type{});
   store_wave<OUT_F32, ACCUM, 4, 4>(acc, C, ldc, m0 + 128 * wr, n0 + 128 * wc);
 }
 
@@ -573,9 +580,9 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const bool f32 = c.scalar_type() == at::kFloat;
   // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline) | 3 (k-step + ping-pong) | 4 (k-step,
   // 10-slot ring, 8 quarters ahead) | 5 (2 k-steps per barrier, 6 quarters ahead)
-  // | 6 (4 waves x 128 x 128, ring 8 ahead); read per call
+  // | 6 (4 waves x 128 x 128, ring 8 ahead) | 7 (6 with 2 k-steps per barrier, 6 ahead); read per call
   const char* ve = std::getenv("DTG_DWG_VARIANT");
-  const int variant = ve ? std::atoi(ve) : 2;
+  const int variant = ve ? std::atoi(ve) : 5;  // the fastest measured (profiles/r4/s15, s16)
 #define DTG_DWG_LAUNCH(F, ACC)                                                                                    \
   do {                                                                                                            \
     if (variant == 1)                                                                                             \
@@ -586,9 +593,13 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
                                                                          b.stride(0), c.data_ptr(), c.stride(0),   \
                                                                          (int)M, (int)N, (int)K);                  \
     else if (variant == 6)                                                                                        \
-      dwg::dw_gemm_w4_kernel<F, ACC, 8><<<grid, dim3(256), 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),   \
+      dwg::dw_gemm_w4_kernel<F, ACC, 1, 8><<<grid, dim3(256), 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),   \
                                                                           b.stride(0), c.data_ptr(), c.stride(0),  \
                                                                           (int)M, (int)N, (int)K);                 \
+    else if (variant == 7)                                                                                        \
+      dwg::dw_gemm_w4_kernel<F, ACC, 2, 6><<<grid, dim3(256), 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b), \
+                                                                             b.stride(0), c.data_ptr(), c.stride(0), \
+                                                                             (int)M, (int)N, (int)K);              \
     else if (variant == 5)                                                                                        \
       dwg::dw_gemm_v4_kernel<F, ACC, 2, 6><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
                                                                          b.stride(0), c.data_ptr(), c.stride(0),   \
