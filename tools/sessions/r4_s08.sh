@@ -6,6 +6,9 @@ set -o pipefail
 out=gpurun_out/r4_s08
 mkdir -p "$out"
 export TMPDIR=/tmp
+timeout -k 10 200 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
+    tests/test_dw_gemm_gpu.py > "$out/pytest_dwg.log" 2>&1 || { tail -40 "$out/pytest_dwg.log"; exit 1; }
+tail -1 "$out/pytest_dwg.log"
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
     tests/test_xgmi_dp_gpu.py -k fsdp > "$out/pytest_xdp.log" 2>&1 || { tail -40 "$out/pytest_xdp.log"; exit 1; }
 tail -1 "$out/pytest_xdp.log"
