@@ -19,9 +19,9 @@ MODEL = "llama-tiny-d128"
 STEPS = 3
 
 
-def _batches(vocab):
+def _batches(vocab, rows=8):
     g = torch.Generator().manual_seed(0)
-    return [torch.randint(0, vocab, (8, 128), generator=g) for _ in range(STEPS)]
+    return [torch.randint(0, vocab, (rows, 128), generator=g) for _ in range(STEPS)]
 
 
 def _train(rank, world, dp_comm, skew=False):
@@ -97,9 +97,10 @@ def _fsdp_train(rank, world, dp_comm, resident=False):
     assert world == 1 or eng.dp_comm == dp_comm
     opt = FlatAdamW(eng, lr=1e-3)
     losses = []
-    for ids in _batches(cfg.vocab_size):
+    for ids in _batches(cfg.vocab_size, rows=16):  # 2 rows per rank at world 8: two micro-batches
         per = ids.shape[0] // world
         mine = ids[rank * per:(rank + 1) * per].to(dev)
+        assert mine.shape[0] >= 2
         opt.zero_grad()
         for j, mb in enumerate(mine.chunk(2)):  # two micro-batches: accumulation into the shard
             if j == 0:
