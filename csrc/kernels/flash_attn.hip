@@ -100,6 +100,14 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// One v_add_f32 that the SLP vectorizer cannot pair into v_pk_add_f32 (a packed f32 add beside
+// MFMAs costs more issue cycles than two single ones: CDNA4 guide, attention rules).
+__device__ __forceinline__ float add1(float a, float b) {
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // Reductions of x over the lane pair (l, l ^ 32): v_permlane32_swap(x, x) leaves x[l & 31] and
 // x[32 + (l & 31)] in its two results on every lane (VALU only; __shfl_xor compiles to
 // ds_bpermute_b32, whose LDS round trip sits on the softmax's dependency chain).  max and +
@@ -419,12 +427,16 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
             s[kt][i] = (acc_row0(i) > lim || acc_row0(i) < llim) ? -INFINITY : s[kt][i];
         }
       }
-      float mx = s[0][0];
+      // Row max and row sum as four independent partial chains (a 32-deep dependent fmax / add
+      // chain per tile otherwise sits on the critical path of the softmax); max is exact in any
+      // order, the sum's reassociation only moves rounding.
+      float mx4[4] = {s[0][0], s[0][1], s[0][2], s[0][3]};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kt][i]);
+        for (int i = (kt == 0 ? 4 : 0); i < 16; ++i) mx4[i & 3] = fmaxf(mx4[i & 3], s[kt][i]);
       }
+      float mx = fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]));
       mx = pair_max(mx) * P.c2;
       if (__builtin_amdgcn_ballot_w64(mx > m + kRescaleThreshold) != 0) {
         const float mn = fmaxf(m, mx);
@@ -435,17 +447,17 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
         m = mn;
       }
       const float mu = (m == -INFINITY) ? 0.f : m;
-      float rs = 0.f;
+      float rs4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = fexp2(__builtin_fmaf(s[kt][i], P.c2, -mu));
           s[kt][i] = p;
-          rs += p;
+          rs4[i & 3] = add1(rs4[i & 3], p);
         }
       }
-      l += rs;  // the softmax normaliser counts every probability, dropped or not
+      l += (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);  // the normaliser counts every probability, dropped or not
       if constexpr (DROP) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) drop_row_half(P.drop, s0, qrow, head, kt0 + 32 * kt, h, s[kt]);
