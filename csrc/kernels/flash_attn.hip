@@ -100,14 +100,6 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// One v_add_f32 that the SLP vectorizer cannot pair into v_pk_add_f32 (a packed f32 add beside
-// MFMAs costs more issue cycles than two single ones: CDNA4 guide, attention rules).
-__device__ __forceinline__ float add1(float a, float b) {
-  float r;
-  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-
 // Reductions of x over the lane pair (l, l ^ 32): v_permlane32_swap(x, x) leaves x[l & 31] and
 // x[32 + (l & 31)] in its two results on every lane (VALU only; __shfl_xor compiles to
 // ds_bpermute_b32, whose LDS round trip sits on the softmax's dependency chain).  max and +
@@ -454,7 +446,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
         for (int i = 0; i < 16; ++i) {
           const float p = fexp2(__builtin_fmaf(s[kt][i], P.c2, -mu));
           s[kt][i] = p;
-          rs4[i & 3] = add1(rs4[i & 3], p);
+          // plain adds (hipcc pairs them into v_pk_add_f32).  An inline-asm v_add_f32 here, to
+          // keep them unpacked, read v_exp_f32 results without the transcendental-use wait
+          // states the compiler inserts only around its own instructions: NaN losses on the GPU
+          // (tools/diag_fsdp_nan.py, profiles/r4/s17).
+          rs4[i & 3] += p;
         }
       }
       l += (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);  // the normaliser counts every probability, dropped or not
