@@ -419,16 +419,15 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
             s[kt][i] = (acc_row0(i) > lim || acc_row0(i) < llim) ? -INFINITY : s[kt][i];
         }
       }
-      // Row max and row sum as four independent partial chains (a 32-deep dependent fmax / add
-      // chain per tile otherwise sits on the critical path of the softmax); max is exact in any
-      // order, the sum's reassociation only moves rounding.
-      float mx4[4] = {s[0][0], s[0][1], s[0][2], s[0][3]};
+      // (Four independent partial max / sum chains instead of one 32-deep chain measured no gain
+      // at the 8B shape and -2 % on rime, profiles/r4/s17: hipcc packs the partial sums into
+      // v_pk_add_f32, and the other wave on the SIMD already fills the chain's latency.)
+      float mx = s[0][0];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-        for (int i = (kt == 0 ? 4 : 0); i < 16; ++i) mx4[i & 3] = fmaxf(mx4[i & 3], s[kt][i]);
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kt][i]);
       }
-      float mx = fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]));
       mx = pair_max(mx) * P.c2;
       if (__builtin_amdgcn_ballot_w64(mx > m + kRescaleThreshold) != 0) {
         const float mn = fmaxf(m, mx);
@@ -439,21 +438,17 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
         m = mn;
       }
       const float mu = (m == -INFINITY) ? 0.f : m;
-      float rs4[4] = {0.f, 0.f, 0.f, 0.f};
+      float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = fexp2(__builtin_fmaf(s[kt][i], P.c2, -mu));
           s[kt][i] = p;
-          // plain adds (hipcc pairs them into v_pk_add_f32).  An inline-asm v_add_f32 here, to
-          // keep them unpacked, read v_exp_f32 results without the transcendental-use wait
-          // states the compiler inserts only around its own instructions: NaN losses on the GPU
-          // (tools/diag_fsdp_nan.py, profiles/r4/s17).
-          rs4[i & 3] += p;
+          rs += p;
         }
       }
-      l += (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);  // the normaliser counts every probability, dropped or not
+      l += rs;  // the softmax normaliser counts every probability, dropped or not
       if constexpr (DROP) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) drop_row_half(P.drop, s0, qrow, head, kt0 + 32 * kt, h, s[kt]);
@@ -967,9 +962,10 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
                           bf16x8 (&dsf)[2]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
-    // causal: only a half where some query precedes this wave's last key needs the mask (the
-    // mask used to run on every half of every item: 16 v_cmp + 16 v_cndmask + 16 s_nop each)
-    if (CAUSAL && wkey0 + 31 > qsu + koff_c) {
+    // causal: the mask runs on every half (branch-free).  Skipping it on halves that need none
+    // (a wave-uniform branch) measured 1 % slower at the 8B shape and 3 % on packed rime rows
+    // (profiles/r4/s17): the branch splits the halves' basic block and with it the schedule.
+    if constexpr (CAUSAL) {
       const int lim = key - koff_c - qsu - 4 * h;  // query row qsu + acc_row < key - koff_c is masked
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = acc_row0(i) < lim ? 0.f : s[i];
