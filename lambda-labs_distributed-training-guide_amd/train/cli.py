@@ -48,7 +48,9 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                        help="with --cpu-offload on: stage each unit's reduced gradient in one of N unit-sized "
                             "pinned host slots consumed by the overlapped host AdamW, instead of a host gradient "
                             "shard for the whole model (saves 2 B/param of host RAM: 101 GB per rank for 405B at "
-                            "W = 8); auto = 4 slots without gradient accumulation, else off; 0 = off")
+                            "W = 8); auto = 4 slots with the HBM-resident parameter layout, and with parameters "
+                            "on the host only when the node's host state would not fit in RAM (profiles/r4/s23); "
+                            "off under gradient accumulation; 0 = off")
     if chapter == "07":
         p.add_argument("--tp", default=8, type=int)
     if chapter in ("06", "07"):

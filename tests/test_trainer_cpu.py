@@ -164,3 +164,25 @@ def test_pp_chapter_runs_and_checkpoint_reshards_to_no_pp(tmp_path):
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "Resuming" in out, out[-3000:]
     assert json.loads((tmp_path / "pp" / "state.json").read_text())["global_step"] == 4
+
+
+def test_offload_grad_ring_auto_policy(monkeypatch):
+    """--offload-grad-ring auto (profiles/r4/s23): on with the HBM-resident parameter layout, off
+    with parameters on the host unless the node's host state would not fit in RAM, off under
+    gradient accumulation."""
+    import types
+
+    import psutil
+    import torch
+
+    from dtg.train.trainer import _grad_ring_auto
+
+    model = torch.nn.Linear(1000, 1000)  # 1.001 M parameters
+    args = types.SimpleNamespace(grad_accum=1)
+    assert _grad_ring_auto(args, model, None, offload_params=False) == 4
+    assert _grad_ring_auto(args, model, None, offload_params=True) == 0  # plenty of host RAM
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setattr(psutil, "virtual_memory", lambda: types.SimpleNamespace(available=50_000_000))
+    assert _grad_ring_auto(args, model, None, offload_params=True) == 4  # 8 ranks x 8 MB > 85 % of 50 MB
+    args.grad_accum = 2
+    assert _grad_ring_auto(args, model, None, offload_params=False) == 0
