@@ -145,14 +145,10 @@ class DataParallel:
         self._wt_buf = None
         self._wt_version = -1
         self._wt_stream = None
-        self._wt_ready = {}  # per-bucket W^T: bucket -> event after its transposes (side stream)
-        # W^T rebuilt per bucket (instead of by the whole-buffer adamw_t_ in step()): ZeRO (each
-        # rank updates 1/W of a bucket: transposes once its all-gather lands) and the in-backward
-        # optimizer (each bucket's update runs on the optimizer stream during the backward: its
-        # transposes follow on that stream)
-        self._wt_per_bucket = self.mode == "zero" or overlap_optimizer
-        if (weight_t and self.space.dtype == torch.bfloat16 and self.space.grad_dtype == torch.bfloat16) or \
-                (weight_t and dev.type == "cpu"):
+        self._wt_ready = {}  # zero: bucket -> event after its W^T transposes (side stream)
+        if (weight_t and not overlap_optimizer
+                and self.space.dtype == torch.bfloat16 and self.space.grad_dtype == torch.bfloat16) or \
+                (weight_t and dev.type == "cpu" and not overlap_optimizer):
             self._build_weight_t()
 
     # ------------------------------------------------------------------ transposed weights
@@ -193,11 +189,10 @@ class DataParallel:
         self._wt_mats = torch.tensor(rows_desc, dtype=torch.long, device=dev)
         self._wt_tiles = tile0
         self._wt_buf = torch.empty(toff, dtype=sp.dtype, device=dev)
-        if self._wt_per_bucket:
+        if self.mode == "zero":
             # ZeRO updates 1/W of every bucket, so adamw_t_ cannot write whole W^T copies; they
             # are rebuilt per bucket the moment its parameter all-gather lands, by one batched
-            # transpose launch on a side stream that runs under the next forward's GEMMs.  The
-            # in-backward optimizer rebuilds a bucket's right after its update, on that stream.
+            # transpose launch on a side stream that runs under the next forward's GEMMs.
             per_b = {}
             for i, (t, rows, cols) in sorted(slots.items()):
                 per_b.setdefault(sp.param_bucket[i].index, []).append((sp.offsets[i], rows, cols, t))
@@ -239,7 +234,7 @@ class DataParallel:
             w = ps[i]
             view.copy_(_F.ops.transpose2d(w) if w.is_cuda else w.t())
         self._wt_version = self.space.param_buf._version
-        if self._wt_per_bucket:
+        if self.mode == "zero":
             self._wt_ready.clear()
             for b in self._wt_valid:
                 self._wt_valid[b] = True
@@ -249,7 +244,7 @@ class DataParallel:
         refresh (the caller then transposes)."""
         if self._wt_buf is None or self.space.param_buf._version != self._wt_version:
             return None
-        if self._wt_per_bucket:
+        if self.mode == "zero":
             b = self.space.param_bucket[i].index
             if not self._wt_valid.get(b, False):
                 return None
@@ -258,22 +253,13 @@ class DataParallel:
                 torch.cuda.current_stream(self.space.param_buf.device).wait_event(ev)
         return self._wt_views.get(i)
 
-    def _transpose_bucket(self, i, work, here: bool = False):
-        """W^T of bucket i's matrices: ZeRO once its all-gather (`work`) has landed; `here`: on
-        the current stream, right behind the bucket's in-backward update."""
-        ent = self._wt_bucket_mats.get(i) if self._wt_buf is not None and self._wt_per_bucket else None
+    def _transpose_bucket(self, i, work):
+        """ZeRO: W^T of bucket i's matrices once its all-gather (`work`) has landed."""
+        ent = self._wt_bucket_mats.get(i) if self._wt_buf is not None and self.mode == "zero" else None
         if ent is None:
             return
         mats_dev, mats_host, ntiles = ent
         st = self._wt_stream
-        if here:
-            torch.ops.dtg.transpose_mats_(self.space.param_buf.data, self._wt_buf, mats_dev, mats_host, ntiles)
-            if self.space.param_buf.is_cuda:
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(self.space.param_buf.device))
-                self._wt_ready[i] = ev
-            self._wt_valid[i] = True
-            return
         if st is None:  # CPU engine (gloo tests): in order
             if work is not None:
                 work.wait()
@@ -359,8 +345,6 @@ class DataParallel:
             self._update_bucket(b, lr, beta1, beta2, eps, wd, scale)
             if self.mode == "zero":
                 self._gather_bucket(b.index)
-            elif self._wt_buf is not None:
-                self._transpose_bucket(b.index, None, here=True)
         b.stepped = True
 
     def _update_bucket(self, b, lr, beta1, beta2, eps, wd, scale):
@@ -452,10 +436,6 @@ class DataParallel:
                                    float(beta1), float(beta2), float(eps), float(weight_decay), int(self.step_count),
                                    float(grad_scale), self.graph_hyper, self._wt_tc)
             self._wt_version = self.space.param_buf._version
-            if self._wt_per_bucket:  # the in-backward optimizer's engine, stepped here instead
-                self._wt_ready.clear()
-                for b in self._wt_valid:
-                    self._wt_valid[b] = True
         else:
             adamw_step(self.space.param_buf, self.space.grad_buf, self.exp_avg, self.exp_avg_sq, lr=lr,
                        step=self.step_count, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,

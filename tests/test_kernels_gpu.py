@@ -284,12 +284,11 @@ def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master, tile_co
             assert torch.equal(pt[d[3]:d[3] + r * c].view(c, r), p[off:off + r * c].view(r, c).t())
 
 
-@pytest.mark.parametrize("engine_mode,overlap", [("single", False), ("single", True)])
-def test_engine_weight_t_bitwise_and_fewer_transposes(cuda, engine_mode, overlap, monkeypatch):
+@pytest.mark.parametrize("engine_mode", ["single"])
+def test_engine_weight_t_bitwise_and_fewer_transposes(cuda, engine_mode, monkeypatch):
     """Llama on the GPU with the TN backward (T = 4096 tokens): persistent W^T written by the
     optimizer gives bitwise the same training as per-backward weight transposes, with 4 fewer
-    transpose launches per layer (+1 for the tied/untied loss-head weight).  overlap: the
-    in-backward optimizer, whose buckets rebuild their W^T on the optimizer stream."""
+    transpose launches per layer (+1 for the tied/untied loss-head weight)."""
     import dtg.ops.functional as F_
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
@@ -301,7 +300,7 @@ def test_engine_weight_t_bitwise_and_fewer_transposes(cuda, engine_mode, overlap
     for wt in (False, True, "again"):  # "again": plain once more, the run-to-run control
         torch.manual_seed(0)
         m = build_model(cfg, device=cuda)
-        eng = DataParallel(m, mode=engine_mode, weight_t=wt is True, overlap_optimizer=overlap)
+        eng = DataParallel(m, mode=engine_mode, weight_t=wt is True)
         opt = FlatAdamW(eng, lr=1e-3)
         calls = [0]
         real = torch.ops.dtg.transpose2d
