@@ -8,8 +8,10 @@ eight ranks already need ~406 GB each for the offloaded training state.
 
 `pinned_zeros` instead allocates ordinary (pageable) host memory of the exact size and
 page-locks it in place with hipHostRegister, so the copy engines DMA straight from / into it
-(`non_blocking=True` copies stay asynchronous).  The registration is dropped when the tensor
-object is collected.  Without a GPU (or if registration fails) the buffer is returned pageable.
+(`non_blocking=True` copies stay asynchronous).  The registration is dropped when the memory
+itself is freed (after the device drains), however many views of it are still around until
+then.  Without a GPU the buffer is returned pageable; if registration fails, from the caching
+allocator.
 """
 from __future__ import annotations
 
@@ -19,22 +21,32 @@ import torch
 
 
 def _unregister(ptr: int) -> None:
+    # Runs when the buffer's STORAGE is freed (the finalizer hangs on the numpy array the storage
+    # keeps alive, not on one tensor object whose views may outlive it).  Drain the device first:
+    # an asynchronous copy still reading / writing the pages must not see them unpinned.
     try:
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
         torch.cuda.cudart().cudaHostUnregister(ptr)
     except Exception:
         pass
 
 
 def pinned_zeros(n: int, dtype: torch.dtype) -> torch.Tensor:
-    t = torch.zeros(int(n), dtype=dtype)
+    n = int(n)
     if n == 0 or not torch.cuda.is_available():
-        return t
+        return torch.zeros(n, dtype=dtype)
+    import numpy as np
+
+    esz = torch.empty((), dtype=dtype).element_size()
+    arr = np.zeros(n * esz, dtype=np.uint8)  # exact size, zero-filled, pageable
+    t = torch.from_numpy(arr).view(dtype)  # shares arr's memory; the storage keeps arr alive
     try:
         rt = torch.cuda.cudart()
-        err = rt.cudaHostRegister(t.data_ptr(), t.numel() * t.element_size(), 0)
+        err = rt.cudaHostRegister(t.data_ptr(), n * esz, 0)
         if int(err) != 0:
             raise RuntimeError(f"hipHostRegister returned {int(err)}")
     except Exception:
-        return torch.zeros(int(n), dtype=dtype, pin_memory=True)  # the caching allocator's path
-    weakref.finalize(t, _unregister, t.data_ptr())
+        return torch.zeros(n, dtype=dtype, pin_memory=True)  # the caching allocator's path
+    weakref.finalize(arr, _unregister, t.data_ptr())
     return t

@@ -19,3 +19,22 @@ def test_pinned_zeros_exact_size_and_async_copies(cuda):
     back.copy_(h, non_blocking=True)
     torch.cuda.synchronize()
     assert torch.equal(back, d)
+
+
+def test_pinned_view_outlives_the_tensor_object(cuda):
+    """The registration belongs to the memory, not to the first tensor object: a view kept after
+    the original tensor is gone is still page-locked (async copies stay DMA), and the pages are
+    unpinned only when the last view is freed."""
+    import gc
+
+    from dtg.utils.pinned import pinned_zeros
+
+    h = pinned_zeros(1 << 20, torch.bfloat16)
+    v = h[4096:8192]
+    del h
+    gc.collect()
+    assert v.is_pinned()
+    d = torch.randn(4096, device=cuda).bfloat16()
+    v.copy_(d, non_blocking=True)
+    torch.cuda.synchronize()
+    assert torch.equal(v.to(cuda), d)
