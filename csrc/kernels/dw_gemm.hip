@@ -692,6 +692,9 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
                 reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
             "dw_gemm_: operands must be 16-byte aligned rows");
   DTG_CHECK(K < (int64_t(1) << 31) && M * N < (int64_t(1) << 40), "dw_gemm_: too large");
+  // per-lane / scalar byte offsets within one K-tile (64 rows) are 32-bit in the ring and
+  // register-staged variants
+  DTG_CHECK(a.stride(0) < (int64_t(1) << 24) && b.stride(0) < (int64_t(1) << 24), "dw_gemm_: row pitch too large");
   const int64_t tiles = (M / dwg::BM) * (N / dwg::BN);
   DTG_CHECK(tiles < (int64_t(1) << 31), "dw_gemm_: too many tiles");
   const c10::DeviceGuard g(a.device());
