@@ -32,7 +32,6 @@ namespace dtg {
 namespace dwg {
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int ROWB = 512;                 // bytes per k-row of a tile image (BM == BN == 256)
@@ -112,33 +111,6 @@ __device__ __forceinline__ void tile_of(int tm_n, int tn_n, int& tm, int& tn) {
   const int in = wgid - band * per_band;
   tm = first + in % rows;
   tn = in / rows;
-}
-
-// Generic form: wave tile of MT x NT 32x32 accumulators at (row0, col0) of the output.
-template <bool OUT_F32, bool ACCUM, int MT, int NT>
-__device__ __forceinline__ void store_wave(const f32x16 (&acc)[MT][NT], void* __restrict__ C, int64_t ldc, int64_t row0,
-                                           int64_t col0) {
-  const int lane = threadIdx.x & 63;
-  const int h = lane >> 5, col = lane & 31;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = row0 + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int64_t n = col0 + 32 * nt + col;
-        float v = acc[mt][nt][r];
-        if constexpr (OUT_F32) {
-          float* c = reinterpret_cast<float*>(C) + m * ldc + n;
-          if constexpr (ACCUM) v += *c;
-          *c = v;
-        } else {
-          uint16_t* c = reinterpret_cast<uint16_t*>(C) + m * ldc + n;
-          if constexpr (ACCUM) v += bf2f(*c);
-          *c = f2bf(v);
-        }
-      }
 }
 
 // acc[mt][nt][r] = C[m0 + 128 wr + 32 mt + row(r)][n0 + 64 wc + 32 nt + (lane & 31)]
@@ -453,225 +425,9 @@ __global__ __launch_bounds__(512) void dw_gemm_v4_kernel(const uint16_t* __restr
   store_tile<OUT_F32, ACCUM>(acc, C, ldc, m0, n0, wr, wc);
 }
 
-// Variant 6: hipBLASLt's TN geometry on the ring -- 4 waves (2 x 2), one per SIMD, each owning a
-// 128 x 128 sub-tile (4 x 4 accumulators = 256 f32 registers, which the compiler keeps in the
-// accumulation registers): 16 MFMAs per 8 fragments (1 tr-read per MFMA instead of 1.5) and
-// half as many waves meeting at each barrier.  Each wave issues two DMA instructions per operand
-// and quarter (rows 2j, 2j + 1 for j = w, w + 4).
-template <bool OUT_F32, bool ACCUM, int KS, int AHEAD>
-__global__ __launch_bounds__(256) void dw_gemm_w4_kernel(const uint16_t* __restrict__ A, int64_t lda,
-                                                         const uint16_t* __restrict__ B, int64_t ldb,
-                                                         void* __restrict__ C, int64_t ldc, int M, int N, int K) {
-  constexpr int RING = AHEAD + 2 * KS;
-  static_assert(AHEAD % KS == 0, "whole phases in flight");
-  static_assert(RING * 2 * QBYTES <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) char smem[RING * 2 * QBYTES];
-  int tm, tn;
-  tile_of(M / BM, N / BN, tm, tn);
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 1, wc = w & 1;
-
-  int oa[4], ob[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) oa[mt] = frag_off(128 * wr + 32 * mt);
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) ob[nt] = frag_off(128 * wc + 32 * nt);
-
-  uint32_t va[2], vb[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int qrow = 2 * (w + 4 * i) + (lane >> 5);
-    const int lc = (lane & 31) ^ ((qrow & 3) << 2);
-    va[i] = (uint32_t)(qrow * lda * 2 + lc * 16);
-    vb[i] = (uint32_t)(qrow * ldb * 2 + lc * 16);
-  }
-  const uint16_t* abase = A + m0;
-  const uint16_t* bbase = B + n0;
-  const int64_t astep = 16 * lda, bstep = 16 * ldb;
-  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
-  auto issue = [&](int q) {
-    const uint32_t slot = lds0 + (uint32_t)(q % RING) * (2 * QBYTES);
-    const uint16_t* ap = uniform_ptr(abase + (int64_t)q * astep);
-    const uint16_t* bp = uniform_ptr(bbase + (int64_t)q * bstep);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint32_t d = slot + 1024 * (w + 4 * i);
-      glds16_s(va[i], ap, __builtin_amdgcn_readfirstlane(d));
-      glds16_s(vb[i], bp, __builtin_amdgcn_readfirstlane(d + QBYTES));
-    }
-  };
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
-
-  const int nq = K / 16;
-  const int pre = nq < AHEAD ? nq : AHEAD;
-  for (int q = 0; q < pre; ++q) issue(q);
-  if (nq > AHEAD) wait_vm<4 * (AHEAD - KS)>();
-  else wait_vm<0>();
-  barrier();
-  auto phase = [&](int q, auto steady) {
-    bf16x8 fa[KS][4], fb[KS][4];
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      const char* ia = smem + ((q + k) % RING) * (2 * QBYTES);
-      const char* ib = ia + QBYTES;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) fb[k][nt] = tr_frag(ib, ob[nt]);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) fa[k][mt] = tr_frag(ia, oa[mt]);
-    }
-    if constexpr (decltype(steady)::value) {
-#pragma unroll
-      for (int k = 0; k < KS; ++k) issue(q + AHEAD + k);
-      wait_vm<4 * (AHEAD - KS)>();
-    } else {
-      wait_vm<0>();
-    }
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < KS; ++k)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma(fa[k][mt], fb[k][nt], acc[mt][nt]);
-  };
-  const int steady_end = nq - AHEAD > 0 ? nq - AHEAD : 0;
-  int q = 0;
-  for (; q + KS < steady_end; q += 2 * KS) {
-    phase(q, std::true_type{});
-    phase(q + KS, std::true_type{});
-  }
-  for (; q < steady_end; q += KS) phase(q, std::true_type{});
-  for (; q < nq; q += KS) phase(q, std::false_type{});
-  store_wave<OUT_F32, ACCUM, 4, 4>(acc, C, ldc, m0 + 128 * wr, n0 + 128 * wc);
-}
-
-// Variant 8: hipBLASLt's own TN structure, transposed through the LDS image: 4 waves (2 x 2), one
-// per SIMD, 128 x 128 outputs each (accumulators in the AGPR file); K-tiles of 64 rows; global
-// loads REGISTER-staged two K-tiles ahead (two sets of 8 + 8 16-byte buffer loads per thread),
-// each set written to one of two LDS images right after the iteration's single barrier; the
-// k-step loop reads the next k-step's fragments while the current one's 16 MFMAs run.  The
-// variants above keep the pipeline depth in LDS (at most 8 quarter-tiles), this one in VGPRs.
-//   iteration t:  barrier | wait for set t%2 (tile t+1) -> ds_write to image (t+1)%2 |
-//                 issue tile t+3 into set t%2 | 4 k-steps of tile t from image t%2
-// Hazards: image (t+1)%2 was last read in iteration t-1 (all its reads retired before this
-// barrier: every wave waits lgkmcnt(0) before its MFMAs and again after its ds_writes); image t%2
-// was written in iteration t-1 before that iteration's lgkmcnt(0), which precedes this barrier.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int64_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
-  const int n = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7fffffff ? 0x7fffffff : bytes));
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo),
-                                           (short)0, n, 0x00020000);
-}
-
-template <bool OUT_F32, bool ACCUM, int NSET>
-__global__ __launch_bounds__(256) void dw_gemm_rs_kernel(const uint16_t* __restrict__ A, int64_t lda,
-                                                         const uint16_t* __restrict__ B, int64_t ldb,
-                                                         void* __restrict__ C, int64_t ldc, int M, int N, int K) {
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];  // 2 x (A image + B image)
-  int tm, tn;
-  tile_of(M / BM, N / BN, tm, tn);
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int tid = threadIdx.x;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 1, wc = w & 1;
-
-  int oa[4], ob[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) oa[mt] = frag_off(128 * wr + 32 * mt);
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) ob[nt] = frag_off(64 * 2 * wc + 32 * nt);
-
-  // this thread's 8 chunks of a K-tile: chunk c = tid + 256 i -> row c / 32 (= tid / 32 + 8 i),
-  // 16-byte column c % 32 (= tid % 32); 32 consecutive threads read one 512-byte row
-  // (rows row0 + 8 i share row & 3, so chunk i's LDS offset is woff + 8 i ROWB -- an immediate --
-  // and its global offset voa + 8 i ld 2 goes in the loads' scalar offset: three VGPRs in all)
-  const int row0 = tid >> 5, ch = tid & 31;
-  const int voa = (int)(row0 * lda * 2 + ch * 16), vob = (int)(row0 * ldb * 2 + ch * 16);
-  const int woff = img_off(row0, ch);
-  const int sa = __builtin_amdgcn_readfirstlane((int)(8 * lda * 2)), sb = __builtin_amdgcn_readfirstlane((int)(8 * ldb * 2));
-  const int nk = K / BK;
-  const int64_t abytes = (int64_t)(BK - 1) * lda * 2 + BM * 2, bbytes = (int64_t)(BK - 1) * ldb * 2 + BN * 2;
-  u32x4 ra[NSET][8], rb[NSET][8];
-  auto load = [&](int t, auto set_c) {
-    constexpr int set = decltype(set_c)::value;
-    const __amdgpu_buffer_rsrc_t rA = rsrc_of(A + (int64_t)t * BK * lda + m0, abytes);
-    const __amdgpu_buffer_rsrc_t rB = rsrc_of(B + (int64_t)t * BK * ldb + n0, bbytes);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      ra[set][i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, voa, i * sa, 0));
-      rb[set][i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, vob, i * sb, 0));
-    }
-  };
-  auto store = [&](int img, auto set_c) {
-    constexpr int set = decltype(set_c)::value;
-    char* ia = smem + img * STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      *reinterpret_cast<u32x4*>(ia + woff + 8 * i * ROWB) = ra[set][i];
-      *reinterpret_cast<u32x4*>(ia + TILE_BYTES + woff + 8 * i * ROWB) = rb[set][i];
-    }
-  };
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
-
-  // prologue: tile 0 -> image 0; tiles 1, 2 in flight in sets 0, 1... (set of tile u = (u + 1) % 2)
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, NSET - 1>;  // NSET == 1: one set, tiles one ahead
-  // iteration t stores the register set holding tile t + 1 into image (t + 1) % 2 and reloads the
-  // set with tile t + 1 + NSET
-  load(0, S0{});
-  store(0, S0{});
-  if (nk > 1) load(1, S0{});
-  if (NSET == 2 && nk > 2) load(2, S1{});
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  auto iter = [&](int t, auto set_c) {
-    barrier();
-    if (t + 1 < nk) {
-      store((t + 1) & 1, set_c);
-      if (t + 1 + NSET < nk) load(t + 1 + NSET, set_c);
-    }
-    const char* ia = smem + (t & 1) * STAGE_BYTES;
-    const char* ib = ia + TILE_BYTES;
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      bf16x8 fa[4], fb[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) fb[nt] = tr_frag(ib + 16 * s * ROWB, ob[nt]);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) fa[mt] = tr_frag(ia + 16 * s * ROWB, oa[mt]);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma(fa[mt], fb[nt], acc[mt][nt]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  int t = 0;
-  for (; t + 1 < nk; t += 2) {
-    iter(t, S0{});
-    iter(t + 1, S1{});
-  }
-  if (t < nk) iter(t, S0{});
-  store_wave<OUT_F32, ACCUM, 4, 4>(acc, C, ldc, m0 + 128 * wr, n0 + 128 * wc);
-}
+// Variants 6-9 (4 waves x 128 x 128 with AGPR accumulators on the ring; hipBLASLt's register-
+// staged structure one / two K-tiles ahead) measured slower than 5 (MFMA busy 0.42-0.53,
+// profiles/r4/s16, s20) and were removed; their source is in the git history of this file.
 
 }  // namespace dwg
 
@@ -702,9 +458,7 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const bool f32 = c.scalar_type() == at::kFloat;
   // DTG_DWG_VARIANT = 1 (K-tile pipeline) | 2 (k-step pipeline) | 3 (k-step + ping-pong) | 4 (k-step,
   // 10-slot ring, 8 quarters ahead) | 5 (2 k-steps per barrier, 6 quarters ahead)
-  // | 6 (4 waves x 128 x 128, ring 8 ahead) | 7 (6 with 2 k-steps per barrier, 6 ahead)
-  // | 8 (4 waves x 128 x 128, register-staged global loads two K-tiles ahead) | 9 (8, one K-tile ahead);
-  // read per call
+  // (6-9: removed after measurement); read per call
   const char* ve = std::getenv("DTG_DWG_VARIANT");
   const int variant = ve ? std::atoi(ve) : 5;  // the fastest measured (profiles/r4/s15, s16)
 #define DTG_DWG_LAUNCH(F, ACC)                                                                                    \
@@ -716,22 +470,6 @@ void dw_gemm_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
       dwg::dw_gemm_v4_kernel<F, ACC, 1, 8><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
                                                                          b.stride(0), c.data_ptr(), c.stride(0),   \
                                                                          (int)M, (int)N, (int)K);                  \
-    else if (variant == 6)                                                                                        \
-      dwg::dw_gemm_w4_kernel<F, ACC, 1, 8><<<grid, dim3(256), 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),   \
-                                                                          b.stride(0), c.data_ptr(), c.stride(0),  \
-                                                                          (int)M, (int)N, (int)K);                 \
-    else if (variant == 8)                                                                                        \
-      dwg::dw_gemm_rs_kernel<F, ACC, 2><<<grid, dim3(256), 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),   \
-                                                                          b.stride(0), c.data_ptr(), c.stride(0),  \
-                                                                          (int)M, (int)N, (int)K);                 \
-    else if (variant == 9)                                                                                        \
-      dwg::dw_gemm_rs_kernel<F, ACC, 1><<<grid, dim3(256), 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),   \
-                                                                          b.stride(0), c.data_ptr(), c.stride(0),  \
-                                                                          (int)M, (int)N, (int)K);                 \
-    else if (variant == 7)                                                                                        \
-      dwg::dw_gemm_w4_kernel<F, ACC, 2, 6><<<grid, dim3(256), 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b), \
-                                                                             b.stride(0), c.data_ptr(), c.stride(0), \
-                                                                             (int)M, (int)N, (int)K);              \
     else if (variant == 5)                                                                                        \
       dwg::dw_gemm_v4_kernel<F, ACC, 2, 6><<<grid, block, 0, stream()>>>(bf16_ptr(a), a.stride(0), bf16_ptr(b),    \
                                                                          b.stride(0), c.data_ptr(), c.stride(0),   \

@@ -14,7 +14,7 @@ def _ref(a, b):
 
 @pytest.mark.parametrize("K,M,N", [(64, 256, 256), (1024, 512, 768), (4096, 1024, 256), (192, 2560, 512)])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6", "7", "8", "9"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5"])
 def test_dw_gemm_matches_f32(cuda, K, M, N, out_dtype, variant, monkeypatch):
     import dtg.ops  # noqa: F401
 
