@@ -632,11 +632,25 @@ def main(argv=None):
     gc.collect()
     if cuda:
         torch.cuda.empty_cache()
-    # ---- after the timed region: diagnostics of the multi-rank run (none of this is in `value`)
-    coll = collective_sweep(args, torch, dist, device, world, cuda) if (multi and args.coll_sweep_mb) else None
+    # ---- after the timed region: diagnostics of the multi-rank run (none of this is in `value`).
+    # A diagnostic that raises is recorded in the JSON line instead of losing the measurement.
+    diag_errors = {}
+
+    def _diag(name, fn):
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 - recorded, not swallowed
+            diag_errors[name] = repr(e)[:300]
+            gc.collect()
+            if cuda:
+                torch.cuda.empty_cache()
+            return None
+
+    coll = _diag("collectives", lambda: collective_sweep(args, torch, dist, device, world, cuda)) \
+        if (multi and args.coll_sweep_mb) else None
     sweep = None
     if multi and args.bucket_sweep_mb and args.parallel in ("ddp", "zero") and args.tp == 1:
-        sweep = bucket_sweep(args, torch, dist, device, world, rank, cuda)
+        sweep = _diag("bucket_sweep", lambda: bucket_sweep(args, torch, dist, device, world, rank, cuda))
     xgmi_diag = None
     if multi and cuda and args.xgmi_child and world <= 8:
         gc.collect()
@@ -647,12 +661,12 @@ def main(argv=None):
         dist.barrier()
     mem = None
     if args.fsdp_mem_steps > 0:
-        mem = fsdp_memory_phase(args, torch, dist, device, world, rank, cuda)
+        mem = _diag("fsdp_mem", lambda: fsdp_memory_phase(args, torch, dist, device, world, rank, cuda))
         gc.collect()
     mem_one = None
     if args.fsdp_mem_steps > 0 and cuda and rank == 0 and world < args.fsdp_mem_world:
         torch.cuda.empty_cache()
-        mem_one = fsdp_mem_one_rank(args)
+        mem_one = _diag("fsdp_mem_one_rank", lambda: fsdp_mem_one_rank(args))
 
     # per-rank facts, gathered to rank 0: elapsed, device ordinal, PCI bus, peaks
     ref_sum = sum(res["ref_ms"].values()) if res["ref_ms"] else 0.0
@@ -747,6 +761,8 @@ def main(argv=None):
                                "ms_per_step": round(max(r[5] for r in rows), 1),
                                "reference_a100x8": {"valley_gb": 8, "peak_gb": 74}}
             rec["fsdp_peak_mem_gb"] = rec["fsdp_mem"]["peak_gb_max_rank"]
+        if diag_errors:
+            rec["diagnostic_errors"] = diag_errors
         if mem_one is not None:
             rec["fsdp_mem_one_rank_of_w"] = {"world": mem_one["world"], "valley_gb": mem_one["valley_gib"],
                                              "peak_gb": mem_one["peak_gib"], "method": "rank 0 alone, other ranks a "
