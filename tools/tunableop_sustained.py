@@ -8,10 +8,15 @@ forward GEMM takes 2.58 ms where its tuning burst measured 1.79 ms.  A solution 
 bytes or issues less work per FLOP can win under that limit while losing the burst.
 
     # 1. list: tune each shape with PYTORCH_TUNABLEOP_VERBOSE=3 and keep every candidate's burst time
-    python tools/gemm_sustained.py list --out gpurun_out/cands.json
+    python tools/tunableop_sustained.py list --out gpurun_out/cands.json
     # 2. time the top-k candidates of each shape in a sustained loop (one child per candidate rank,
     #    the committed table with that rank's solutions substituted)
-    python tools/gemm_sustained.py time --cands gpurun_out/cands.json --top 4 --out gpurun_out/sustained.jsonl
+    python tools/tunableop_sustained.py time --cands gpurun_out/cands.json --top 4 --out gpurun_out/sustained.jsonl
+
+Round 1's tools/gemm_sustained.cpp swept every hipBLASLt solution of the system library the same
+way (profiles/r1: defaults within noise of the best, 32x32-MFMA solutions 13-17 % slower); this
+tool ranks what PyTorch's own bundled library offers through TunableOp, i.e. exactly the
+solutions a table entry can pin.
 
 Shapes: the Llama-3-8B bench step's TN GEMMs at T = 16384 (key "tn_m_n_k": C[n, m] = A[n, k] B[m, k]^T).
 """
