@@ -1035,9 +1035,12 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
   // Settle this lane's K/V fragment loads before the item loop, on every path into it.  Left
   // pending, hipcc's wait-count analysis carried them around the loop's back edge and put an
   // s_waitcnt vmcnt(1) / vmcnt(0) in front of the first S MFMA of every item -- a wait on the
-  // Q/dO loads just issued for a later item (ISA: llvm-objdump of bwd_dkdv_kernel).
-#pragma unroll
-  for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(kf[c]), "+v"(vf[c]));
+  // Q/dO loads just issued for a later item (ISA: llvm-objdump of bwd_dkdv_kernel).  The wait
+  // is the builtin (vmcnt(0); expcnt, lgkmcnt unconstrained), which the wait-count pass sees.
+  // The earlier form, an empty asm with "+v" operands on the fragments, pinned them to VGPRs
+  // there; the allocator then homed them in AGPRs and copied 44 AGPR -> AGPR registers every
+  // item (v_accvgpr_mov; 695 -> 648 loop instructions without them).
+  __builtin_amdgcn_s_waitcnt(0x0f70);
 
   static_assert(PF == 1 || QB == 32, "two-item prefetch only with 32-row items");
   if constexpr (PF == 2) {
