@@ -8,6 +8,6 @@ export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread -p no:cacheprovider \
     tests/test_xgmi_dp_gpu.py > "$out/pytest_xdp.log" 2>&1 || { tail -40 "$out/pytest_xdp.log"; exit 1; }
 tail -1 "$out/pytest_xdp.log"
-bash tools/sessions/r4_s06.sh
+bash profiles/sessions/r4_s06.sh
 mkdir -p "$out" && cp -r gpurun_out/r4_s06/* "$out/" 2>/dev/null
 true
