@@ -773,13 +773,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 // pipeline (S/dP MFMAs of half 1 under the softmax VALU of half 0, dK/dV MFMAs of half 0 under
 // the softmax of half 1): at one wave per SIMD there is no partner wave to fill the matrix pipe
 // while a wave does its VALU, so the overlap has to come from the wave's own instruction stream.
-// VLDS: the workgroup's V rows live in LDS (one image, read per item as the dP MFMAs' operand)
-// instead of as register fragments, so the D = 128 kernel fits two waves per SIMD (256 registers)
-// and each SIMD has a second wave to run while one waits on its LDS reads or the item barrier.
-template <int D, bool CAUSAL, int PF, bool WIN = false, int QB = kKvBQ, bool DROP = false, bool VLDS = false>
-__global__ __launch_bounds__(256, (D == 128 && !VLDS) ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
+template <int D, bool CAUSAL, int PF, bool WIN = false, int QB = kKvBQ, bool DROP = false>
+__global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
   static_assert(QB == 32 || QB == 64, "query rows per item");
-  static_assert(!VLDS || (QB == 32 && PF == 1 && !DROP), "VLDS: single-set 32-row items");
   constexpr int RB = 2 * D;
   constexpr int NC = D / 16;
   constexpr int ND = D / 32;
@@ -787,7 +783,6 @@ __global__ __launch_bounds__(256, (D == 128 && !VLDS) ? 1 : 2) void bwd_dkdv_ker
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [Q0 | dO0 | Q1 | dO1 | rowc]
   char* qd = smem;
   float* rowc = reinterpret_cast<float*>(qd + 4 * SLICE);      // [2][-lse/scale x QB, -delta x QB]
-  char* vimg = reinterpret_cast<char*>(rowc + 4 * QB);         // VLDS: [kKvBK][RB] V image
 
   const int seq = blockIdx.y, kvh = blockIdx.x;
   const int s0 = P.cu[seq];
@@ -804,17 +799,12 @@ __global__ __launch_bounds__(256, (D == 128 && !VLDS) ? 1 : 2) void bwd_dkdv_ker
   const int wkey0 = kb + 32 * w;
   const int key = wkey0 + r;
 
-  bf16x8 kf[NC], vf[VLDS ? 1 : NC];
+  bf16x8 kf[NC], vf[NC];
   {
     const bool ok = key < klen;
     const int64_t t = kr.start + (ok ? key : klen - 1);
     load_row_frags<NC>(P.k + t * P.sk + (int64_t)kvh * D, ok, h, kf);
-    if constexpr (!VLDS) load_row_frags<NC>(P.v + t * P.sv + (int64_t)kvh * D, ok, h, vf);
-  }
-  if constexpr (VLDS) {  // rows past the sequence read as zeros; visible after the first barrier
-    Stager<kKvBK, D, 256> sv;
-    sv.load(P.v + (int64_t)(kr.start + kb) * P.sv + (int64_t)kvh * D, P.sv, klen - kb);
-    sv.store(vimg);
+    load_row_frags<NC>(P.v + t * P.sv + (int64_t)kvh * D, ok, h, vf);
   }
   int roff[NC], toa[ND], tob[ND];
 #pragma unroll
@@ -913,20 +903,10 @@ __global__ __launch_bounds__(256, (D == 128 && !VLDS) ? 1 : 2) void bwd_dkdv_ker
         for (int c = 0; c < NC; ++c) s = mfma(f[c], kf[c], s);
 #pragma unroll
         for (int c = 0; c < NC; ++c) g[c] = lds_frag(dOl + roff[c]);
-        if constexpr (VLDS) {
-          const char* Vw = vimg + 32 * w * RB;  // this wave's 32 key rows
-          bf16x8 vl[NC];
 #pragma unroll
-          for (int c = 0; c < NC; ++c) vl[c] = lds_frag(Vw + roff[c]);
-#pragma unroll
-          for (int c = 0; c < NC; ++c) dp = mfma(g[c], vl[c], dp);
-        } else {
-#pragma unroll
-          for (int c = 0; c < NC; ++c) dp = mfma(g[c], vf[c], dp);
-        }
+        for (int c = 0; c < NC; ++c) dp = mfma(g[c], vf[c], dp);
       }
-      if constexpr (VLDS) pipeline_reads<2 * NC, 2, 1>();
-      else pipeline_reads<2 * NC, 1, 4>();
+      pipeline_reads<2 * NC, 1, 4>();
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = fexp2(s[i] * P.c2);
@@ -976,7 +956,7 @@ __global__ __launch_bounds__(256, (D == 128 && !VLDS) ? 1 : 2) void bwd_dkdv_ker
 #pragma unroll
     for (int c = 0; c < NC; ++c) g[c] = lds_frag(dOl + roff[c]);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) dp = mfma(g[c], vf[VLDS ? 0 : c], dp);  // (QB = 64 only: never VLDS)
+    for (int c = 0; c < NC; ++c) dp = mfma(g[c], vf[c], dp);
   };
   auto softmax_half = [&](int qsu, int hqi, const float* cnd, f32x16& s, f32x16& dp, bf16x8 (&pf)[2],
                           bf16x8 (&dsf)[2]) {
@@ -1097,19 +1077,9 @@ __global__ __launch_bounds__(256, (D == 128 && !VLDS) ? 1 : 2) void bwd_dkdv_ker
     for (int it = it0; it < it1; ++it) {
       const int buf = it & 1;
       const bool more = it + 1 < it1;
-      if constexpr (VLDS) {
-        // the next item's loads go out after this item's math, so their staging registers are
-        // not live across it (the other wave on the SIMD covers their latency)
-        run_item(it, buf);
-        if (more) {
-          load_item(ia, it + 1);
-          store_item(ia, buf ^ 1);
-        }
-      } else {
-        if (more) load_item(ia, it + 1);
-        run_item(it, buf);
-        if (more) store_item(ia, buf ^ 1);
-      }
+      if (more) load_item(ia, it + 1);
+      run_item(it, buf);
+      if (more) store_item(ia, buf ^ 1);
       __syncthreads();
     }
   }
@@ -1452,12 +1422,8 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
     // pipeline) is the default: backward 2-4 % faster on every benchmarked shape, -1.9 ms per 8B
     // step (profiles/r3_s39).  Sliding windows and the two-item prefetch keep 32.
     const char* qe = std::getenv("DTG_FA_KV_QB");
-    // DTG_FA_KV_VLDS=1: the D = 128 kernel with V in LDS at two waves per SIMD (32-row items);
-    // per call (A/B).
-    const char* ve = std::getenv("DTG_FA_KV_VLDS");
-    const bool vlds = ve != nullptr && ve[0] == '1' && D == 128 && !drop && P.window == 0 && kv_pf == 1;
-    const int qb = !vlds && (drop || ((qe == nullptr || std::atoi(qe) != 32) && P.window == 0 && kv_pf == 1)) ? 64 : 32;
-    const size_t lds = 4 * (size_t)qb * D * 2 + 2 * 2 * qb * 4 + (vlds ? (size_t)fa::kKvBK * D * 2 : 0);
+    const int qb = drop || ((qe == nullptr || std::atoi(qe) != 32) && P.window == 0 && kv_pf == 1) ? 64 : 32;
+    const size_t lds = 4 * (size_t)qb * D * 2 + 2 * 2 * qb * 4;
 #define DTG_BWD_KV(DD, C, PF, ...)                                                        \
   do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>, lds);      \
        hipLaunchKernelGGL((fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>), grid, dim3(256), lds, st, P); } while (0)
@@ -1466,8 +1432,6 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
       else { if (causal) DTG_BWD_KV(64, true, 1, false, 64, true); else DTG_BWD_KV(64, false, 1, false, 64, true); }
     } else if (P.window > 0) {  // sliding window (causal only)
       if (D == 128) DTG_BWD_KV(128, true, 1, true); else DTG_BWD_KV(64, true, 1, true);
-    } else if (vlds) {
-      if (causal) DTG_BWD_KV(128, true, 1, false, 32, false, true); else DTG_BWD_KV(128, false, 1, false, 32, false, true);
     } else if (kv_pf == 2) {
       if (D == 128) { if (causal) DTG_BWD_KV(128, true, 2); else DTG_BWD_KV(128, false, 2); }
       else { if (causal) DTG_BWD_KV(64, true, 2); else DTG_BWD_KV(64, false, 2); }
