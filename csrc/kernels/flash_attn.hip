@@ -35,6 +35,11 @@
 #include <cmath>
 
 namespace dtg {
+
+// csrc/kernels/rope.hip
+void rope_rows_launch(uint16_t* x, int64_t row_stride, int nheads, int head_dim, const float* cos_t,
+                      const float* sin_t, const int64_t* pos, int64_t T, bool inverse, hipStream_t st);
+
 namespace fa {
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
@@ -531,7 +536,42 @@ struct BwdParams {
   float *dk_part, *dv_part;
   int nsplit;
   DropCfg drop;  // DROP instantiations only
+  // Optional RoPE backward fused into the dQ / dK epilogues (flash_attn_bwd_qkv_rope): f32
+  // tables [max_pos, D/2] and int64 position ids [T]; null = none.
+  const float *rope_cos, *rope_sin;
+  const int64_t* rope_pos;
 };
+
+// Inverse rotary rotation of a row-per-lane accumulator (lane = row, registers = columns
+// 32d + 8g + 4h + e) in place, in f32 before the single bf16 rounding of the store: the backward
+// of q' = q cos + rotate_half(q) sin, i.e. (x1, x2) -> (x1 cos + x2 sin, x2 cos - x1 sin) for the
+// column pairs (i, i + D/2), which live in tiles d and d + ND/2 of the same register.  Same
+// semantics as rope_kernel(inverse = true), one rounding fewer.
+template <int ND>
+__device__ __forceinline__ void rope_inv_rows(f32x16* acc, const float* cos_t, const float* sin_t, int64_t p) {
+  constexpr int HT = ND / 2;     // tiles in the first half
+  constexpr int HALF = 16 * ND;  // D / 2
+  const int h = (threadIdx.x & 63) >> 5;
+  const float* cp = cos_t + p * HALF;
+  const float* sp = sin_t + p * HALF;
+#pragma unroll
+  for (int d = 0; d < HT; ++d) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int i = 32 * d + 8 * g + 4 * h;
+      const float4 c = *reinterpret_cast<const float4*>(cp + i);
+      const float4 sn = *reinterpret_cast<const float4*>(sp + i);
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * g + e;
+        const float x1 = acc[d][r], x2 = acc[d + HT][r];
+        acc[d][r] = x1 * cc[e] + x2 * ss[e];
+        acc[d + HT][r] = x2 * cc[e] - x1 * ss[e];
+      }
+    }
+  }
+}
 
 constexpr int kDqBQ = 128;  // query rows per workgroup (4 waves x 32)
 constexpr int kDqBK = 64;   // keys per K/V tile
@@ -757,6 +797,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   }
   if (t < ntiles) tile_step(t, std::integral_constant<int, 0>{});
 
+  if (P.rope_cos != nullptr) rope_inv_rows<ND>(acc, P.rope_cos, P.rope_sin, P.rope_pos[s0 + min(qrow, seqlen - 1)]);
   store_rows_wide<ND>(acc, P.scale, P.dq + (int64_t)(s0 + min(qrow, seqlen - 1)) * P.sdq + (int64_t)head * D, qok);
 }
 
@@ -1101,6 +1142,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
     }
     return;
   }
+  if (P.rope_cos != nullptr) rope_inv_rows<ND>(dk, P.rope_cos, P.rope_sin, P.rope_pos[krow]);
   store_rows_wide<ND>(dk, P.scale, P.dk + krow * P.sdk + (int64_t)kvh * D, key < klen);
   store_rows_wide<ND>(dv, 1.f, P.dv + krow * P.sdv + (int64_t)kvh * D, key < klen);
 }
@@ -1270,13 +1312,18 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
                             int nseq, hipStream_t st, const at::Tensor& dk_t, const at::Tensor& dv_t, bool drop = false);
 
 // Shared backward driver: outputs are [T, H, D] views (contiguous heads, any token stride).
+struct RopeTabs {
+  const at::Tensor *cos, *sin, *pos;
+};
+
 static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, const at::Tensor& k,
                                 const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
                                 const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale,
                                 bool causal, const at::Tensor& dq, const at::Tensor& dk,
                                 const at::Tensor& dv, const at::Tensor* k_start = nullptr,
                                 const at::Tensor* k_len = nullptr, int64_t max_seqlen_k = -1,
-                                int64_t window = 0, const fa::DropCfg* drop = nullptr) {
+                                int64_t window = 0, const fa::DropCfg* drop = nullptr,
+                                const RopeTabs* rope = nullptr) {
   auto dout = dout_.contiguous();
   const int64_t T = q.size(0), hq = q.size(1), D = q.size(2), hkv = k.size(1);
   check_qkv(q, "q", hq, D);
@@ -1313,6 +1360,18 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   DTG_CHECK(window >= 0 && window < (1ll << 30), "flash_attn: window must be >= 0 (0 = full causal)");
   P.window = causal ? (int)window : 0;
   if (max_seqlen_k < 0) max_seqlen_k = max_seqlen;
+  if (rope != nullptr) {
+    const at::Tensor &ct = *rope->cos, &stb = *rope->sin, &pt = *rope->pos;
+    DTG_CHECK(ct.is_cuda() && ct.scalar_type() == at::kFloat && stb.scalar_type() == at::kFloat && ct.is_contiguous() &&
+                  stb.is_contiguous() && ct.dim() == 2 && ct.size(1) == D / 2 && stb.sizes() == ct.sizes(),
+              "flash_attn rope: tables must be contiguous f32 [max_pos, D/2] on the GPU");
+    DTG_CHECK(pt.is_cuda() && pt.scalar_type() == at::kLong && pt.is_contiguous() && pt.numel() == T,
+              "flash_attn rope: position ids must be int64 [T] on the GPU");
+    DTG_CHECK(P.kstart == nullptr && drop == nullptr, "flash_attn rope: self-attention without dropout only");
+    P.rope_cos = ct.data_ptr<float>();
+    P.rope_sin = stb.data_ptr<float>();
+    P.rope_pos = pt.data_ptr<int64_t>();
+  }
   if (drop != nullptr) {
     DTG_CHECK(P.window == 0 && P.kstart == nullptr, "flash_attn dropout: no sliding window / key ranges");
     P.drop = *drop;
@@ -1454,6 +1513,9 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
       fa::bwd_kv_combine_kernel<64><<<(nv + 255) / 256, 256, 0, st>>>(P.dk_part, P.dv_part, nsplit, P.T, (int)hkv,
                                                                      P.scale, P.dk, P.sdk, P.dv, P.sdv);
     DTG_LAUNCH_CHECK();
+    // the split kernel's epilogue writes f32 partials: the fused RoPE backward runs on the
+    // combined dK instead
+    if (P.rope_cos != nullptr) rope_rows_launch(P.dk, P.sdk, (int)hkv, (int)D, P.rope_cos, P.rope_sin, P.rope_pos, P.T, true, st);
   }
 }
 
@@ -1486,6 +1548,28 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& qkv, int
   flash_attn_bwd_impl(dout, view3(qkv, 0, nq), view3(qkv, nq, nkv), view3(qkv, nq + nkv, nkv), o, lse,
                       cu_seqlens, max_seqlen, scale, causal, view3(dqkv, 0, nq), view3(dqkv, nq, nkv),
                       view3(dqkv, nq + nkv, nkv), nullptr, nullptr, -1, window);
+  return dqkv;
+}
+
+// flash_attn_bwd_qkv with the RoPE backward of the q and k heads fused into the dQ / dK
+// epilogues (replaces rope_(dqkv, cos, sin, pos, nq + nkv, D, inverse = true) after it).
+at::Tensor flash_attn_bwd_qkv_rope(const at::Tensor& dout, const at::Tensor& qkv, int64_t nq, int64_t nkv,
+                                   int64_t head_dim, const at::Tensor& o, const at::Tensor& lse,
+                                   const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale, bool causal,
+                                   const at::Tensor& cos_t, const at::Tensor& sin_t, const at::Tensor& pos,
+                                   int64_t window) {
+  DTG_CHECK_CUDA_BF16(qkv);
+  const int64_t T = qkv.size(0), D = head_dim;
+  DTG_CHECK(qkv.dim() == 2 && qkv.size(1) == (nq + 2 * nkv) * D && qkv.stride(1) == 1,
+            "flash_attn_bwd_qkv_rope: qkv must be [T, (nq + 2 nkv) * D]");
+  auto dqkv = at::empty({T, (nq + 2 * nkv) * D}, qkv.options());
+  auto view3 = [&](const at::Tensor& t, int64_t h0, int64_t nh) {
+    return t.as_strided({T, nh, D}, {t.stride(0), D, 1}, t.storage_offset() + h0 * D);
+  };
+  const RopeTabs rt{&cos_t, &sin_t, &pos};
+  flash_attn_bwd_impl(dout, view3(qkv, 0, nq), view3(qkv, nq, nkv), view3(qkv, nq + nkv, nkv), o, lse,
+                      cu_seqlens, max_seqlen, scale, causal, view3(dqkv, 0, nq), view3(dqkv, nq, nkv),
+                      view3(dqkv, nq + nkv, nkv), nullptr, nullptr, -1, window, nullptr, &rt);
   return dqkv;
 }
 
@@ -1562,6 +1646,7 @@ TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
   m.impl("flash_attn_fwd_stamped", &flash_attn_fwd_stamped);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("flash_attn_bwd_qkv", &flash_attn_bwd_qkv);
+  m.impl("flash_attn_bwd_qkv_rope", &flash_attn_bwd_qkv_rope);
 }
 
 }  // namespace dtg

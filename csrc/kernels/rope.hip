@@ -51,6 +51,24 @@ __global__ void rope_kernel(uint16_t* __restrict__ qkv, int64_t row_stride, int 
   store8(base + HALF, o2);
 }
 
+// Raw-pointer launch for other translation units (the flash-attention backward's split dK path).
+void rope_rows_launch(uint16_t* x, int64_t row_stride, int nheads, int head_dim, const float* cos_t,
+                      const float* sin_t, const int64_t* pos, int64_t T, bool inverse, hipStream_t st) {
+  const int threads = 256;
+  if (T == 0) return;
+  if (head_dim == 128) {
+    const int64_t total = T * nheads * (64 / 8);
+    rope_kernel<128><<<(total + threads - 1) / threads, threads, 0, st>>>(x, row_stride, nheads, cos_t, sin_t, pos, T,
+                                                                          inverse);
+  } else {
+    DTG_CHECK(head_dim == 64, "rope: head_dim must be 64 or 128");
+    const int64_t total = T * nheads * (32 / 8);
+    rope_kernel<64><<<(total + threads - 1) / threads, threads, 0, st>>>(x, row_stride, nheads, cos_t, sin_t, pos, T,
+                                                                         inverse);
+  }
+  DTG_LAUNCH_CHECK();
+}
+
 void rope_(const at::Tensor& qkv, const at::Tensor& cos_t, const at::Tensor& sin_t,
            const at::Tensor& pos, int64_t nheads, int64_t head_dim, bool inverse) {
   DTG_CHECK_CUDA_BF16(qkv);

@@ -391,6 +391,13 @@ def flash_attn_bwd_qkv(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seq
     return torch.cat([dq.reshape(T, -1), dk.reshape(T, -1), dv.reshape(T, -1)], dim=1)
 
 
+def flash_attn_bwd_qkv_rope(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal, cos, sin,
+                            pos, window=0):
+    dqkv = flash_attn_bwd_qkv(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal, window)
+    rope_(dqkv, cos, sin, pos, nq + nkv, head_dim, True)
+    return dqkv
+
+
 def swiglu_bwd_t(dh, gu):
     dgu = swiglu_bwd(dh, gu)
     return dgu, dgu.t().contiguous(), swiglu_fwd(gu).t().contiguous()
@@ -429,6 +436,6 @@ for _name, _fn in list(globals().items()):
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "adamw_t_", "flash_attn_fwd", "flash_attn_bwd",
         "flash_attn_bwd_qkv", "transpose2d", "transpose_mats_", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
         "flash_attn_varlen_bwd", "flash_attn_fwd_drop", "flash_attn_bwd_drop", "flash_attn_bwd_qkv_drop",
-        "swiglu_bwd_h", "dw_gemm_",
+        "swiglu_bwd_h", "dw_gemm_", "flash_attn_bwd_qkv_rope",
     ):
         LIB.impl(_name, _fn, "CPU")

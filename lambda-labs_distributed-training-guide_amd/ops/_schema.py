@@ -37,6 +37,10 @@ _DEFS = [
     "int max_seqlen, float scale, bool causal, int window=0) -> (Tensor, Tensor, Tensor)",
     "flash_attn_bwd_qkv(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
     "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, int window=0) -> Tensor",
+    # the same with the RoPE backward of the q / k heads fused into the dQ / dK epilogues
+    "flash_attn_bwd_qkv_rope(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
+    "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, Tensor cos, Tensor sin, Tensor pos, "
+    "int window=0) -> Tensor",
     # attention-probability dropout regenerated from Philox(seed, offset) in the backward
     "flash_attn_fwd_drop(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, bool causal, "
     "float p, int seed, int offset) -> (Tensor, Tensor)",

@@ -213,6 +213,11 @@ def rope_tables(head_dim, theta, max_pos, scaling=None, device=None):
 # --------------------------------------------------------------------------------------------
 # Attention (RoPE fused into the same autograd node; fused QKV in, fused dQKV out)
 # --------------------------------------------------------------------------------------------
+# DTG_FA_ROPE_FUSED=1: the RoPE backward of the q / k heads inside the attention backward's dQ / dK
+# epilogues (csrc/kernels/flash_attn.hip, one bf16 rounding) instead of a separate in-place pass.
+_FA_ROPE_FUSED = os.environ.get("DTG_FA_ROPE_FUSED", "0") == "1"
+
+
 class _AttentionQKV(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, cos, sin, pos, cu_seqlens, max_seqlen, nq, nkv, head_dim, scale, causal, rope, window):
@@ -233,10 +238,14 @@ class _AttentionQKV(torch.autograd.Function):
         qkv, o, lse, cu, cos, sin, pos = ctx.saved_tensors
         max_seqlen, nq, nkv, d, scale, causal, rope, window = ctx.meta
         T = qkv.shape[0]
-        dqkv = ops.flash_attn_bwd_qkv(do.contiguous().view(T, nq, d), qkv, nq, nkv, d, o, lse, cu, max_seqlen, scale,
-                                      causal, window)
-        if rope:
-            ops.rope_(dqkv, cos, sin, pos, nq + nkv, d, True)
+        if rope and _FA_ROPE_FUSED:  # RoPE backward inside the dQ / dK epilogues
+            dqkv = ops.flash_attn_bwd_qkv_rope(do.contiguous().view(T, nq, d), qkv, nq, nkv, d, o, lse, cu, max_seqlen,
+                                               scale, causal, cos, sin, pos, window)
+        else:
+            dqkv = ops.flash_attn_bwd_qkv(do.contiguous().view(T, nq, d), qkv, nq, nkv, d, o, lse, cu, max_seqlen,
+                                          scale, causal, window)
+            if rope:
+                ops.rope_(dqkv, cos, sin, pos, nq + nkv, d, True)
         return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
 
 
