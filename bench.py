@@ -34,6 +34,7 @@ import subprocess
 import sys
 import time
 
+T_START = time.time()  # the run's wall clock starts here (diagnostic budget, deadline, wall_s)
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -52,13 +53,16 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=int, default=256)
     # ZeRO's bucket collectives: RCCL (default) or copy-engine pulls between the ranks' shared flat
     # buffers over xGMI (parallel/xgmi_dp.py); the N > 1 sweep times the other one too
-    ap.add_argument("--dp-comm", default="rccl", choices=["rccl", "xgmi-dma"])
+    # auto (default) = the faster of the two on this job's group at one bucket, timed at startup in a
+    # child job (parallel/transport.py; a first contact with cross-device IPC cannot take the measured
+    # run down); recorded as dp_comm_calibration
+    ap.add_argument("--dp-comm", default="auto", choices=["auto", "rccl", "xgmi-dma"])
     # BASELINE config 06 (Llama-3-8B TP=8 over xGMI): --tp 8 --gpus 8.  Tensor + sequence parallel
     # inside groups of --tp ranks, data parallel (--parallel) across them; a step is dp x B x S
     # tokens (the reference's TP tok/s formula, 06-tensor-parallel/train_llm.py:256).
     ap.add_argument("--tp", type=int, default=1)
-    # auto = xgmi-dma on a GPU (the README's recommendation for config 06; the N > 1 collective
-    # sweep records RCCL vs both xGMI engines at the TP message sizes), the PG backend on CPU
+    # auto = the fastest of RCCL / xGMI pull kernels / xGMI copy engines at this job's TP message size,
+    # timed at startup like --dp-comm auto (the chapter-06/07 trainer's default too); the PG backend on CPU
     ap.add_argument("--tp-comm", default="auto", choices=["auto", "rccl", "xgmi", "xgmi-dma"])
     ap.add_argument("--tp-overlap-chunks", type=int, default=2)
     ap.add_argument("--overlap-optimizer", type=int, default=0,
@@ -92,7 +96,18 @@ def parse(argv=None):
     # engines) run in a CHILD job launched by rank 0 after the timed region: a first contact of
     # IPC-mapped peer memory with a machine must not be able to take the measured run down.
     ap.add_argument("--xgmi-child", type=int, default=1)
-    ap.add_argument("--diag-only", default="", choices=["", "xgmi"], help=argparse.SUPPRESS)
+    ap.add_argument("--diag-only", default="", choices=["", "xgmi", "calibrate"], help=argparse.SUPPRESS)
+    # Wall-clock contract of a run (the driver kills a bench at its own limit, 600 s so far): every
+    # diagnostic phase after the timed region starts only while the run is younger than
+    # --diag-budget-s; at --deadline-s a watchdog prints the headline line (diagnostics done so far,
+    # the rest named in diagnostic_errors) and ends every rank with exit code 0.
+    ap.add_argument("--diag-budget-s", type=float, default=240.0)
+    ap.add_argument("--deadline-s", type=float, default=480.0)
+    ap.add_argument("--xgmi-child-timeout", type=float, default=150.0)
+    ap.add_argument("--calib-child-timeout", type=float, default=120.0)
+    # tests: "child-sleep:S" replaces the xGMI child job by one that sleeps S s; "hang" adds a
+    # diagnostic phase that never returns
+    ap.add_argument("--diag-stub", default="", help=argparse.SUPPRESS)
     # reference-mode throughput: this many extra steps under the reference's synchronising
     # LocalTimer phases (outside the timed region); 0 = off
     ap.add_argument("--ref-steps", type=int, default=3)
@@ -204,11 +219,11 @@ def close_job(job, torch):
 
 
 def resolve_tp_comm(choice: str, cuda: bool) -> str:
-    """--tp-comm auto: the copy-engine xGMI path on a GPU (every TP group of this bench lives
-    inside one node, the xGMI island), the process group's collectives on CPU."""
+    """A transport still "auto" here (nothing calibrated it: CPU, one rank, a gloo rehearsal) is the
+    process group's own collectives; resolve_transports() replaces "auto" by the measured pick."""
     if choice != "auto":
         return choice
-    return "xgmi-dma" if cuda else "rccl"
+    return "rccl"
 
 
 def throughput_phase(args, torch, dist, device, world, rank, cuda):
@@ -502,29 +517,139 @@ def _xgmi_sweep(torch, dist, device, world, cuda, sizes):
     return rows
 
 
-def xgmi_child_diag(args, world):
+_CHILD_PGIDS = set()  # process groups of running child jobs: the watchdog kills them before exiting
+
+
+def _run_child(cmd, timeout, env):
+    """Run a child job in its own process group; on timeout the whole group (torchrun and its
+    workers) is killed.  Returns (returncode or None on timeout, stdout, stderr)."""
+    import signal
+
+    pr = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                          start_new_session=True)
+    _CHILD_PGIDS.add(pr.pid)
+    try:
+        out, err = pr.communicate(timeout=max(1.0, timeout))
+        return pr.returncode, out, err
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(pr.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        out, err = pr.communicate()
+        return None, out, err
+    finally:
+        _CHILD_PGIDS.discard(pr.pid)
+
+
+def _child_env():
+    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+            "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE", "NCCL_DEBUG", "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS")
+    return {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+
+
+def _child_cmd(args, world, what):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+           "--gpus", str(world), "--diag-only", what, "--model", args.model, "--batch-size", str(args.batch_size),
+           "--seq-len", str(args.seq_len), "--bucket-mb", str(args.bucket_mb), "--coll-sweep-mb", args.coll_sweep_mb,
+           "--sweep-steps", str(args.sweep_steps), "--tunableop", args.tunableop, "--parallel", args.parallel,
+           "--tp", str(args.tp), "--tp-overlap-chunks", str(args.tp_overlap_chunks),
+           "--dp-comm", args.dp_comm, "--tp-comm", args.tp_comm]
+    if args.backend:
+        cmd += ["--backend", args.backend]
+    return cmd
+
+
+def _child_json(rc, out, err, label, timeout):
+    if rc is None:
+        return {"error": f"{label} child timed out ({timeout:.0f} s)", "stderr_tail": (err or "")[-400:]}
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if rc != 0 or not lines:
+        return {"error": f"{label} child exited {rc}", "stderr_tail": (err or "")[-600:]}
+    return json.loads(lines[-1])
+
+
+def xgmi_child_diag(args, world, timeout):
     """Rank 0: `torchrun --nproc-per-node world bench.py --diag-only xgmi ...` as a child job on the
     same GPUs; returns its JSON record (or an error record).  The child times the xGMI library's
     all-gather / reduce-scatter (pull kernels and copy engines) and a ZeRO step over the copy
     engines at this run's config."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
-           "--gpus", str(world), "--diag-only", "xgmi", "--model", args.model, "--batch-size", str(args.batch_size),
-           "--seq-len", str(args.seq_len), "--bucket-mb", str(args.bucket_mb), "--coll-sweep-mb", args.coll_sweep_mb,
-           "--sweep-steps", str(args.sweep_steps), "--tunableop", args.tunableop, "--parallel", args.parallel]
-    if args.backend:
-        cmd += ["--backend", args.backend]
-    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
-            "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE", "NCCL_DEBUG", "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS")
-    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
-    try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, env=env)
-    except subprocess.TimeoutExpired:
-        return {"error": "xgmi diagnostic child timed out (420 s)"}
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    if r.returncode != 0 or not lines:
-        return {"error": f"xgmi diagnostic child exited {r.returncode}", "stderr_tail": r.stderr[-600:]}
-    return json.loads(lines[-1])
+    if args.diag_stub.startswith("child-sleep:"):
+        cmd = [sys.executable, "-c", f"import time; time.sleep({float(args.diag_stub.split(':')[1])})"]
+    else:
+        cmd = _child_cmd(args, world, "xgmi")
+    rc, out, err = _run_child(cmd, timeout, _child_env())
+    return _child_json(rc, out, err, "xgmi diagnostic", timeout)
+
+
+def calibrate_child(args, world, timeout):
+    """Rank 0, before anything is built: `--diag-only calibrate` as a child job times RCCL against the
+    xGMI transports at this job's message sizes (parallel/transport.py) and returns
+    {"dp": {"choice", "table"}, "tp": {...}}.  The first contact of the xGMI library with
+    cross-device IPC happens there, never in the measured processes."""
+    rc, out, err = _run_child(_child_cmd(args, world, "calibrate"), timeout, _child_env())
+    return _child_json(rc, out, err, "transport calibration", timeout)
+
+
+def calibrate_main(args, torch, dist, device, world, rank, cuda):
+    """--diag-only calibrate (the child job)."""
+    from dtg.parallel import transport
+
+    out = {}
+    if args.dp_comm == "auto" and args.parallel in ("zero", "fsdp") and world // max(1, args.tp) > 1:
+        group = None
+        if args.tp > 1:
+            from dtg.parallel.tensor_parallel import make_mesh
+
+            group = make_mesh(args.tp)[0]
+        if args.parallel == "zero":
+            msg = args.bucket_mb << 20
+        else:
+            from dtg.models import resolve_config
+
+            cfg = resolve_config(args.model)
+            emb = cfg.vocab_size * cfg.hidden_size * (1 if cfg.tie_word_embeddings else 2)
+            msg = 2 * ((cfg.num_params() - emb) // cfg.num_hidden_layers) // max(1, args.tp)
+        choice, table = transport.select("dp", group, device, msg)
+        out["dp"] = {"choice": choice, "table": table}
+    if args.tp_comm == "auto" and args.tp > 1:
+        from dtg.models import resolve_config
+        from dtg.parallel.tensor_parallel import make_mesh
+
+        cfg = resolve_config(args.model)
+        tp_group = make_mesh(args.tp)[1]
+        msg = transport.tp_message_bytes(args.batch_size, args.seq_len, cfg.hidden_size) // max(1, args.tp_overlap_chunks)
+        choice, table = transport.select("tp", tp_group, device, msg)
+        out["tp"] = {"choice": choice, "table": table}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
+
+
+def resolve_transports(args, torch, dist, world, rank, cuda, backend):
+    """--dp-comm / --tp-comm auto -> concrete transports on every rank.  GPU + RCCL: rank 0 runs the
+    calibration child job and broadcasts its pick; otherwise (CPU, gloo rehearsals, one rank) the
+    process group's own collectives.  Returns the calibration record (or None)."""
+    need_dp = args.dp_comm == "auto"
+    need_tp = args.tp_comm == "auto"
+    if not (need_dp or need_tp):
+        return None
+    rec = None
+    if cuda and world > 1 and backend == "nccl" and (
+            (need_dp and args.parallel in ("zero", "fsdp") and world // max(1, args.tp) > 1) or (need_tp and args.tp > 1)):
+        box = [None]
+        if rank == 0:
+            box[0] = calibrate_child(args, world, args.calib_child_timeout)
+        dist.broadcast_object_list(box, src=0)
+        rec = box[0]
+    if need_dp:
+        args.dp_comm = (rec or {}).get("dp", {}).get("choice", "rccl")
+    if need_tp:
+        args.tp_comm = (rec or {}).get("tp", {}).get("choice", "rccl")
+    return rec
 
 
 def xgmi_diag_main(args, torch, dist, device, world, rank, cuda):
@@ -540,6 +665,55 @@ def xgmi_diag_main(args, torch, dist, device, world, rank, cuda):
     dist.barrier()
     dist.destroy_process_group()
     return 0
+
+
+class Reporter:
+    """Rank 0's one JSON line, printed exactly once: normally at the end of the run, or by the
+    watchdog at --deadline-s with whatever the diagnostics have added so far."""
+
+    def __init__(self, rank, deadline_s):
+        import threading
+
+        self.rank = rank
+        self.rec = None
+        self.phase = "startup"
+        self.lock = threading.Lock()
+        self.done = False
+        self.deadline_s = deadline_s
+        self.timer = threading.Thread(target=self._watch, daemon=True)
+        self.timer.start()
+
+    def _watch(self):
+        time.sleep(max(0.0, T_START + self.deadline_s - time.time()))
+        import signal
+
+        for pg in list(_CHILD_PGIDS):
+            try:
+                os.killpg(pg, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+        with self.lock:
+            if self.done:
+                return
+            if self.rec is None:  # the timed region never finished: nothing to report
+                print(f"[bench] rank {self.rank}: deadline {self.deadline_s:.0f} s reached in phase "
+                      f"'{self.phase}' before the timed region finished", file=sys.stderr, flush=True)
+                os._exit(3)
+            self.rec.setdefault("diagnostic_errors", {})[self.phase] = (
+                f"still running at the {self.deadline_s:.0f} s deadline: the line was printed by the watchdog")
+            self._print_locked()
+        os._exit(0)
+
+    def _print_locked(self):
+        self.done = True
+        if self.rank == 0:
+            self.rec["wall_s"] = round(time.time() - T_START, 1)
+            print(json.dumps(self.rec), flush=True)
+
+    def emit(self):
+        with self.lock:
+            if not self.done:
+                self._print_locked()
 
 
 def _load_rccl_module():
@@ -627,79 +801,50 @@ def main(argv=None):
     torch.manual_seed(0)
     if args.diag_only == "xgmi":
         return xgmi_diag_main(args, torch, dist, device, world, rank, cuda)
+    if args.diag_only == "calibrate":
+        return calibrate_main(args, torch, dist, device, world, rank, cuda)
 
+    reporter = Reporter(rank, args.deadline_s)
+    phase_s = {}
+    t_ph = time.time()
+    reporter.phase = "transport_calibration"
+    calib = resolve_transports(args, torch, dist, world, rank, cuda, backend)
+    phase_s["startup_and_calibration"] = round(time.time() - T_START, 1)
+    reporter.phase = "throughput"
+    t_ph = time.time()
     res = throughput_phase(args, torch, dist, device, world, rank, cuda)
+    phase_s["throughput"] = round(time.time() - t_ph, 1)
     gc.collect()
     if cuda:
         torch.cuda.empty_cache()
-    # ---- after the timed region: diagnostics of the multi-rank run (none of this is in `value`).
-    # A diagnostic that raises is recorded in the JSON line instead of losing the measurement.
-    diag_errors = {}
 
-    def _diag(name, fn):
-        try:
-            return fn()
-        except Exception as e:  # noqa: BLE001 - recorded, not swallowed
-            diag_errors[name] = repr(e)[:300]
-            gc.collect()
-            if cuda:
-                torch.cuda.empty_cache()
-            return None
+    # ---- the headline, gathered and built BEFORE any diagnostic: from here on the line is printed
+    # whatever a diagnostic does (error -> diagnostic_errors; hang -> the watchdog at --deadline-s)
+    def gather(vals):
+        mine = torch.tensor(vals, dtype=torch.float64, device=device)
+        if world > 1 and fake_world <= 1:
+            allv = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(allv, mine)
+            return [v.cpu().tolist() for v in allv]
+        return [mine.cpu().tolist()]  # one rank, or the other ranks do not exist (fake world)
 
-    coll = _diag("collectives", lambda: collective_sweep(args, torch, dist, device, world, cuda)) \
-        if (multi and args.coll_sweep_mb) else None
-    sweep = None
-    if multi and args.bucket_sweep_mb and args.parallel in ("ddp", "zero") and args.tp == 1:
-        sweep = _diag("bucket_sweep", lambda: bucket_sweep(args, torch, dist, device, world, rank, cuda))
-    xgmi_diag = None
-    if multi and cuda and args.xgmi_child and world <= 8:
-        gc.collect()
-        torch.cuda.empty_cache()
-        dist.barrier()
-        if rank == 0:
-            xgmi_diag = xgmi_child_diag(args, world)
-        dist.barrier()
-    mem = None
-    if args.fsdp_mem_steps > 0:
-        mem = _diag("fsdp_mem", lambda: fsdp_memory_phase(args, torch, dist, device, world, rank, cuda))
-        gc.collect()
-    mem_one = None
-    if args.fsdp_mem_steps > 0 and cuda and rank == 0 and world < args.fsdp_mem_world:
-        torch.cuda.empty_cache()
-        mem_one = _diag("fsdp_mem_one_rank", lambda: fsdp_mem_one_rank(args))
-
-    # per-rank facts, gathered to rank 0: elapsed, device ordinal, PCI bus, peaks
-    ref_sum = sum(res["ref_ms"].values()) if res["ref_ms"] else 0.0
-    me = [res["elapsed"], float(dev_idx), float(res["peak_gb"]),
-          mem["valley"] if mem else 0.0, mem["peak"] if mem else 0.0, mem["ms"] if mem else 0.0,
-          ref_sum, res["replica_sum"]] + ([res["ref_ms"][k] for k in ("data", "forward", "backward", "update")]
-                                         if res["ref_ms"] else [0.0] * 4)
-    mine = torch.tensor(me, dtype=torch.float64, device=device)
-    if world > 1 and fake_world > 1:
-        rows = [mine.cpu().tolist()]  # the other ranks do not exist
-    elif world > 1:
-        allv = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(allv, mine)
-        rows = [v.cpu().tolist() for v in allv]
-    else:
-        rows = [mine.cpu().tolist()]
+    ref_keys = ("data", "forward", "backward", "update")
+    rows = gather([res["elapsed"], float(dev_idx), float(res["peak_gb"]), sum(res["ref_ms"].values()) if res["ref_ms"]
+                   else 0.0, res["replica_sum"]] + ([res["ref_ms"][k] for k in ref_keys] if res["ref_ms"] else [0.0] * 4))
     bus = None
     if cuda:
-        p = torch.cuda.get_device_properties(device)
-        bus = getattr(p, "pci_bus_id", None)
+        bus = getattr(torch.cuda.get_device_properties(device), "pci_bus_id", None)
     elapsed = max(r[0] for r in rows)  # the slowest rank bounds the job
-
     cfg = res["cfg"]
     B, S = args.batch_size, args.seq_len
     dp = res["dp"]
-    tokens = dp * B * S * args.steps
-    tps = tokens / elapsed
+    tps = dp * B * S * args.steps / elapsed
     ms = 1000 * elapsed / args.steps
-    flops_tok = cfg.flops_per_token(S)
-    mfu = tps * flops_tok / (world * 2.5e15) if cuda else 0.0
+    mfu = tps * cfg.flops_per_token(S) / (world * 2.5e15) if cuda else 0.0
     # TP collectives: "rccl" means the process group's own backend (gloo in CPU / shared-GPU rehearsals)
     tp_comm = res["tp_comm"]
     tp_comm_label = tp_comm if tp_comm != "rccl" else ("rccl" if backend in (None, "nccl") else backend)
+    rec = {}
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -725,50 +870,118 @@ def main(argv=None):
             "backend": backend or "none",
             "rank_devices": [int(r[1]) for r in rows],
             "rank0_pci_bus_id": bus,
-            "rank_ms_per_step": {"max": round(1000 * elapsed / args.steps, 2),
-                                 "min": round(1000 * min(r[0] for r in rows) / args.steps, 2)},
+            "rank_ms_per_step": {"max": round(ms, 2), "min": round(1000 * min(r[0] for r in rows) / args.steps, 2)},
+            "loss_band": [round(math.log(cfg.vocab_size) - 3.5, 2), round(math.log(cfg.vocab_size) + 1.5, 2)],
+            "phase_s": phase_s,
         }
-        rec["loss_band"] = [round(math.log(cfg.vocab_size) - 3.5, 2), round(math.log(cfg.vocab_size) + 1.5, 2)]
         if res["ref_ms"]:
             # the reference's own tok/s (synchronised LocalTimer phases, slowest rank)
-            ref_sum_max = max(r[6] for r in rows)
-            rec["tok_s_reference_timers"] = round(1000 * dp * B * S / ref_sum_max, 1)
-            rec["reference_timer_ms"] = {k: round(max(r[8 + j] for r in rows), 2)
-                                         for j, k in enumerate(("data", "forward", "backward", "update"))}
+            rec["tok_s_reference_timers"] = round(1000 * dp * B * S / max(r[3] for r in rows), 1)
+            rec["reference_timer_ms"] = {k: round(max(r[5 + j] for r in rows), 2) for j, k in enumerate(ref_keys)}
             rec["reference_timer_steps"] = args.ref_steps
-        sums = [r[7] for r in rows]
-        if world > 1 and fake_world <= 1 and all(math.isfinite(s) for s in sums):
+        sums = [r[4] for r in rows]
+        if world > 1 and fake_world <= 1 and all(math.isfinite(x) for x in sums):
             # every data-parallel replica must hold bit-identical weights after the last step
             rec["replicas_consistent"] = len(set(sums)) == 1
         if fake_world > 1:
             rec["metric"] = "REHEARSAL (not a measurement of the job): " + METRIC
             rec["rehearsal"] = (f"rank 0 of a {world}-rank job alone on one GPU, other ranks a fake process "
                                 "group: communication not included, value = one rank's compute rate x world")
-        if coll is not None and fake_world <= 1:
-            rec["collectives"] = coll
-        if sweep is not None:
-            rec["bucket_sweep"] = sweep
-        if xgmi_diag is not None:
-            rec["xgmi_diag"] = xgmi_diag
+        if calib is not None:
+            for k in ("dp", "tp"):
+                if k in calib:
+                    rec[f"{k}_comm_calibration"] = calib[k]
+            if "error" in calib:
+                rec["transport_calibration_error"] = calib
         if multi and backend == "nccl":
             rec["rccl"] = _load_rccl_module().diagnose(rccl_log)
             rec["rccl"]["preset_applied"] = rccl_applied
-        if mem is not None:
+    reporter.rec = rec
+    diag_errors = {}
+
+    def in_budget(collective=True):
+        """Start the next diagnostic only while the run is younger than --diag-budget-s (all ranks
+        decide together on the oldest rank's clock)."""
+        age = time.time() - T_START
+        if collective and world > 1 and fake_world <= 1:
+            t = torch.tensor([age], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            age = float(t.item())
+        return age < args.diag_budget_s
+
+    def phase(name, fn, collective=True):
+        if not in_budget(collective):
+            diag_errors[name] = f"skipped: run older than the {args.diag_budget_s:.0f} s diagnostic budget"
+            if rank == 0:
+                rec.setdefault("diagnostic_errors", {})[name] = diag_errors[name]
+            return None
+        reporter.phase = name
+        t0 = time.time()
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 - recorded in the line, never loses the measurement
+            diag_errors[name] = repr(e)[:300]
+            if rank == 0:
+                rec.setdefault("diagnostic_errors", {})[name] = diag_errors[name]
+            gc.collect()
+            if cuda:
+                torch.cuda.empty_cache()
+            return None
+        finally:
+            phase_s[name] = round(time.time() - t0, 1)
+
+    # ---- after the timed region: diagnostics of the multi-rank run (none of this is in `value`),
+    # cheapest and safest first; the xGMI child job (a first contact with cross-device IPC) last
+    if multi and args.coll_sweep_mb:
+        coll = phase("collectives", lambda: collective_sweep(args, torch, dist, device, world, cuda))
+        if coll is not None and rank == 0:
+            rec["collectives"] = coll
+    if multi and args.bucket_sweep_mb and args.parallel in ("ddp", "zero") and args.tp == 1:
+        sweep = phase("bucket_sweep", lambda: bucket_sweep(args, torch, dist, device, world, rank, cuda))
+        if sweep is not None and rank == 0:
+            rec["bucket_sweep"] = sweep
+    if args.diag_stub == "hang":
+        phase("stub_hang", lambda: time.sleep(10 ** 6))
+    if args.fsdp_mem_steps > 0:
+        mem = phase("fsdp_mem", lambda: fsdp_memory_phase(args, torch, dist, device, world, rank, cuda))
+        gc.collect()
+        mrows = gather([mem["valley"], mem["peak"], mem["ms"]] if mem else [-1.0, -1.0, -1.0])
+        if rank == 0 and all(r[0] >= 0 for r in mrows):
             rec["fsdp_mem"] = {"model": mem["model"], "batch_per_gpu": args.fsdp_mem_batch,
                                "seq_len": args.fsdp_mem_seq, "wrap": f"size>={args.numel_to_wrap}",
-                               "valley_gb_max_rank": round(max(r[3] for r in rows), 2),
-                               "peak_gb_max_rank": round(max(r[4] for r in rows), 2),
-                               "ms_per_step": round(max(r[5] for r in rows), 1),
+                               "valley_gb_max_rank": round(max(r[0] for r in mrows), 2),
+                               "peak_gb_max_rank": round(max(r[1] for r in mrows), 2),
+                               "ms_per_step": round(max(r[2] for r in mrows), 1),
                                "reference_a100x8": {"valley_gb": 8, "peak_gb": 74}}
             rec["fsdp_peak_mem_gb"] = rec["fsdp_mem"]["peak_gb_max_rank"]
-        if diag_errors:
-            rec["diagnostic_errors"] = diag_errors
+    if args.fsdp_mem_steps > 0 and cuda and rank == 0 and world < args.fsdp_mem_world:
+        torch.cuda.empty_cache()
+        mem_one = phase("fsdp_mem_one_rank", lambda: fsdp_mem_one_rank(args), collective=False)
         if mem_one is not None:
             rec["fsdp_mem_one_rank_of_w"] = {"world": mem_one["world"], "valley_gb": mem_one["valley_gib"],
                                              "peak_gb": mem_one["peak_gib"], "method": "rank 0 alone, other ranks a "
                                              "fake process group (tools/fsdp_mem_one_rank.py)",
                                              "reference_a100x8": {"valley_gb": 8, "peak_gb": 74}}
-        print(json.dumps(rec), flush=True)
+    run_child = multi and args.xgmi_child and world <= 8 and (cuda or args.diag_stub.startswith("child-sleep:"))
+    if run_child:
+        gc.collect()
+        if cuda:
+            torch.cuda.empty_cache()
+        remaining = T_START + args.deadline_s - 30 - time.time()
+        timeout = min(args.xgmi_child_timeout, remaining)
+        box = [None]
+        if rank == 0:
+            box[0] = phase("xgmi_child", lambda: xgmi_child_diag(args, world, timeout), collective=False) \
+                if timeout > 10 else None
+            if timeout <= 10:
+                rec.setdefault("diagnostic_errors", {})["xgmi_child"] = "skipped: too close to the deadline"
+        dist.barrier()
+        if rank == 0 and box[0] is not None:
+            rec["xgmi_diag"] = box[0]
+            if "error" in box[0]:
+                rec.setdefault("diagnostic_errors", {})["xgmi_child"] = box[0]["error"]
+    reporter.phase = "report"
+    reporter.emit()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

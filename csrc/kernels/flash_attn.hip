@@ -28,6 +28,10 @@
 //    sequence read as zeros from the range check, with no per-row branches.
 #include "common.h"
 
+#include <ATen/hip/HIPGeneratorImpl.h>
+#include <ATen/hip/PhiloxUtils.cuh>
+#include <ATen/core/DistributionsHelper.h>
+
 #include <climits>
 #include <cstdlib>
 #include <type_traits>
@@ -152,7 +156,24 @@ struct DropCfg {
   uint32_t k0, k1, off;  // seed (low, high word), per-call offset
   int thr;               // keep iff random byte < thr (0..256)
   float scale;           // 256 / thr
+  // Device words {seed lo, seed hi, offset lo, offset hi} (an int64 [2] tensor) that override
+  // k0 / k1 / off when set: the forward's draw from torch's CUDA generator, written by
+  // drop_rng_kernel on the stream, read back by the backward.  Under HIP-graph capture the
+  // generator hands out device pointers refreshed before every replay, so each replay of a
+  // captured step draws a new mask (the values baked into a kernel argument would repeat it).
+  const uint32_t* rng;
 };
+
+// The kernel's effective dropout key / offset (wave-uniform loads of dc.rng when set).
+__device__ __forceinline__ DropCfg resolve_drop(const DropCfg& in) {
+  DropCfg d = in;
+  if (d.rng != nullptr) {
+    d.k0 = d.rng[0];
+    d.k1 = d.rng[1];
+    d.off = d.rng[2];
+  }
+  return d;
+}
 
 __device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -323,6 +344,7 @@ constexpr int kFwdBK = 64;   // keys per K/V tile
 // term folds to a compile-time 0 and the kernel is the plain causal one.
 template <int D, bool CAUSAL, bool WIDE, bool QLDS, bool WIN = false, bool DROP = false>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
+  [[maybe_unused]] const DropCfg dcfg = DROP ? resolve_drop(P.drop) : P.drop;
   constexpr int RB = 2 * D;
   constexpr int TILE = kFwdBK * RB;
   constexpr int NC = D / 16;  // k-steps over head_dim
@@ -456,7 +478,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       l += rs;  // the softmax normaliser counts every probability, dropped or not
       if constexpr (DROP) {
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) drop_row_half(P.drop, s0, qrow, head, kt0 + 32 * kt, h, s[kt]);
+        for (int kt = 0; kt < 2; ++kt) drop_row_half(dcfg, s0, qrow, head, kt0 + 32 * kt, h, s[kt]);
       }
       bf16x8 pf[4];
 #pragma unroll
@@ -606,6 +628,7 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restri
 // delta = rowsum(dO * O) for its rows, which bwd_dkdv_kernel (launched after it) reads.
 template <int D, bool CAUSAL, int OCC, bool WIN = false, bool PRE_DELTA = false, bool DROP = false>
 __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
+  [[maybe_unused]] const DropCfg dcfg = DROP ? resolve_drop(P.drop) : P.drop;
   constexpr int RB = 2 * D;
   constexpr int TILE = kDqBK * RB;
   constexpr int NC = D / 16;
@@ -725,9 +748,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     }
     if constexpr (DROP) {  // dS = P o (M dP_dropped / keep - delta); delta = rowsum(dO o O) still holds
       f32x16 z = dp;
-      drop_row_half(P.drop, s0, qrow, head, key0, h, z);
+      drop_row_half(dcfg, s0, qrow, head, key0, h, z);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] *= z[i] * P.drop.scale - delta;
+      for (int i = 0; i < 16; ++i) s[i] *= z[i] * dcfg.scale - delta;
     } else {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] *= dp[i] - delta;  // dS^T / scale
@@ -816,6 +839,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
 // while a wave does its VALU, so the overlap has to come from the wave's own instruction stream.
 template <int D, bool CAUSAL, int PF, bool WIN = false, int QB = kKvBQ, bool DROP = false>
 __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdParams P) {
+  [[maybe_unused]] const DropCfg dcfg = DROP ? resolve_drop(P.drop) : P.drop;
   static_assert(QB == 32 || QB == 64, "query rows per item");
   constexpr int RB = 2 * D;
   constexpr int NC = D / 16;
@@ -907,16 +931,16 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void bwd_dkdv_kernel(BwdPara
   auto drop_cols = [&](int qsu, int hqi, f32x16& s, f32x16& dp, const float* cnd) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      uint32_t c[4] = {(uint32_t)(key & ~3), (uint32_t)(s0 + qsu + 8 * g + 4 * h), (uint32_t)hqi, P.drop.off};
-      philox4x32_10(c, P.drop.k0, P.drop.k1);
+      uint32_t c[4] = {(uint32_t)(key & ~3), (uint32_t)(s0 + qsu + 8 * g + 4 * h), (uint32_t)hqi, dcfg.off};
+      philox4x32_10(c, dcfg.k0, dcfg.k1);
       const int sh = 8 * (key & 3);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int i = 4 * g + e;
-        const bool keep = (int)((c[e] >> sh) & 255u) < P.drop.thr;
+        const bool keep = (int)((c[e] >> sh) & 255u) < dcfg.thr;
         const float p = s[i];
-        dp[i] = p * ((keep ? dp[i] * P.drop.scale : 0.f) + cnd[acc_row(i, h)]);
-        s[i] = keep ? p * P.drop.scale : 0.f;
+        dp[i] = p * ((keep ? dp[i] * dcfg.scale : 0.f) + cnd[acc_row(i, h)]);
+        s[i] = keep ? p * dcfg.scale : 0.f;
       }
     }
   };
@@ -1387,10 +1411,8 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   // (profiles/r3_s04): SLOWER -- 8B shape 0.737 -> 0.803 ms, rime 0.320 -> 0.342, 2 x 8192
   // 4.22 -> 4.40 -- the pair contends for LDS bandwidth and L2 more than it gains in issue
   // overlap; kept as an option, not the default.
-  static const bool conc = [] {
-    const char* e = std::getenv("DTG_FA_BWD_CONC");
-    return e != nullptr && e[0] == '1';
-  }();
+  const char* conc_env = std::getenv("DTG_FA_BWD_CONC");  // per call: tests switch it in-process
+  const bool conc = conc_env != nullptr && conc_env[0] == '1';
   const bool concurrent = conc && P.window == 0;
   hipStream_t main_st = stream(), dq_st = main_st;
   if (concurrent) {
@@ -1595,20 +1617,30 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_varlen_bwd(
   return {dq, dk, dv};
 }
 
-// Attention-probability dropout (GPT-2 attn_pdrop): p, Philox seed and per-call offset; the
-// backward regenerates the same keep mask (see fa::DropCfg).
+// Attention-probability dropout (GPT-2 attn_pdrop): p and the Philox key / offset of this call as
+// an int64 [2] device tensor {seed, offset} (dtg::philox_rng draws it from torch's CUDA generator,
+// graph-safe); the backward regenerates the same keep mask from the same tensor (see fa::DropCfg).
+static fa::DropCfg make_drop_dev(double p, const at::Tensor& rng, const at::Tensor& like) {
+  DTG_CHECK(rng.is_cuda() && rng.scalar_type() == at::kLong && rng.numel() == 2 && rng.is_contiguous() &&
+                rng.device() == like.device(),
+            "flash_attn dropout: rng must be a contiguous int64 [2] tensor {seed, offset} on the inputs' device");
+  fa::DropCfg d = make_drop(p, 0, 0);
+  d.rng = reinterpret_cast<const uint32_t*>(rng.data_ptr<int64_t>());
+  return d;
+}
+
 std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_drop(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                                        const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale,
-                                                       bool causal, double p, int64_t seed, int64_t offset) {
-  const fa::DropCfg d = make_drop(p, seed, offset);
+                                                       bool causal, double p, const at::Tensor& rng) {
+  const fa::DropCfg d = make_drop_dev(p, rng, q);
   return flash_attn_fwd_impl(q, k, v, cu_seqlens, max_seqlen, scale, causal, nullptr, nullptr, nullptr, 0, &d);
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd_drop(
     const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
     const at::Tensor& lse, const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale, bool causal, double p,
-    int64_t seed, int64_t offset) {
-  const fa::DropCfg d = make_drop(p, seed, offset);
+    const at::Tensor& rng) {
+  const fa::DropCfg d = make_drop_dev(p, rng, q);
   auto dq = at::empty(q.sizes(), q.options());
   auto dk = at::empty(k.sizes(), k.options());
   auto dv = at::empty(v.sizes(), v.options());
@@ -1620,9 +1652,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd_drop(
 at::Tensor flash_attn_bwd_qkv_drop(const at::Tensor& dout, const at::Tensor& qkv, int64_t nq, int64_t nkv,
                                    int64_t head_dim, const at::Tensor& o, const at::Tensor& lse,
                                    const at::Tensor& cu_seqlens, int64_t max_seqlen, double scale, bool causal,
-                                   double p, int64_t seed, int64_t offset) {
+                                   double p, const at::Tensor& rng) {
   DTG_CHECK_CUDA_BF16(qkv);
-  const fa::DropCfg d = make_drop(p, seed, offset);
+  const fa::DropCfg d = make_drop_dev(p, rng, qkv);
   const int64_t T = qkv.size(0), D = head_dim;
   DTG_CHECK(qkv.dim() == 2 && qkv.size(1) == (nq + 2 * nkv) * D && qkv.stride(1) == 1,
             "flash_attn_bwd_qkv_drop: qkv must be [T, (nq + 2 nkv) * D]");
@@ -1636,10 +1668,39 @@ at::Tensor flash_attn_bwd_qkv_drop(const at::Tensor& dout, const at::Tensor& qkv
   return dqkv;
 }
 
+// {seed, offset} of one dropout call from torch's CUDA generator for `like`'s device, written into
+// a fresh int64 [2] device tensor by a one-lane kernel on the current stream.  Outside capture the
+// generator hands out values; under HIP-graph capture it hands out pointers to its seed and to an
+// offset it advances before every replay, so the captured unpack yields a new offset each replay.
+__global__ void philox_rng_kernel(at::PhiloxCudaState st, int64_t* out) {
+  if (threadIdx.x == 0) {
+    const auto so = at::cuda::philox::unpack(st);
+    out[0] = static_cast<int64_t>(std::get<0>(so));
+    out[1] = static_cast<int64_t>(std::get<1>(so));
+  }
+}
+
+at::Tensor philox_rng(const at::Tensor& like, int64_t increment) {
+  DTG_CHECK(like.is_cuda(), "philox_rng: needs a GPU tensor");
+  const c10::DeviceGuard g(like.device());
+  auto gen = at::get_generator_or_default<at::CUDAGeneratorImpl>(
+      std::nullopt, at::cuda::detail::getDefaultCUDAGenerator(like.device().index()));
+  at::PhiloxCudaState st;
+  {
+    std::lock_guard<std::mutex> lock(gen->mutex_);
+    st = gen->philox_cuda_state(static_cast<uint64_t>(std::max<int64_t>(4, increment)));
+  }
+  auto out = at::empty({2}, like.options().dtype(at::kLong));
+  philox_rng_kernel<<<1, 64, 0, stream()>>>(st, out.data_ptr<int64_t>());
+  DTG_LAUNCH_CHECK();
+  return out;
+}
+
 TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
   m.impl("flash_attn_fwd_drop", &flash_attn_fwd_drop);
   m.impl("flash_attn_bwd_drop", &flash_attn_bwd_drop);
   m.impl("flash_attn_bwd_qkv_drop", &flash_attn_bwd_qkv_drop);
+  m.impl("philox_rng", &philox_rng);
   m.impl("flash_attn_varlen_fwd", &flash_attn_varlen_fwd);
   m.impl("flash_attn_varlen_bwd", &flash_attn_varlen_bwd);
   m.impl("flash_attn_fwd", &flash_attn_fwd);

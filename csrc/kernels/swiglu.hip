@@ -29,17 +29,14 @@ __global__ void swiglu_fwd_kernel(const uint16_t* __restrict__ gu, int64_t gu_st
   store8(h + t * I + c, o);
 }
 
-// h != nullptr: also writes h = silu(g) * u (the token-major operand of dW_down for the
-// token-major weight-gradient GEMM, csrc/kernels/dw_gemm.hip) in the same pass.
 __global__ void swiglu_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_t* __restrict__ gu,
-                                  int64_t gu_stride, uint16_t* __restrict__ dgu, int64_t T, int I,
-                                  uint16_t* __restrict__ h = nullptr) {
+                                  int64_t gu_stride, uint16_t* __restrict__ dgu, int64_t T, int I) {
   const int chunks = I >> 3;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= T * chunks) return;
   const int64_t t = gid / chunks;
   const int c = (gid % chunks) * 8;
-  float g[8], u[8], d[8], dg[8], du[8], hv[8];
+  float g[8], u[8], d[8], dg[8], du[8];
   load8(gu + t * gu_stride + c, g);
   load8(gu + t * gu_stride + I + c, u);
   load8(dh + t * I + c, d);
@@ -49,11 +46,9 @@ __global__ void swiglu_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_
     const float silu = g[j] * s;
     du[j] = d[j] * silu;
     dg[j] = d[j] * u[j] * s * (1.f + g[j] * (1.f - s));
-    hv[j] = silu * u[j];
   }
   store8(dgu + t * 2 * I + c, dg);
   store8(dgu + t * 2 * I + I + c, du);
-  if (h != nullptr) store8(h + t * I + c, hv);
 }
 
 // Backward that also emits the operands of the MLP's weight-gradient GEMMs in K-contiguous
@@ -229,28 +224,7 @@ at::Tensor swiglu_bwd(const at::Tensor& dh_, const at::Tensor& gu) {
   return dgu;
 }
 
-std::tuple<at::Tensor, at::Tensor> swiglu_bwd_h(const at::Tensor& dh_, const at::Tensor& gu) {
-  auto dh = dh_.contiguous();
-  DTG_CHECK_CUDA_BF16(gu);
-  DTG_CHECK_CUDA_BF16(dh);
-  DTG_CHECK(gu.dim() == 2 && gu.stride(1) == 1 && gu.stride(0) % 8 == 0 && gu.size(1) % 16 == 0,
-            "swiglu_bwd_h: gu must be [T, 2I] with I % 8 == 0");
-  const int64_t T = gu.size(0);
-  const int I = gu.size(1) / 2;
-  DTG_CHECK(dh.size(0) == T && dh.size(1) == I, "swiglu_bwd_h: shape mismatch");
-  const c10::DeviceGuard g(gu.device());
-  auto dgu = at::empty({T, 2 * I}, gu.options());
-  auto h = at::empty({T, I}, gu.options());
-  const int64_t n = T * (I / 8);
-  if (n == 0) return {dgu, h};
-  swiglu_bwd_kernel<<<(n + 255) / 256, 256, 0, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0),
-                                                           bf16_mut(dgu), T, I, bf16_mut(h));
-  DTG_LAUNCH_CHECK();
-  return {dgu, h};
-}
-
 TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
-  m.impl("swiglu_bwd_h", &swiglu_bwd_h);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("swiglu_bwd_t", &swiglu_bwd_t);

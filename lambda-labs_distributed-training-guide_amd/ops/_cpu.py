@@ -261,8 +261,21 @@ def _drop_masks(cu_seqlens, hq, p, seed, offset):
     return out
 
 
-def flash_attn_fwd_drop(q, k, v, cu_seqlens, max_seqlen, scale, causal, p, seed, offset):
+def _rng_pair(rng):
+    seed, offset = (int(x) for x in rng.reshape(-1).tolist())
+    return seed, offset
+
+
+def philox_rng(like, increment):
+    """{seed, offset} of one dropout call from torch's CPU generator (reproducible under
+    torch.manual_seed, checkpointed with the RNG state)."""
+    r = torch.randint(0, 2**62, (2,))
+    return torch.tensor([int(r[0]), int(r[1] % (2**31))], dtype=torch.int64)
+
+
+def flash_attn_fwd_drop(q, k, v, cu_seqlens, max_seqlen, scale, causal, p, rng):
     """o = (M o softmax(S) * 256/thr) V per sequence; lse of the undropped softmax."""
+    seed, offset = _rng_pair(rng)
     _check_attn_inputs(q, k, v)
     T, hq, d = q.shape
     rep = hq // k.shape[1]
@@ -285,7 +298,8 @@ def flash_attn_fwd_drop(q, k, v, cu_seqlens, max_seqlen, scale, causal, p, seed,
     return o.to(q.dtype), lse
 
 
-def flash_attn_bwd_drop(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, p, seed, offset):
+def flash_attn_bwd_drop(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, p, rng):
+    seed, offset = _rng_pair(rng)
     _check_attn_inputs(q, k, v)
     T, hq, d = q.shape
     hkv = k.shape[1]
@@ -317,14 +331,13 @@ def flash_attn_bwd_drop(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, ca
     return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
 
 
-def flash_attn_bwd_qkv_drop(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal, p, seed,
-                            offset):
+def flash_attn_bwd_qkv_drop(dout, qkv, nq, nkv, head_dim, o, lse, cu_seqlens, max_seqlen, scale, causal, p, rng):
     T = qkv.shape[0]
     d = head_dim
     q = qkv[:, : nq * d].reshape(T, nq, d)
     k = qkv[:, nq * d : (nq + nkv) * d].reshape(T, nkv, d)
     v = qkv[:, (nq + nkv) * d :].reshape(T, nkv, d)
-    dq, dk, dv = flash_attn_bwd_drop(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, p, seed, offset)
+    dq, dk, dv = flash_attn_bwd_drop(dout, q, k, v, o, lse, cu_seqlens, max_seqlen, scale, causal, p, rng)
     return torch.cat([dq.reshape(T, -1), dk.reshape(T, -1), dv.reshape(T, -1)], dim=1)
 
 
@@ -403,15 +416,6 @@ def swiglu_bwd_t(dh, gu):
     return dgu, dgu.t().contiguous(), swiglu_fwd(gu).t().contiguous()
 
 
-def swiglu_bwd_h(dh, gu):
-    return swiglu_bwd(dh, gu), swiglu_fwd(gu)
-
-
-def dw_gemm_(a, b, c, accumulate):
-    r = a.float().t() @ b.float()
-    c.copy_((r + c.float()) if accumulate else r)
-
-
 def transpose2d(x):
     return x.t().contiguous()
 
@@ -435,7 +439,7 @@ for _name, _fn in list(globals().items()):
         "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "adamw_t_", "flash_attn_fwd", "flash_attn_bwd",
         "flash_attn_bwd_qkv", "transpose2d", "transpose_mats_", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
-        "flash_attn_varlen_bwd", "flash_attn_fwd_drop", "flash_attn_bwd_drop", "flash_attn_bwd_qkv_drop",
-        "swiglu_bwd_h", "dw_gemm_", "flash_attn_bwd_qkv_rope",
+        "flash_attn_varlen_bwd", "flash_attn_fwd_drop", "flash_attn_bwd_drop", "flash_attn_bwd_qkv_drop", "philox_rng",
+        "flash_attn_bwd_qkv_rope",
     ):
         LIB.impl(_name, _fn, "CPU")

@@ -41,22 +41,20 @@ _DEFS = [
     "flash_attn_bwd_qkv_rope(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
     "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, Tensor cos, Tensor sin, Tensor pos, "
     "int window=0) -> Tensor",
-    # attention-probability dropout regenerated from Philox(seed, offset) in the backward
+    # attention-probability dropout regenerated from Philox(seed, offset) in the backward; `rng` is
+    # the int64 [2] tensor {seed, offset} of the call (philox_rng: torch's generator, graph-safe)
     "flash_attn_fwd_drop(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, bool causal, "
-    "float p, int seed, int offset) -> (Tensor, Tensor)",
+    "float p, Tensor rng) -> (Tensor, Tensor)",
     "flash_attn_bwd_drop(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor cu_seqlens, "
-    "int max_seqlen, float scale, bool causal, float p, int seed, int offset) -> (Tensor, Tensor, Tensor)",
+    "int max_seqlen, float scale, bool causal, float p, Tensor rng) -> (Tensor, Tensor, Tensor)",
     "flash_attn_bwd_qkv_drop(Tensor dout, Tensor qkv, int nq, int nkv, int head_dim, Tensor o, Tensor lse, "
-    "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, float p, int seed, int offset) -> Tensor",
+    "Tensor cu_seqlens, int max_seqlen, float scale, bool causal, float p, Tensor rng) -> Tensor",
+    "philox_rng(Tensor like, int increment) -> Tensor",
     "transpose2d(Tensor x) -> Tensor",
     # many matrices of a flat buffer transposed in one launch: rows of `mats` (int64 [n, 5]:
     # source offset, rows, cols, destination offset, first 64 x 64 tile); `mats_host` = its CPU copy
     "transpose_mats_(Tensor x, Tensor(a!) out, Tensor mats, Tensor mats_host, int ntiles) -> ()",
     "embedding_bwd_(Tensor(a!) out, Tensor ids, Tensor dy) -> ()",
-    # weight-gradient GEMM over token-major operands: c (=|+=) a^T @ b, a [K, M], b [K, N]
-    "dw_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()",
-    # SwiGLU backward that also returns h = silu(g) * u (token-major operand of dW_down)
-    "swiglu_bwd_h(Tensor dh, Tensor gu) -> (Tensor, Tensor)",
     # FlashAttention-2-style varlen with explicit per-sequence key ranges (disjoint), causal mask
     # bottom-right aligned: context parallelism's local query chunks over gathered key prefixes
     "flash_attn_varlen_fwd(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens_q, Tensor k_start, Tensor k_len, "

@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import grad_routing as _gr
-from .grad_routing import route_embedding_grad, route_param_grad, route_weight_grad_hand, route_weight_grad_mm
+from .grad_routing import route_embedding_grad, route_param_grad, route_weight_grad_mm
 
 ops = torch.ops.dtg
 
@@ -31,17 +31,6 @@ ops = torch.ops.dtg
 # native 24.3k, auto 27.0k, tn 27.0-27.1k -- "tn" is the default.
 _LINEAR_BWD = os.environ.get("DTG_LINEAR_BWD", "tn")
 _TN_MIN_TOKENS = 4096
-# DTG_DW_GEMM=1: weight gradients by the hand-written token-major GEMM (csrc/kernels/dw_gemm.hip)
-# on dY and X as they are -- no transposes, and the MLP backward writes dgu and h row-major
-# (swiglu_bwd_h) instead of dgu, dgu^T and h^T.  Shapes that are not 256 x 256 x 64 tile
-# multiples keep the hipBLASLt path.
-_DW_GEMM = os.environ.get("DTG_DW_GEMM", "0") == "1"
-
-
-def _dw_hand_ok(w, *ts):
-    return (_DW_GEMM and w.shape[0] % 256 == 0 and w.shape[1] % 256 == 0
-            and all(t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.shape[0] % 64 == 0
-                    and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in ts))
 
 
 def _tn_ok(*ts):
@@ -86,9 +75,7 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy, _wt(w).t()) if dx_tn else torch.mm(dy, w)
         if ctx.needs_input_grad[1]:
-            if _dw_hand_ok(w, dy, x):
-                dw = route_weight_grad_hand(w, dy, x)
-            elif dw_tn and _tn_ok(dy):
+            if dw_tn and _tn_ok(dy):
                 dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
             else:
                 dw = route_weight_grad_mm(w, dy, x)
@@ -118,9 +105,7 @@ class _LinearBias(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy, _wt(w).t()) if dx_tn else torch.mm(dy, w)
         if ctx.needs_input_grad[1]:
-            if _dw_hand_ok(w, dy, x):
-                dw = route_weight_grad_hand(w, dy, x)
-            elif dw_tn and _tn_ok(dy):
+            if dw_tn and _tn_ok(dy):
                 dw = route_weight_grad_mm(w, dy, x, a_t=ops.transpose2d(dy), b_t=ops.transpose2d(x))
             else:
                 dw = route_weight_grad_mm(w, dy, x)
@@ -254,35 +239,36 @@ class _AttentionQKV(torch.autograd.Function):
 class _AttentionQKVDrop(torch.autograd.Function):
     """Attention with dropout on the probabilities, inside the flash kernels: the keep mask is a
     counter-based (Philox) function of (seed, offset, head, query, key), drawn in the forward and
-    regenerated in the backward -- nothing [S, S] is stored."""
+    regenerated in the backward -- nothing [S, S] is stored.  {seed, offset} is a device tensor
+    drawn from torch's CUDA generator (ops.philox_rng), so a captured HIP graph draws a new mask
+    every replay (a Python int would be baked into the graph)."""
 
     @staticmethod
-    def forward(ctx, qkv, cu_seqlens, max_seqlen, nq, nkv, head_dim, scale, causal, p, seed, offset):
+    def forward(ctx, qkv, cu_seqlens, max_seqlen, nq, nkv, head_dim, scale, causal, p, rng):
         T = qkv.shape[0]
         d = head_dim
         q = qkv.as_strided((T, nq, d), (qkv.stride(0), d, 1), qkv.storage_offset())
         k = qkv.as_strided((T, nkv, d), (qkv.stride(0), d, 1), qkv.storage_offset() + nq * d)
         v = qkv.as_strided((T, nkv, d), (qkv.stride(0), d, 1), qkv.storage_offset() + (nq + nkv) * d)
-        o, lse = ops.flash_attn_fwd_drop(q, k, v, cu_seqlens, max_seqlen, scale, causal, p, seed, offset)
-        ctx.save_for_backward(qkv, o, lse, cu_seqlens)
-        ctx.meta = (max_seqlen, nq, nkv, d, scale, causal, p, seed, offset)
+        o, lse = ops.flash_attn_fwd_drop(q, k, v, cu_seqlens, max_seqlen, scale, causal, p, rng)
+        ctx.save_for_backward(qkv, o, lse, cu_seqlens, rng)
+        ctx.meta = (max_seqlen, nq, nkv, d, scale, causal, p)
         return o.view(T, nq * d)
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse, cu = ctx.saved_tensors
-        max_seqlen, nq, nkv, d, scale, causal, p, seed, offset = ctx.meta
+        qkv, o, lse, cu, rng = ctx.saved_tensors
+        max_seqlen, nq, nkv, d, scale, causal, p = ctx.meta
         T = qkv.shape[0]
         dqkv = ops.flash_attn_bwd_qkv_drop(do.contiguous().view(T, nq, d), qkv, nq, nkv, d, o, lse, cu, max_seqlen,
-                                           scale, causal, p, seed, offset)
-        return dqkv, None, None, None, None, None, None, None, None, None, None
+                                           scale, causal, p, rng)
+        return dqkv, None, None, None, None, None, None, None, None, None
 
 
-def dropout_seed_offset(generator=None):
-    """(seed, offset) of one dropout call, from torch's CPU generator (host only, no device sync;
-    reproducible under torch.manual_seed and checkpointed with the RNG state)."""
-    r = torch.randint(0, 2**62, (2,), generator=generator)
-    return int(r[0]), int(r[1] % (2**31))
+def dropout_rng(like):
+    """{seed, offset} (int64 [2] on `like`'s device) of one attention-dropout call: torch's CUDA
+    generator on a GPU (graph-safe), its CPU generator on the CPU reference path."""
+    return ops.philox_rng(like, 4)
 
 
 class _Rope(torch.autograd.Function):
@@ -349,9 +335,8 @@ def attention(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos=None, sin=None
             raise ValueError("attention dropout is supported without RoPE / sliding windows (GPT-2)")
         if qkv.is_cuda and head_dim not in FA_HEAD_DIMS:
             raise ValueError(f"attention dropout: head_dim {head_dim} needs a kernel instantiation {FA_HEAD_DIMS}")
-        seed, offset = dropout_seed_offset()
         return _AttentionQKVDrop.apply(qkv, cu_seqlens, int(max_seqlen), nq, nkv, head_dim, float(scale), causal,
-                                       float(dropout_p), seed, offset)
+                                       float(dropout_p), dropout_rng(qkv))
     if qkv.is_cuda and head_dim not in FA_HEAD_DIMS:  # the CPU reference takes any width
         return _attention_padded(qkv, nq, nkv, head_dim, cu_seqlens, max_seqlen, cos, sin, pos, causal, scale, window)
     rope = cos is not None
@@ -404,16 +389,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         dy = dy.contiguous()
         dx_tn, dw_tn = _bwd_layout(x, w_gu)
         fused = dw_tn and _tn_ok(dy, gu) and gu.stride(0) == gu.shape[1]
-        hand = _dw_hand_ok(w_down, dy, x, gu) and _dw_hand_ok(w_gu)
         dh = torch.mm(dy, _wt(w_down).t()) if dx_tn else torch.mm(dy, w_down)
-        if hand:
-            dgu, h = ops.swiglu_bwd_h(dh, gu)
-            del dh
-            dw_down = route_weight_grad_hand(w_down, dy, h)
-            del h
-            dx = torch.mm(dgu, _wt(w_gu).t()) if dx_tn else torch.mm(dgu, w_gu)
-            dw_gu = route_weight_grad_hand(w_gu, dgu, x)
-            return dx, dw_gu, dw_down, None
         if fused:
             dgu, dgu_t, h_t = ops.swiglu_bwd_t(dh, gu)
             del dh

@@ -7,40 +7,7 @@ Functions compute a weight gradient straight into `main_grad` -- the first contr
 step writes (`out=`), later ones (tied embeddings, gradient accumulation) add -- and return
 None to autograd.  Parameters without `main_grad` get an ordinary gradient.
 """
-import os
-
 import torch
-
-# Weight-gradient GEMMs on a side stream (DTG_DW_STREAM=1).  In a backward the dX GEMMs and the
-# streaming kernels between them (norm / SwiGLU / attention backward, transposes) form the
-# critical path; every dW GEMM hangs off it and is needed only by the gradient collective or the
-# optimizer.  Issued on a second stream, the dW GEMMs can fill the chip while the critical path
-# runs bandwidth-bound kernels.  Operands are recorded on the side stream (the caching allocator
-# does not reuse them early); consumers of the gradients join the stream first (join_dw).
-# Only PRIVATE operands may be read there -- the TN path's fresh transposed copies: dY itself is
-# also the residual stream's gradient, into which autograd later accumulates the norm branch's
-# contribution IN PLACE on the main stream (InputBuffer steals the buffer), so a delayed GEMM
-# reading dY directly sees the sum (tests/test_dw_stream_gpu.py caught exactly that with a spin
-# ahead of every side-stream GEMM).  Shared operands keep the GEMM on the main stream.
-_DW_STREAM = os.environ.get("DTG_DW_STREAM", "0") == "1"
-_dw_streams = {}
-
-
-def dw_stream(device):
-    s = _dw_streams.get(device)
-    if s is None:
-        s = _dw_streams[device] = torch.cuda.Stream(device=device)
-    return s
-
-
-def join_dw(device=None):
-    """The current stream waits for every weight-gradient GEMM issued so far."""
-    if not _dw_streams:
-        return
-    for dev, s in _dw_streams.items():
-        if device is None or torch.device(device) == dev:
-            torch.cuda.current_stream(dev).wait_stream(s)
-
 
 # When an engine owns the loss (it back-propagates the loss with an implicit gradient of 1 and
 # folds any scaling into the optimizer's grad_scale), the fused loss head writes the lm_head
@@ -126,20 +93,6 @@ def notify_param(param):
     _mark(param)
 
 
-def route_weight_grad_hand(param, a, b):
-    """Weight gradient a^T @ b by the token-major hand GEMM (torch.ops.dtg.dw_gemm_, no
-    transposes), straight into main_grad (accumulating after the first micro-batch)."""
-    mg = getattr(param, "main_grad", None)
-    if mg is None:
-        out = torch.empty(a.shape[1], b.shape[1], dtype=a.dtype, device=a.device)
-        torch.ops.dtg.dw_gemm_(a, b, out, False)
-        return out
-    # main stream only: a and b are the shared dY / X (see the side-stream note above)
-    torch.ops.dtg.dw_gemm_(a, b, mg, not _fresh(param))
-    _mark(param)
-    return None
-
-
 def route_weight_grad_mm(param, a, b, a_t=None, b_t=None):
     """Weight gradient a^T @ b (a: [T, out], b: [T, in]) into main_grad without a temporary.
 
@@ -153,17 +106,7 @@ def route_weight_grad_mm(param, a, b, a_t=None, b_t=None):
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return lhs @ rhs
-    if _DW_STREAM and mg.is_cuda and a_t is not None and b_t is not None:
-        s = dw_stream(mg.device)
-        s.wait_stream(torch.cuda.current_stream(mg.device))
-        with torch.cuda.stream(s):
-            if _fresh(param):
-                torch.mm(lhs, rhs, out=mg)
-            else:
-                mg.addmm_(lhs, rhs)
-        for t in (lhs, rhs):
-            t.record_stream(s)
-    elif _fresh(param):
+    if _fresh(param):
         torch.mm(lhs, rhs, out=mg)
     else:
         mg.addmm_(lhs, rhs)

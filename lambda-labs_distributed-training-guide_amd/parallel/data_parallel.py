@@ -47,7 +47,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.adamw import adamw_step
-from ..ops.grad_routing import join_dw, reset_grad_state, set_direct_loss_grad
+from ..ops.grad_routing import reset_grad_state, set_direct_loss_grad
 from ..utils import comm
 from .flat import FlatSpace, rebind_parameters
 
@@ -308,7 +308,6 @@ class DataParallel:
         if b.launched:
             return
         b.launched = True
-        join_dw(self.space.grad_buf.device)  # weight-gradient GEMMs on the side stream (DTG_DW_STREAM)
         if b.trailing:
             self._reduce_sp()
         view = self.space.grad_buf[b.start:b.end]
@@ -363,7 +362,6 @@ class DataParallel:
 
     def finish_grad_sync(self):
         """Call after backward (the last micro-batch): flush unlaunched buckets, wait for all."""
-        join_dw(self.space.grad_buf.device)
         if self.mode == "single" and not self.overlap_optimizer and self._sync_enabled:
             self._reduce_sp()
         if (self.mode != "single" or self.overlap_optimizer) and self._sync_enabled:
@@ -381,7 +379,6 @@ class DataParallel:
 
     def backward(self, loss):
         loss.backward()
-        join_dw(self.space.grad_buf.device)
         self.accum_count += 1
         if self._sync_enabled:
             self.finish_grad_sync()
@@ -405,7 +402,6 @@ class DataParallel:
             out.copy_(self.space.param_buf)
 
     def step(self, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, grad_scale=None):
-        join_dw(self.space.grad_buf.device)
         if self._bwd_stepped:  # overlap_optimizer: every bucket was updated during backward
             assert all(b.stepped for b in self.space.buckets), "a bucket missed its in-backward update"
             if self._opt_stream is not None:

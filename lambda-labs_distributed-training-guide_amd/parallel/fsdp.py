@@ -40,7 +40,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.adamw import adamw_step
-from ..ops.grad_routing import join_dw, reset_grad_state, set_direct_loss_grad
+from ..ops.grad_routing import reset_grad_state, set_direct_loss_grad
 from ..utils import comm
 
 ALIGN = 16
@@ -314,7 +314,7 @@ class FullyShard:
         self.accum_count = 0
         self._sync_enabled = True
         self._first_micro = True
-        self._final_micro = True
+        self._final_micro = None  # set by backward(); None = derive from no_sync() (external callers)
         set_direct_loss_grad(True)
 
     # ------------------------------------------------------------------ memory helpers
@@ -459,7 +459,6 @@ class FullyShard:
         if u.rs_launched:
             return
         u.rs_launched = True
-        join_dw(self.device)  # weight-gradient GEMMs on the side stream (DTG_DW_STREAM)
         # zero the padding / never-written params so the reduce-scatter sums only real grads
         for i, p in enumerate(u.params):
             if not getattr(p, "_dtg_grad_written", False):
@@ -491,7 +490,8 @@ class FullyShard:
         if work is not None:
             work.wait()
         merged = False
-        if self.replicas > 1 and self._final_micro:
+        final = (not self._in_no_sync) if self._final_micro is None else self._final_micro
+        if self.replicas > 1 and final:
             # HYBRID: the shard summed over the replicas once per optimizer step, on the last
             # micro-batch: earlier micro-batches accumulate locally (no inter-replica traffic)
             # and their sum joins this micro-batch's shard before the one all-reduce.  RCCL:
@@ -645,11 +645,11 @@ class FullyShard:
         ok = False
         try:
             loss.backward()
-            join_dw(self.device)
             self.accum_count += 1
             self.finish_grad_sync()
             ok = True
         finally:
+            self._final_micro = None  # a caller driving loss.backward() itself derives it from no_sync()
             snap, self._bwd_step = self._bwd_step, None
             if not ok and self._cpu_futs:
                 # host updates of some units were submitted: let them finish, then refuse to

@@ -34,12 +34,16 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     if chapter == "04":
         p.add_argument("--numel-to-wrap", default=100_000_000, type=int,
                        help="Only applies FSDP to modules with numel > this value.")
-    if chapter in ("04", "05"):
+    if chapter in ("04", "05", "07"):
+        # 07: the 2-D recipe (FSDP over dp x TP over tp) with the 405B offload of chapter 05, so Llama-3.1-405B
+        # fits ONE 8-GPU node (a TP-local 1/8 shard is 406 GB of bf16 state per rank without it)
         p.add_argument("--cpu-offload", default="on" if chapter == "05" else "off", choices=["on", "off"])
+    if chapter in ("04", "05"):
         p.add_argument("--sharding", default="full", choices=["full", "hybrid"],
                        help="full: FULL_SHARD over all ranks; hybrid: shard within --shard-size ranks (one node), "
                             "replicate across nodes (HYBRID_SHARD)")
         p.add_argument("--shard-size", default=None, type=int, help="ranks per shard group (default LOCAL_WORLD_SIZE)")
+    if chapter in ("04", "05", "07"):
         p.add_argument("--offload-params", default="auto", choices=["auto", "on", "off"],
                        help="with --cpu-offload on: on = parameters on the host too (reference); off = parameter "
                             "shard resident in HBM, only gradients + AdamW state offloaded; auto = off when the "
@@ -54,11 +58,12 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     if chapter == "07":
         p.add_argument("--tp", default=8, type=int)
     if chapter in ("06", "07"):
-        p.add_argument("--tp-comm", default="rccl", choices=["rccl", "xgmi", "xgmi-dma"],
+        p.add_argument("--tp-comm", default="auto", choices=["auto", "rccl", "xgmi", "xgmi-dma"],
                        help="TP/SP all-gather / reduce-scatter / all-reduce: RCCL, or the direct-peer xGMI "
                             "library (csrc/comm/xgmi.hip; one node per TP group); xgmi-dma moves the "
                             "all-gathers and reduce-scatters on the copy engines, one stream per peer (no CU "
-                            "time under the overlapped GEMMs)")
+                            "time under the overlapped GEMMs); auto = whichever of the three is fastest at this "
+                            "job's message size on the TP group, timed at startup (parallel/transport.py)")
         p.add_argument("--tp-comm-mb", default=256, type=int, help="xGMI workspace per rank (largest TP message)")
         p.add_argument("--tp-comm-timeout", default=None, type=float,
                        help="seconds an xGMI barrier waits for a peer before the collective fails (default: "
@@ -102,9 +107,10 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                         "parameters after every update (param) or both (on); each check syncs the device")
     g.add_argument("--bucket-mb", default=256, type=int, help="gradient bucket size for DDP/ZeRO")
     if chapter in ("02", "04", "05", "07"):
-        g.add_argument("--dp-comm", default="rccl", choices=["rccl", "xgmi-dma"],
+        g.add_argument("--dp-comm", default="auto", choices=["auto", "rccl", "xgmi-dma"],
                        help="ZeRO / FSDP collectives: RCCL, or copy-engine pulls between the ranks' shared shard / "
-                            "gradient buffers over xGMI (one node; no CU time under the overlapped compute)")
+                            "gradient buffers over xGMI (one node; no CU time under the overlapped compute); "
+                            "auto = the faster of the two at this job's bucket / layer size, timed at startup")
     if chapter == "02":
         g.add_argument("--dp-mode", default="zero", choices=["ddp", "zero"],
                        help="zero: sharded optimizer (reference's ZeroRedundancyOptimizer); ddp: replicated")

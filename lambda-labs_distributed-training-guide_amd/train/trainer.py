@@ -137,6 +137,25 @@ def xgmi_timeout(flag) -> float:
     return float(env) if env is not None else 60.0
 
 
+def _resolve_dp_comm(args, chapter, cfg, device, dp_group, world, fsdp, pp, nseq) -> str:
+    """--dp-comm auto: RCCL vs the copy-engine path, timed on the data-parallel group at this
+    job's message size (ZeRO: one gradient bucket; FSDP: one decoder layer's flat parameters).
+    Only ZeRO and FSDP have a copy-engine path; everything else is RCCL without measuring."""
+    zero = chapter == "02" and getattr(args, "dp_mode", "zero") == "zero" and pp == 1 and nseq == 1
+    if device.type != "cuda" or world == 1 or not (zero or fsdp) or getattr(args, "cpu_offload", "off") == "on":
+        return "rccl"
+    from ..parallel import transport
+
+    if zero:  # one gradient bucket (a model smaller than a bucket is one bucket)
+        msg = min(args.bucket_mb << 20, 2 * cfg.num_params())
+    else:
+        tp = max(1, getattr(args, "tp", 1)) if chapter == "07" else 1
+        emb = cfg.vocab_size * cfg.hidden_size * (1 if getattr(cfg, "tie_word_embeddings", False) else 2)
+        msg = 2 * ((cfg.num_params() - emb) // max(1, cfg.num_hidden_layers)) // tp
+    choice, args.dp_comm_calibration = transport.resolve("auto", "dp", dp_group, device, msg, log=LOGGER.info)
+    return choice
+
+
 def _build(args, chapter, device, world):
     """Model + engine + optimizer for a chapter.  Returns (model, engine, dp_size, dp_rank, ckpt_style)."""
     depth = getattr(args, "num_layers", None)
@@ -152,6 +171,13 @@ def _build(args, chapter, device, world):
         tp = max(1, min(tp, world))
         dp_group, tp_group, dp_rank, tp_rank, dp_size = make_mesh(tp)
         LOGGER.info(f"mesh: dp={dp_size} tp={tp} (dp_rank={dp_rank}, tp_rank={tp_rank})")
+        if getattr(args, "tp_comm", "rccl") == "auto" and tp_group is not None:
+            from ..parallel import transport
+
+            chunks = max(1, getattr(args, "tp_overlap_chunks", 2))
+            msg = transport.tp_message_bytes(args.batch_size, args.seq_length, cfg.hidden_size) // chunks
+            args.tp_comm, args.tp_comm_calibration = transport.resolve(
+                "auto", "tp", tp_group, device, msg, xgmi_timeout(getattr(args, "tp_comm_timeout", None)), LOGGER.info)
         if getattr(args, "tp_comm", "rccl").startswith("xgmi") and tp_group is not None and device.type == "cuda":
             from ..parallel.xgmi import XgmiCommunicator
             from ..utils import comm as _comm
@@ -191,6 +217,8 @@ def _build(args, chapter, device, world):
         replicate_group, dp_group, _, _, n_rep = make_mesh(shard)
         LOGGER.info(f"hybrid sharding: {n_rep} replicas x {shard}-way shards")
     fsdp = chapter in ("04", "05", "07") or (chapter == "deepspeed" and args.zero_stage == 3)
+    if getattr(args, "dp_comm", "rccl") == "auto":
+        args.dp_comm = _resolve_dp_comm(args, chapter, cfg, device, dp_group, world, fsdp, pp, nseq)
     if fsdp:
         with torch.device("meta"):
             model = build_model(cfg, tp_group=tp_group, init=False)

@@ -24,6 +24,10 @@ def _unregister(ptr: int) -> None:
     # Runs when the buffer's STORAGE is freed (the finalizer hangs on the numpy array the storage
     # keeps alive, not on one tensor object whose views may outlive it).  Drain the device first:
     # an asynchronous copy still reading / writing the pages must not see them unpinned.
+    import sys
+
+    if sys.is_finalizing():  # the HIP runtime may already be shutting down: the OS reclaims the pages
+        return
     try:
         if torch.cuda.is_initialized():
             torch.cuda.synchronize()
@@ -48,5 +52,6 @@ def pinned_zeros(n: int, dtype: torch.dtype) -> torch.Tensor:
             raise RuntimeError(f"hipHostRegister returned {int(err)}")
     except Exception:
         return torch.zeros(n, dtype=dtype, pin_memory=True)  # the caching allocator's path
-    weakref.finalize(arr, _unregister, t.data_ptr())
+    fin = weakref.finalize(arr, _unregister, t.data_ptr())
+    fin.atexit = False  # never at interpreter exit (a synchronize then can hang); process exit frees it
     return t

@@ -160,3 +160,65 @@ def test_rccl_log_parse_and_preset():
     applied = rccl.apply_preset("node", env)
     assert env["TORCH_NCCL_HIGH_PRIORITY"] == "0" and "TORCH_NCCL_HIGH_PRIORITY" not in applied
     assert applied["HSA_NO_SCRATCH_RECLAIM"] == "1" and rccl.apply_preset("none", env) == {}
+
+
+@pytest.mark.slow
+def test_bench_child_past_its_budget_still_reports():
+    """the xGMI child job (stubbed: sleeps far past its timeout) is killed at
+    --xgmi-child-timeout; the line still comes out, rc 0, with the child named in
+    diagnostic_errors and every phase's wall time recorded."""
+    import time
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--diag-stub", "child-sleep:1000", "--xgmi-child-timeout", "15", "--deadline-s", "200"] + ARGS
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    took = time.time() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    _check(rec, 2)
+    assert "timed out" in rec["diagnostic_errors"]["xgmi_child"]
+    assert rec["xgmi_diag"]["error"].startswith("xgmi diagnostic child timed out")
+    assert {"throughput", "collectives", "bucket_sweep", "fsdp_mem", "xgmi_child"} <= set(rec["phase_s"])
+    assert 14 <= rec["phase_s"]["xgmi_child"] < 40
+    assert rec["wall_s"] > 0 and took < rec["wall_s"] + 60
+
+
+@pytest.mark.slow
+def test_bench_hung_diagnostic_hits_the_deadline():
+    """A diagnostic that never returns: at --deadline-s the watchdog prints the headline line
+    (with what the diagnostics added so far) and every rank exits 0."""
+    import time
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--diag-stub", "hang", "--deadline-s", "75"] + ARGS
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    took = time.time() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["value"] > 0 and rec["n_gpus"] == 2
+    assert "deadline" in rec["diagnostic_errors"]["stub_hang"]
+    assert "collectives" in rec and "bucket_sweep" in rec  # the phases before the hang made it in
+    assert 75 <= rec["wall_s"] < 85 and took < 75 + 30
+
+
+@pytest.mark.slow
+def test_bench_diagnostic_budget_skips_phases():
+    """With the diagnostic budget already spent, no diagnostic phase starts; each is named."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--diag-budget-s", "0"] + ARGS
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["value"] > 0
+    for name in ("collectives", "bucket_sweep", "fsdp_mem"):
+        assert "budget" in rec["diagnostic_errors"][name]
+    assert "collectives" not in rec and "fsdp_mem" not in rec

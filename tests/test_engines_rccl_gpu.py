@@ -51,8 +51,6 @@ def _train(kind, force, delay, accum=1, S=128, count_wt=False):
     from dtg.models import build_model, resolve_config
     from dtg.parallel.data_parallel import DataParallel, FlatAdamW
 
-    if delay:
-        _install_delay()
     dev = torch.device("cuda", torch.cuda.current_device())
     cfg = resolve_config(MODEL)
     torch.manual_seed(0)
@@ -101,8 +99,37 @@ def _train(kind, force, delay, accum=1, S=128, count_wt=False):
     return {n: p.detach().cpu().clone() for n, p in model.named_parameters()}, losses, mode
 
 
-def _worker(rank, world, kind, delay, accum, S=128, count_wt=False):
-    return _train(kind, True, delay, accum, S, count_wt)
+# (kind, delay, accum, S, count_wt): every world-1 RCCL configuration runs in ONE spawned process
+# (process + communicator start-up dominated these tests); undelayed ones first, since the delay
+# wraps torch.distributed's collectives for the rest of the process
+_W1_CONFIGS = [("ddp", False, 1, 128, False), ("zero", False, 1, 128, False), ("fsdp", False, 1, 128, False),
+               ("ddp", True, 1, 128, False), ("zero", True, 1, 128, False), ("fsdp", True, 1, 128, False),
+               ("ddp", True, 2, 128, False), ("zero", True, 2, 128, False), ("zero", True, 1, 1024, False),
+               ("zero", True, 1, 1024, True)]
+_W1 = {}
+
+
+def _world1_all(rank, world, configs):
+    import gc
+
+    out, delayed = {}, False
+    for c in configs:
+        kind, delay, accum, S, count_wt = c
+        if delay and not delayed:
+            _install_delay()
+            delayed = True
+        assert delay or not delayed, "undelayed configurations must come first"
+        out[c] = _train(kind, True, delay, accum, S, count_wt)
+        gc.collect()
+        torch.cuda.empty_cache()
+    return out
+
+
+def _world1(kind, delay, accum, S=128, count_wt=False):
+    if not _W1:
+        (res,) = run_distributed(_world1_all, 1, _W1_CONFIGS, backend="nccl")
+        _W1.update(res)
+    return _W1[(kind, delay, accum, S, count_wt)]
 
 
 def _single(kind, accum, S=128):
@@ -114,7 +141,7 @@ def _single(kind, accum, S=128):
 @pytest.mark.parametrize("delay", [False, True])
 def test_rccl_world1_engine_bit_identical(cuda, kind, delay):
     ref, ref_losses, ref_mode = _single(kind, 1)
-    (params, losses, mode), = run_distributed(_worker, 1, kind, delay, 1, backend="nccl")
+    params, losses, mode = _world1(kind, delay, 1)
     assert mode == kind and ref_mode in ("single", "fsdp"), (mode, ref_mode)
     assert losses == ref_losses
     for n, v in ref.items():
@@ -124,7 +151,7 @@ def test_rccl_world1_engine_bit_identical(cuda, kind, delay):
 @pytest.mark.parametrize("kind", ["ddp", "zero"])
 def test_rccl_world1_grad_accumulation(cuda, kind):
     ref, ref_losses, _ = _single(kind, 2)
-    (params, losses, mode), = run_distributed(_worker, 1, kind, True, 2, backend="nccl")
+    params, losses, mode = _world1(kind, True, 2)
     assert mode == kind and losses == ref_losses
     for n, v in ref.items():
         assert torch.equal(params[n], v), (kind, n)
@@ -159,16 +186,47 @@ def _offload_worker(rank, world, overlap, accum, offload_params=True, ring=0):
     return {k: v.cpu() for k, v in eng.full_state_dict(rank0_only=False).items()}, stepped
 
 
+def _offload_configs(rank, world, configs):
+    """Every offload configuration in ONE spawn of the ranks (process start-up dominates)."""
+    import gc
+
+    out = {}
+    for c in configs:
+        out[c] = _offload_worker(rank, world, *c)
+        gc.collect()
+        torch.cuda.empty_cache()
+    return out
+
+
+# (overlap, accum, offload_params, ring)
+_OFFLOAD_CONFIGS = [(True, 1, True, 0), (False, 1, True, 0), (True, 2, True, 0), (False, 2, True, 0),
+                    (True, 1, False, 0), (True, 2, False, 0), (False, 1, False, 0),
+                    (True, 1, False, 4), (True, 1, False, 1), (True, 1, True, 2)]
+_OFFLOAD = {}
+
+
+def _offload_results():
+    if not _OFFLOAD:
+        res = run_distributed(_offload_configs, 2, _OFFLOAD_CONFIGS)
+        _OFFLOAD.update({c: [res[r][c] for r in range(2)] for c in _OFFLOAD_CONFIGS})
+    return _OFFLOAD
+
+
+def _same(a, b, tag):
+    for r in range(2):
+        for n, t in b[r][0].items():
+            assert torch.equal(a[r][0][n], t), (tag, r, n)
+
+
 @pytest.mark.parametrize("accum", [1, 2])
 def test_fsdp_cpu_offload_overlap_bit_identical_on_gpu(cuda, accum):
     """pinned host shards, non_blocking H2D gathers, reduce-scatter -> D2H and the
     host-AdamW worker thread running while GPU streams are live: overlapped == post-backward."""
-    on = run_distributed(_offload_worker, 2, True, accum)
-    off = run_distributed(_offload_worker, 2, False, accum)
+    res = _offload_results()
+    on, off = res[(True, accum, True, 0)], res[(False, accum, True, 0)]
     for r in range(2):
         assert all(on[r][1]) and not any(off[r][1])
-        for n, t in off[r][0].items():
-            assert torch.equal(on[r][0][n], t), (r, n)
+    _same(on, off, ("overlap", accum))
 
 
 @pytest.mark.parametrize("overlap,accum", [(True, 1), (True, 2), (False, 1)])
@@ -176,11 +234,8 @@ def test_fsdp_resident_param_offload_bit_identical_on_gpu(cuda, overlap, accum):
     """offload_params=False: shards resident in HBM, host AdamW from the worker thread copying
     each updated unit back on the H2D side stream while backward kernels are still running; the
     next forward's gathers wait on those copies == the full offload, bit for bit."""
-    res = run_distributed(_offload_worker, 2, overlap, accum, False)
-    full = run_distributed(_offload_worker, 2, overlap, accum, True)
-    for r in range(2):
-        for n, t in full[r][0].items():
-            assert torch.equal(res[r][0][n], t), (r, n)
+    res = _offload_results()
+    _same(res[(overlap, accum, False, 0)], res[(overlap, accum, True, 0)], ("resident", overlap, accum))
 
 
 def test_rccl_world1_zero_weight_t_with_delayed_gathers(cuda):
@@ -191,11 +246,11 @@ def test_rccl_world1_zero_weight_t_with_delayed_gathers(cuda):
     copies the optimizer kernel writes), and every backward dX GEMM at >= 4096 tokens must use
     a copy (no per-weight transposes in the backward)."""
     ref, ref_losses, _ = _single("zero", 1, S=1024)
-    (params, losses, mode), = run_distributed(_worker, 1, "zero", True, 1, 1024, backend="nccl")
+    params, losses, mode = _world1("zero", True, 1, 1024)
     assert mode == "zero" and losses == ref_losses
     for n, v in ref.items():
         assert torch.equal(params[n], v), n
-    (used, _, _), = run_distributed(_worker, 1, "zero", True, 1, 1024, True, backend="nccl")
+    used, _, _ = _world1("zero", True, 1, 1024, True)
     assert used and all(used), f"{used.count(False)} of {len(used)} dX GEMMs transposed W in the backward"
 
 
@@ -205,9 +260,8 @@ def test_fsdp_offload_grad_ring_bit_identical_on_gpu(cuda, offload_params, ring)
     stream into a reused pinned slot while the host AdamW of earlier units reads other slots
     (one slot: every D2H waits for the previous unit's host update) == the whole-model host
     gradient shard, bit for bit."""
-    full = run_distributed(_offload_worker, 2, True, 1, offload_params, 0)
-    got = run_distributed(_offload_worker, 2, True, 1, offload_params, ring)
+    res = _offload_results()
+    got, full = res[(True, 1, offload_params, ring)], res[(True, 1, offload_params, 0)]
     for r in range(2):
         assert all(got[r][1])
-        for n, t in full[r][0].items():
-            assert torch.equal(got[r][0][n], t), (r, n)
+    _same(got, full, ("ring", offload_params, ring))

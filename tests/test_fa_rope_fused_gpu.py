@@ -21,18 +21,23 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
-@pytest.mark.parametrize("D,hq,hkv,causal,docs,split", [
-    (128, 8, 2, True, [0, 512], "1"),
-    (128, 8, 2, True, [0, 200, 384, 512], "1"),
-    (128, 4, 1, False, [0, 256, 512], "1"),
-    (64, 6, 2, True, [0, 300, 512], "1"),
-    (128, 4, 1, True, [0, 512], "2"),
+@pytest.mark.parametrize("D,hq,hkv,causal,docs,split,window,conc", [
+    (128, 8, 2, True, [0, 512], "1", 0, "0"),
+    (128, 8, 2, True, [0, 200, 384, 512], "1", 0, "0"),
+    (128, 4, 1, False, [0, 256, 512], "1", 0, "0"),
+    (64, 6, 2, True, [0, 300, 512], "1", 0, "0"),
+    (128, 4, 1, True, [0, 512], "2", 0, "0"),
+    # sliding window (Mistral) and the concurrent dQ / dK-dV backward go through the same epilogues
+    (128, 8, 2, True, [0, 512], "1", 128, "0"),
+    (64, 6, 2, True, [0, 300, 512], "1", 100, "1"),
+    (128, 8, 2, True, [0, 200, 384, 512], "1", 0, "1"),
 ])
-def test_fused_rope_bwd_matches_separate_pass(cuda, monkeypatch, D, hq, hkv, causal, docs, split):
+def test_fused_rope_bwd_matches_separate_pass(cuda, monkeypatch, D, hq, hkv, causal, docs, split, window, conc):
     import dtg.ops  # noqa: F401
 
     ops = torch.ops.dtg
     monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
+    monkeypatch.setenv("DTG_FA_BWD_CONC", conc)
     torch.manual_seed(0)
     T = docs[-1]
     cu = torch.tensor(docs, dtype=torch.int32, device=cuda)
@@ -45,10 +50,10 @@ def test_fused_rope_bwd_matches_separate_pass(cuda, monkeypatch, D, hq, hkv, cau
     q = qkv[:, : hq * D].view(T, hq, D)
     k = qkv[:, hq * D:(hq + hkv) * D].view(T, hkv, D)
     v = qkv[:, (hq + hkv) * D:].view(T, hkv, D)
-    o, lse = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal)
-    ref = ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, D, o, lse, cu, maxlen, scale, causal)
+    o, lse = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal, window)
+    ref = ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, D, o, lse, cu, maxlen, scale, causal, window)
     ops.rope_(ref, cos, sin, pos, hq + hkv, D, True)
-    got = ops.flash_attn_bwd_qkv_rope(do, qkv, hq, hkv, D, o, lse, cu, maxlen, scale, causal, cos, sin, pos)
+    got = ops.flash_attn_bwd_qkv_rope(do, qkv, hq, hkv, D, o, lse, cu, maxlen, scale, causal, cos, sin, pos, window)
     assert torch.equal(got[:, (hq + hkv) * D:], ref[:, (hq + hkv) * D:])  # dV untouched
     for name, sl in (("dq", slice(0, hq * D)), ("dk", slice(hq * D, (hq + hkv) * D))):
         r = _rel(got[:, sl], ref[:, sl])

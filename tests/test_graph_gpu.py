@@ -103,3 +103,31 @@ def test_chapter01_trainer_hip_graph(cuda, tmp_path):
     recs = [json.loads(x) for x in (tmp_path / "hg" / "metrics-rank0.jsonl").read_text().splitlines()]
     assert len(recs) == 3 and all(x["running_loss"] == x["running_loss"] for x in recs)
     assert recs[-1]["time/backward"] == 0.0 and recs[-1]["global_step"] == 12
+
+
+@pytest.mark.parametrize("attn_pdrop", [0.1, 0.0])
+def test_graphed_gpt2_attention_dropout_redraws_every_replay(cuda, attn_pdrop):
+    """GPT-2 in train mode under --hip-graph: the attention-dropout {seed, offset} comes from torch's
+    CUDA generator as a device tensor (ops.philox_rng), so every replay of the captured step draws
+    a new keep mask.  With lr = 0 the weights never move, so on one repeated batch the replayed
+    losses differ only through the mask: all distinct with attn_pdrop > 0, all equal without it
+    (residual / embedding dropout are off here, so nothing else is random)."""
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.data_parallel import DataParallel, FlatAdamW
+    from dtg.train.graph import GraphedStep
+
+    torch.manual_seed(0)
+    cfg = resolve_config("gpt2-tiny", resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=attn_pdrop)
+    model = build_model(cfg, device=cuda)
+    model.train()
+    eng = DataParallel(model, mode="single")
+    opt = FlatAdamW(eng, lr=0.0, weight_decay=0.0)
+    b = torch.randint(0, cfg.vocab_size, (2, 128), generator=torch.Generator().manual_seed(3)).to(cuda)
+    step = GraphedStep(model, eng, opt, None, warmup=2, num_valid=2 * 127)
+    losses = [step({"input_ids": b, "labels": b}).item() for _ in range(6)]
+    assert step.graph is not None
+    replays = losses[2:]
+    if attn_pdrop > 0:
+        assert len(set(replays)) == len(replays), losses
+    else:
+        assert len(set(replays)) == 1, losses

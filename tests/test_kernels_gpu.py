@@ -381,21 +381,22 @@ def test_flash_attn_dropout_matches_masked_reference(cuda, D, hq, hkv, seqlens, 
     do = torch.randn(T, hq, D).bfloat16()
     scale = 1 / math.sqrt(D)
     seed, off = 0x123456789AB, 77
-    o_ref, lse_ref = dops.flash_attn_fwd_drop(q, k, v, cu, max(seqlens), scale, causal, p, seed, off)
+    rng = torch.tensor([seed, off], dtype=torch.int64)
+    o_ref, lse_ref = dops.flash_attn_fwd_drop(q, k, v, cu, max(seqlens), scale, causal, p, rng)
     o, lse = dops.flash_attn_fwd_drop(q.to(cuda), k.to(cuda), v.to(cuda), cu.to(cuda), max(seqlens), scale, causal, p,
-                                      seed, off)
+                                      rng.to(cuda))
     _close(o, o_ref, 3e-2, 2e-2, "attn out (dropout)")
     _close(lse, lse_ref, 2e-3, 1e-3, "lse")
-    ref = dops.flash_attn_bwd_drop(do, q, k, v, o_ref, lse_ref, cu, max(seqlens), scale, causal, p, seed, off)
+    ref = dops.flash_attn_bwd_drop(do, q, k, v, o_ref, lse_ref, cu, max(seqlens), scale, causal, p, rng)
     for split in ("1", "3"):
         monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
         got = dops.flash_attn_bwd_drop(do.to(cuda), q.to(cuda), k.to(cuda), v.to(cuda), o, lse, cu.to(cuda),
-                                       max(seqlens), scale, causal, p, seed, off)
+                                       max(seqlens), scale, causal, p, rng.to(cuda))
         for a, b, n in zip(got, ref, ("dq", "dk", "dv")):
             assert _rel(a, b) < 2e-2, f"{n} (split {split}) rel err {_rel(a, b)}"
     # another offset is another mask
     o2, _ = dops.flash_attn_fwd_drop(q.to(cuda), k.to(cuda), v.to(cuda), cu.to(cuda), max(seqlens), scale, causal, p,
-                                     seed, off + 1)
+                                     torch.tensor([seed, off + 1], dtype=torch.int64, device=cuda))
     assert _rel(o2, o_ref) > 5e-2
 
 

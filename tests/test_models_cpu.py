@@ -157,7 +157,6 @@ def test_gpt2_attention_dropout_in_the_flash_op():
     op's own keep mask, the same torch seed reproduces it, and gradients flow."""
     from dtg import ops
     from dtg.ops import _cpu
-    from dtg.ops.functional import dropout_seed_offset
 
     torch.manual_seed(0)
     B, S, nh, d = 2, 24, 3, 16
@@ -171,7 +170,7 @@ def test_gpt2_attention_dropout_in_the_flash_op():
     again = ops.attention(qkv, nh, nh, d, cu, 20, dropout_p=0.25)
     assert torch.equal(got, again)
     torch.manual_seed(5)
-    seed, off = dropout_seed_offset()
+    seed, off = _cpu._rng_pair(torch.ops.dtg.philox_rng(qkv, 4))
     q, k, v = qkv.view(T, 3, nh, d).unbind(1)
     _, sc = _cpu.dropout_threshold(0.25)
     want = torch.zeros(T, nh, d)

@@ -1,0 +1,74 @@
+"""Transport selection by measurement (`--tp-comm auto` / `--dp-comm auto`, parallel/transport.py)
+on gloo ranks with stubbed timings: the slowest rank's time decides, every rank picks the same
+transport, a candidate that fails on any rank is never picked, RCCL wins ties."""
+import math
+
+import pytest
+
+from _dist import run_distributed
+
+
+def _stub_pick(rank, world, times, fail_on):
+    from dtg.parallel import transport
+
+    def time_fn(c):
+        if (c.name, rank) in fail_on:
+            raise RuntimeError(f"{c.name} broke on rank {rank}")
+        return times[c.name][rank]
+
+    return transport.select("tp", None, "cpu", 16 << 20, time_fn=time_fn)
+
+
+def test_select_uses_the_slowest_rank_and_agrees():
+    # xgmi is fastest on rank 0 but slowest on rank 1; xgmi-dma's worst rank is the best worst
+    times = {"rccl": [3e-4, 3e-4], "xgmi": [1e-4, 5e-4], "xgmi-dma": [2e-4, 2.5e-4]}
+    res = run_distributed(_stub_pick, 2, times, set())
+    (c0, t0), (c1, t1) = res
+    assert c0 == c1 == "xgmi-dma"
+    assert t0 == t1
+    assert t0["xgmi"]["us"] == pytest.approx(500.0) and t0["rccl"]["us"] == pytest.approx(300.0)
+    assert t0["xgmi-dma"]["msg_mib"] == 16.0
+
+
+def test_select_excludes_a_candidate_that_fails_anywhere():
+    times = {"rccl": [3e-4, 3e-4], "xgmi": [1e-4, 1e-4], "xgmi-dma": [2e-4, 2e-4]}
+    res = run_distributed(_stub_pick, 2, times, {("xgmi", 1)})
+    (c0, t0), (c1, t1) = res
+    assert c0 == c1 == "xgmi-dma"
+    assert t0["xgmi"]["us"] is None and t0["xgmi"]["error"] == "failed on another rank"
+    assert "broke on rank 1" in t1["xgmi"]["error"]
+
+
+def test_pick_prefers_rccl_on_ties_and_without_data():
+    from dtg.parallel.transport import pick
+
+    assert pick({"rccl": {"us": 10.0}, "xgmi-dma": {"us": 10.0}}) == "rccl"
+    assert pick({"rccl": {"us": None}, "xgmi-dma": {"us": None}}) == "rccl"
+    assert pick({"rccl": {"us": 12.0}, "xgmi-dma": {"us": 9.0}}) == "xgmi-dma"
+
+
+def _cpu_auto(rank, world):
+    from dtg.parallel import transport
+
+    return transport.resolve("auto", "dp", None, "cpu", 64 << 20), transport.resolve("xgmi", "tp", None, "cpu", 1)
+
+
+def test_resolve_on_cpu_is_the_process_group():
+    (auto, explicit), _ = run_distributed(_cpu_auto, 2)
+    assert auto[0] == "rccl" and "CPU" in auto[1]["rccl"]["note"]
+    assert explicit == ("xgmi", None)
+
+
+def test_trainer_and_bench_default_to_auto():
+    import bench
+    from dtg.train.cli import get_parser
+
+    for ch in ("06", "07"):
+        a = get_parser(ch).parse_args(["-e", "x", "-d", "synthetic", "-m", "llama-tiny"])
+        assert a.tp_comm == "auto"
+    for ch in ("02", "04", "05", "07"):
+        a = get_parser(ch).parse_args(["-e", "x", "-d", "synthetic", "-m", "llama-tiny"])
+        assert a.dp_comm == "auto"
+    b = bench.parse([])
+    assert b.tp_comm == "auto" and b.dp_comm == "auto"
+    assert math.isfinite(b.deadline_s) and b.diag_budget_s < b.deadline_s
