@@ -5,9 +5,11 @@ Directory layout under `{save_dir}/{experiment_name}/` follows the reference per
   * dp   (02):        model.pt (rank 0), lr_scheduler.pt, state.json, rng.pt + the optimizer
                       state as a sharded `checkpoint/` (the reference never saved it and then
                       crashed on resume)
-  * sharded (04-07):  checkpoint/ (index.json + shard_rNNNNN.pt per rank), lr_scheduler.pt, state.json, rng.pt
+  * sharded (04-07):  checkpoint/ (torch DCP: .metadata + __<rank>_0.distcp, the reference's tree;
+                      train/dcp_ckpt.py), lr_scheduler.pt, state.json, rng.pt
 
-Sharded format `dtg-sharded-v2` (this framework's own; not torch DCP, whose file names it does
+`--ckpt-format dtg` keeps this framework's previous sharded format, which every load still reads:
+format `dtg-sharded-v2` (this framework's own; not torch DCP, whose file names it does
 not borrow): every rank writes `checkpoint/shard_rNNNNN.pt` holding, for each parameter slice it
 owns, the parameter values and both AdamW moments (plain tensors: loadable with
 `torch.load(weights_only=True)`), and rank 0 writes `checkpoint/index.json` with every slice's
@@ -563,12 +565,17 @@ class CheckpointManager:
     PENDING = PENDING
 
     def __init__(self, exp_dir, engine, optimizer, lr_scheduler, style: str, local_rank: int = 0,
-                 async_save: bool = False):
+                 async_save: bool = False, fmt: str = "dcp"):
+        """fmt: the `checkpoint/` format of the "dp" / "sharded" styles -- "dcp" (torch DCP, the
+        reference's tree; train/dcp_ckpt.py) or "dtg" (dtg-sharded-v2).  Loading reads either.
+        A DCP save is collective end to end, so --async-ckpt applies to the "dtg" format only."""
+        assert fmt in ("dcp", "dtg"), fmt
         self.exp_dir = Path(exp_dir)
         self.engine, self.optimizer, self.lr_scheduler = engine, optimizer, lr_scheduler
         self.style = style
         self.local_rank = local_rank
-        self.async_save = async_save
+        self.fmt = fmt
+        self.async_save = async_save and not (fmt == "dcp" and style != "full")
         self._writer = None   # background thread of the pending save
         self._pending = None  # (state, lr_scheduler state, rng state) to publish on finalize
         self._error = None
@@ -586,7 +593,10 @@ class CheckpointManager:
                 sd = self.engine.full_state_dict()
                 if get_rank() == 0:
                     jobs.append(("model.pt", sd))
-            shard = snapshot_sharded(self.engine, global_step)
+            if self.fmt == "dcp":
+                shard = ("dcp", global_step)
+            else:
+                shard = snapshot_sharded(self.engine, global_step)
         return jobs, shard
 
     def _write_pending(self, jobs, shard):
@@ -595,7 +605,11 @@ class CheckpointManager:
             pend.mkdir(parents=True, exist_ok=True)
             for rel, obj in jobs:
                 save_durable(obj, pend / rel)
-            if shard is not None:
+            if shard is not None and shard[0] == "dcp":
+                from .dcp_ckpt import save_dcp
+
+                save_dcp(pend / "checkpoint", self.engine, self.optimizer, self.engine.module.config, shard[1])
+            elif shard is not None:
                 write_sharded(pend / "checkpoint", *shard)
         except BaseException as e:  # surfaced by finalize() on the main thread
             self._error = e
@@ -675,7 +689,12 @@ class CheckpointManager:
             self.optimizer.load_state_dict(torch.load(d / "optimizer.pt", map_location=dev, weights_only=True))
             meta = None
         else:
-            meta = load_sharded(d / "checkpoint", self.engine)
+            from .dcp_ckpt import is_dcp_dir, load_dcp
+
+            if is_dcp_dir(d / "checkpoint"):
+                meta = load_dcp(d / "checkpoint", self.engine, self.engine.module.config)
+            else:
+                meta = load_sharded(d / "checkpoint", self.engine)
         self.lr_scheduler.load_state_dict(torch.load(d / "lr_scheduler.pt", weights_only=True))
         # The sharded / per-rank layouts restore the AdamW moments but not the optimizer's
         # param_groups, and chainable schedulers (CosineAnnealingLR) compute the next lr FROM the

@@ -136,6 +136,11 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                    help="override the model's num_hidden_layers (exact-width, reduced-depth runs)")
     g.add_argument("--init-from", default=None, help="HF safetensors directory to load pretrained weights from")
     g.add_argument("--tunableop", default="use", choices=["off", "use", "tune"])
+    g.add_argument("--ckpt-format", default="dcp", choices=["dcp", "dtg"],
+                   help="checkpoint/ of the sharded chapters (02, 04-07): dcp = torch.distributed.checkpoint "
+                        "written by every rank (the reference's tree, readable by dcp_to_torch_save; resumes on "
+                        "any world size / TP degree); dtg = this framework's dtg-sharded-v2 (index.json + "
+                        "shard_rNNNNN.pt; --async-ckpt needs it).  Resume reads either")
     g.add_argument("--async-ckpt", default="off", choices=["on", "off"],
                    help="snapshot checkpoints to host memory and write them on a background thread; published "
                         "(state.json written last) at the next save or at the end of training")

@@ -1,0 +1,339 @@
+"""torch.distributed.checkpoint (DCP) as the sharded chapters' native on-disk format
+(`--ckpt-format dcp`, the default for chapters 02 and 04-07).
+
+The reference saves `{exp_dir}/checkpoint` from every rank with
+`dcp.save({"model": model_sd, "optimizer": optim_sd}, checkpoint_id=exp_dir / "checkpoint")`
+(/root/reference/04-fully-sharded-data-parallel/train_llm.py:121-154, 249-263;
+06-tensor-parallel/train_llm.py:177-190, 283-295): a `.metadata` file plus one `__<rank>_0.distcp`
+file per rank, with HF parameter names (`model.layers.0.self_attn.q_proj.weight`, ...) and torch
+AdamW's state layout (`optimizer.state.<fqn>.{exp_avg, exp_avg_sq, step}`, `param_groups`).
+This module writes exactly that tree from this framework's engines, without DTensors or
+ShardedTensors:
+
+* every rank describes the slices it owns (FSDP flat-shard ranges, ZeRO bucket slices,
+  tensor-parallel row / column blocks -- `checkpoint._TPGeom.rects`, rectangles in GLOBAL
+  parameter coordinates) as DCP chunks: offsets + sizes in the HF tensor's real shape.  The
+  fused `qkv_proj` / `gate_up_proj` rows split into their q / k / v and gate / up tensors at the
+  row boundaries, so a chunk never straddles two HF tensors;
+* a custom `SavePlanner` hands those chunks to DCP's FileSystemWriter (one file per rank,
+  fsynced), and rank 0 adds the `param_groups` with the full AdamW hyper-parameters;
+* resume is `dcp.load` with a custom `LoadPlanner` whose destination chunks are views into the
+  engine's own parameter / moment buffers: DCP's resharding reads the overlap of every stored
+  chunk, so a checkpoint written on W x TP a loads on W' x TP b (data-parallel world, tensor-
+  parallel degree, pipeline stages, FSDP / ZeRO / DDP layouts alike).  A destination element no
+  stored chunk covers fails the load.
+
+`torch.distributed.checkpoint.format_utils.dcp_to_torch_save(exp_dir / "checkpoint", "full.pt")`
+reads a training run's checkpoint directly (the reference's README recipe).  The small
+`checkpoint/dtg.json` records the step counters (DCP ignores files it did not write).
+The previous format (`dtg-sharded-v2`: index.json + shard_rNNNNN.pt) stays readable.
+"""
+from __future__ import annotations
+
+import io
+import json
+import os
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+FORMAT = "dcp"
+META = "dtg.json"
+
+
+def is_dcp_dir(ckpt_dir) -> bool:
+    return (Path(ckpt_dir) / ".metadata").exists()
+
+
+# ------------------------------------------------------------------------------ naming
+class _Names:
+    """This framework's parameter (global name, global [R, C] rectangle) -> HF-named DCP chunks."""
+
+    def __init__(self, cfg):
+        from ..models.config import LlamaConfig
+
+        self.cfg = cfg
+        self.llama = isinstance(cfg, LlamaConfig)
+
+    def split(self, name, full_shape, rect):
+        """[(hf_fqn, hf_shape, offsets, sizes, (r_lo, r_hi))] for rectangle rect = [r0, nr, c0, nc,
+        off] (global rows x flattened columns) of parameter `name`; (r_lo, r_hi) are the rect's
+        rows that chunk covers."""
+        r0, nr, c0, nc, _ = rect
+        shape = list(full_shape)
+        if not self.llama:
+            return [(name, shape, *_chunk(shape, r0, nr, c0, nc), (r0, r0 + nr))]
+        cfg = self.cfg
+        parts = None  # [(HF name, first global row, rows)]
+        if name.endswith("self_attn.qkv_proj.weight") or name.endswith("self_attn.qkv_proj.bias"):
+            d, nq, nkv = cfg.head_dim, cfg.num_attention_heads, cfg.num_key_value_heads
+            pre, leaf = name.rsplit("qkv_proj.", 1)
+            parts = [(f"{pre}q_proj.{leaf}", 0, nq * d), (f"{pre}k_proj.{leaf}", nq * d, nkv * d),
+                     (f"{pre}v_proj.{leaf}", (nq + nkv) * d, nkv * d)]
+        elif name.endswith("mlp.gate_up_proj.weight"):
+            i = shape[0] // 2
+            pre = name[: -len("gate_up_proj.weight")]
+            parts = [(f"{pre}gate_proj.weight", 0, i), (f"{pre}up_proj.weight", i, i)]
+        if parts is None:
+            hf = name if name == "lm_head.weight" else "model." + name
+            return [(hf, shape, *_chunk(shape, r0, nr, c0, nc), (r0, r0 + nr))]
+        out = []
+        for hf, g0, rows in parts:
+            lo, hi = max(r0, g0), min(r0 + nr, g0 + rows)
+            if lo >= hi:
+                continue
+            # this framework's q/k/v bias is [N, 1]; HF's is [N]
+            sub = [rows] if name.endswith("bias") else [rows] + shape[1:]
+            out.append(("model." + hf, sub, *_chunk(sub, lo - g0, hi - lo, c0, nc, rows_1d=len(sub) == 1), (lo, hi)))
+        return out
+
+
+def _chunk(shape, r0, nr, c0, nc, rows_1d=False):
+    """(offsets, sizes) of a global [rows x flattened cols] rectangle in a tensor of `shape`.  A 1-D
+    parameter (norm weight) is one global row [1, C]; `rows_1d`: a 1-D HF tensor stored here as
+    N rows of one column (the [N, 1] q/k/v biases)."""
+    if len(shape) == 2:
+        return [r0, c0], [nr, nc]
+    if len(shape) == 1:
+        return ([r0], [nr]) if rows_1d else ([c0], [nc])
+    raise ValueError(f"DCP chunks: {len(shape)}-D parameters are not supported")
+
+
+def _chunks(engine, cfg, keep=None):
+    """This rank's DCP chunks: [(hf_fqn, hf_shape, offsets, sizes, {"p" | "m" | "v": view})] of the
+    owned pieces whose local parameter name passes `keep`.  Views index the engine's live buffers
+    (reads for a save, in-place writes for a load)."""
+    from .checkpoint import _TPGeom, _name_map, param_kind
+
+    geo = _TPGeom(engine)
+    gname = _name_map(engine)
+    shapes_local = {n: list(p.shape) for n, p in engine.module.named_parameters()}
+    names = _Names(cfg)
+    out = []
+    kind_of = (lambda n: param_kind(n)) if geo.size > 1 else (lambda n: "rep")
+    for name, start, n, pview, sidx in engine.ckpt_pieces():
+        if keep is not None and not keep(name):
+            continue
+        full = geo.full_shape(kind_of(name), shapes_local[name])
+        flat = {"p": pview.detach().reshape(-1), "m": engine.exp_avg[sidx:sidx + n],
+                "v": engine.exp_avg_sq[sidx:sidx + n]}
+        for rect in geo.rects(name, shapes_local[name], int(start), int(n)):
+            r0, nr, c0, nc, off = rect
+            for hf, hshape, offs, sizes, (lo, hi) in names.split(gname(name), full, rect):
+                views = {k: t[off:off + nr * nc].view(nr, nc)[lo - r0:hi - r0] for k, t in flat.items()}
+                views = {k: v.reshape(sizes) for k, v in views.items()}
+                out.append((hf, hshape, list(offs), list(sizes), views))
+    return out
+
+
+# ------------------------------------------------------------------------------ save
+def _planners():
+    from torch.distributed.checkpoint.default_planner import DefaultLoadPlanner, DefaultSavePlanner
+    from torch.distributed.checkpoint.metadata import ChunkStorageMetadata, MetadataIndex, TensorProperties
+    from torch.distributed.checkpoint.planner import (SavePlan, TensorWriteData, WriteItem, WriteItemType,
+                                                      LoadPlan)
+    from torch.distributed.checkpoint.planner_helpers import create_read_items_for_chunk_list
+
+    class ChunkSavePlanner(DefaultSavePlanner):
+        """Writes precomputed chunks (tensors) and objects (coordinator) under flat DCP keys."""
+
+        def __init__(self, tensors, objects, mappings):
+            super().__init__()
+            self._tensors = tensors    # [(flat key, global shape, offsets, tensor)]
+            self._objects = objects    # {flat key: picklable object}
+            self._mappings = mappings  # {flat key: nested path}
+            self._lookup = {}
+
+        def set_up_planner(self, state_dict, storage_meta=None, is_coordinator=False):
+            self.state_dict = {}
+            self.is_coordinator = is_coordinator
+
+        def create_local_plan(self):
+            items = []
+            for key, gshape, offs, t in self._tensors:
+                props = TensorProperties.create_from_tensor(t)
+                chunk = ChunkStorageMetadata(offsets=torch.Size(offs), sizes=t.size())
+                wtype = WriteItemType.SHARD if len(gshape) else WriteItemType.TENSOR
+                items.append(WriteItem(index=MetadataIndex(key, torch.Size(offs)), type=wtype,
+                                       tensor_data=TensorWriteData(chunk=chunk, properties=props,
+                                                                   size=torch.Size(gshape))))
+                self._lookup[(key, tuple(offs))] = t
+            for key in self._objects:
+                items.append(WriteItem(index=MetadataIndex(key), type=WriteItemType.BYTE_IO))
+            self.plan = SavePlan(items, planner_data=dict(self._mappings))
+            return self.plan
+
+        def resolve_data(self, write_item):
+            key = write_item.index.fqn
+            if write_item.type == WriteItemType.BYTE_IO:
+                buf = io.BytesIO()
+                torch.save(self._objects[key], buf)
+                return buf
+            t = self._lookup[(key, tuple(write_item.index.offset or ()))]
+            return t.detach().to("cpu").contiguous()
+
+    class ChunkLoadPlanner(DefaultLoadPlanner):
+        """Reads stored chunks into destination views (any stored layout -> this rank's layout)."""
+
+        def __init__(self, dests, scalars):
+            super().__init__()
+            self._dests = dests      # [(flat key, global shape, offsets, view)]
+            self._scalars = scalars  # {flat key: 0-d tensor} filled from the checkpoint
+            self._lookup = {}
+            self.covered = {}
+
+        def set_up_planner(self, state_dict, metadata=None, is_coordinator=False):
+            self.state_dict = {}
+            self.metadata = metadata
+            self.is_coordinator = is_coordinator
+
+        def create_local_plan(self):
+            md = self.metadata.state_dict_metadata
+            items = []
+            for key, gshape, offs, view in self._dests:
+                if key not in md:
+                    raise KeyError(f"DCP checkpoint has no tensor {key!r}")
+                if list(md[key].size) != list(gshape):
+                    raise ValueError(f"{key}: checkpoint shape {list(md[key].size)} != model's {list(gshape)}")
+                chunk = ChunkStorageMetadata(offsets=torch.Size(offs), sizes=view.size())
+                got = create_read_items_for_chunk_list(key, md[key], [chunk])
+                self._lookup[(key, tuple(offs))] = view
+                vol = 0
+                for it in got:
+                    n = 1
+                    for x in it.lengths:
+                        n *= int(x)
+                    vol += n
+                if vol != view.numel():
+                    raise RuntimeError(f"DCP checkpoint covers {vol} of the {view.numel()} elements of {key} "
+                                       f"this rank owns at offsets {offs}")
+                items += got
+            for key, t in self._scalars.items():
+                if key not in md:
+                    raise KeyError(f"DCP checkpoint has no tensor {key!r}")
+                chunk = ChunkStorageMetadata(offsets=torch.Size([]), sizes=torch.Size([]))
+                items += create_read_items_for_chunk_list(key, md[key], [chunk])
+                self._lookup[(key, ())] = t
+            self.plan = LoadPlan(items)
+            return self.plan
+
+        def create_global_plan(self, global_plan):
+            return global_plan
+
+        def resolve_tensor(self, read_item):
+            from torch.distributed._shard._utils import narrow_tensor_by_index
+
+            dst = self._lookup[(read_item.dest_index.fqn, tuple(read_item.dest_index.offset or ()))]
+            return narrow_tensor_by_index(dst, read_item.dest_offsets, read_item.lengths)
+
+        def commit_tensor(self, read_item, tensor):
+            pass  # the reader copied into a view of the destination
+
+    return ChunkSavePlanner, ChunkLoadPlanner
+
+
+def _adamw_group(optimizer):
+    g = optimizer.param_groups[0] if optimizer is not None else {}
+    return {"lr": float(g.get("lr", 0.0)), "betas": tuple(g.get("betas", (0.9, 0.999))), "eps": float(g.get("eps", 1e-8)),
+            "weight_decay": float(g.get("weight_decay", 0.01)), "amsgrad": False, "foreach": None, "maximize": False,
+            "capturable": False, "differentiable": False, "fused": True, "decoupled_weight_decay": True}
+
+
+def save_dcp(ckpt_dir, engine, optimizer, cfg, global_step=None):
+    """Collective (every rank): write `ckpt_dir` as a DCP checkpoint of {"model": ...,
+    "optimizer": ...} in the reference's layout."""
+    import torch.distributed.checkpoint as dcp
+    from torch.distributed.checkpoint import FileSystemWriter
+
+    from .checkpoint import _writes_shards, _TPGeom, param_kind, fsync_dir
+
+    ckpt_dir = Path(ckpt_dir)
+    ckpt_dir.mkdir(parents=True, exist_ok=True)
+    SavePlanner, _ = _planners()
+    geo = _TPGeom(engine)
+    write = _writes_shards(engine)
+    skip = getattr(engine.module, "_dtg_ckpt_skip", set())
+    tied = getattr(cfg, "tie_word_embeddings", False)
+    tensors, mappings, fqns = [], {}, set()
+    step = torch.tensor(float(engine.step_count))
+    if write:
+        keep = lambda n: n not in skip and not (geo.size > 1 and geo.rank != 0 and param_kind(n) == "rep")  # noqa: E731
+        for hf, hshape, offs, sizes, views in _chunks(engine, cfg, keep):
+            if hf == "lm_head.weight" and tied:
+                continue
+            fqns.add(hf)
+            for key, path, t in ((f"model.{hf}", ("model", hf), views["p"]),
+                                 (f"optimizer.state.{hf}.exp_avg", ("optimizer", "state", hf, "exp_avg"), views["m"]),
+                                 (f"optimizer.state.{hf}.exp_avg_sq", ("optimizer", "state", hf, "exp_avg_sq"),
+                                  views["v"])):
+                tensors.append((key, hshape, offs, t))
+                mappings[key] = path
+        for hf in sorted(fqns):  # one replicated 0-d "step" per parameter (deduplicated across ranks)
+            key = f"optimizer.state.{hf}.step"
+            tensors.append((key, [], [], step))
+            mappings[key] = ("optimizer", "state", hf, "step")
+    multi = dist.is_initialized() and dist.get_world_size() > 1
+    all_fqns = [None] * dist.get_world_size() if multi else [sorted(fqns)]
+    if multi:
+        dist.all_gather_object(all_fqns, sorted(fqns))
+    rank0 = (dist.get_rank() if dist.is_initialized() else 0) == 0
+    objects = {}
+    if rank0:
+        names = sorted(set().union(*[set(x) for x in all_fqns]))
+        group = dict(_adamw_group(optimizer), params=names)
+        objects["optimizer.param_groups"] = [group]
+        mappings["optimizer.param_groups"] = ("optimizer", "param_groups")
+    writer = FileSystemWriter(str(ckpt_dir), single_file_per_rank=True, sync_files=True)
+    dcp.save({}, storage_writer=writer, planner=SavePlanner(tensors, objects, mappings), no_dist=not multi)
+    if rank0:
+        meta = {"format": FORMAT, "step": int(engine.step_count), "global_step": global_step,
+                "world_size": dist.get_world_size() if multi else 1, "tp_size": geo.size}
+        with open(ckpt_dir / META, "w") as fp:
+            json.dump(meta, fp)
+            fp.flush()
+            os.fsync(fp.fileno())
+    if multi:
+        dist.barrier()
+    fsync_dir(ckpt_dir)
+
+
+# ------------------------------------------------------------------------------ load
+def load_dcp(ckpt_dir, engine, cfg, load_optimizer: bool = True) -> dict:
+    """Collective: fill this rank's owned parameter (and AdamW-moment) slices from a DCP
+    checkpoint written on any layout.  Returns the dtg.json record (step counters)."""
+    import torch.distributed.checkpoint as dcp
+    from torch.distributed.checkpoint import FileSystemReader
+
+    ckpt_dir = Path(ckpt_dir)
+    _, LoadPlanner = _planners()
+    tied = getattr(cfg, "tie_word_embeddings", False)
+    dests, first = [], None
+    for hf, hshape, offs, sizes, views in _chunks(engine, cfg):
+        if hf == "lm_head.weight" and tied:
+            continue
+        dests.append((f"model.{hf}", hshape, offs, views["p"]))
+        if load_optimizer:
+            dests.append((f"optimizer.state.{hf}.exp_avg", hshape, offs, views["m"]))
+            dests.append((f"optimizer.state.{hf}.exp_avg_sq", hshape, offs, views["v"]))
+        first = first or hf
+    scalars = {}
+    step = torch.zeros(())
+    if load_optimizer and first is not None:
+        scalars[f"optimizer.state.{first}.step"] = step
+    multi = dist.is_initialized() and dist.get_world_size() > 1
+    with torch.no_grad():
+        dcp.load({}, storage_reader=FileSystemReader(str(ckpt_dir)), planner=LoadPlanner(dests, scalars),
+                 no_dist=not multi)
+    meta = {}
+    if (ckpt_dir / META).exists():
+        with open(ckpt_dir / META) as fp:
+            meta = json.load(fp)
+    if load_optimizer:
+        engine.step_count = int(meta.get("step", int(step.item())))
+    sync = getattr(engine, "sync_params_after_load", None)
+    if sync is not None:
+        sync()
+    if multi:
+        dist.barrier()
+    return meta

@@ -352,8 +352,13 @@ def run(chapter: str, argv=None):
     exp_dir = Path(args.save_dir) / args.experiment_name
     state = new_state()
     resumed = False
+    fmt = getattr(args, "ckpt_format", "dcp")
+    if fmt == "dcp" and getattr(args, "async_ckpt", "off") == "on" and style != "full":
+        LOGGER.warning("--async-ckpt writes the dtg-sharded-v2 format (a DCP save is collective end to end): "
+                       "using --ckpt-format dtg")
+        fmt = "dtg"
     mgr = CheckpointManager(exp_dir, engine, opt, lr_scheduler, style, local_rank,
-                            async_save=getattr(args, "async_ckpt", "off") == "on")
+                            async_save=getattr(args, "async_ckpt", "off") == "on", fmt=fmt)
     # DTG_FAKE_WORLD rehearsal: the other ranks are a fake process group, so its weights are
     # not a training result -- never resume into it, never write (or journal-commit) a checkpoint
     fake = udist.fake_world() > 1

@@ -317,7 +317,7 @@ def test_every_payload_is_fsynced_before_commit(tmp_path, monkeypatch, style):
     before = set(events[:marker])
     pend = str(tmp_path / ".pending")
     payload = ["lr_scheduler.pt", "rng.pt", "state.json", "model.pt"]
-    payload += ["optimizer.pt"] if style == "full" else ["checkpoint/index.json", "checkpoint/shard_r00000.pt",
+    payload += ["optimizer.pt"] if style == "full" else ["checkpoint/__0_0.distcp", "checkpoint/dtg.json",
                                                           "checkpoint"]
     for rel in payload:
         assert f"{pend}/{rel}" in before, rel

@@ -142,6 +142,8 @@ def test_dcp_export_readable_by_torch_format_utils_and_imports_back():
         st = sd["optimizer"]["state"]
         assert set(st) == set(sd["model"]) and all(float(x["step"]) == 2 for x in st.values())
         assert all(x["exp_avg"].shape == sd["model"][k].shape for k, x in st.items())
+        (pg,) = sd["optimizer"]["param_groups"]  # torch AdamW's full group
+        assert {"lr", "betas", "eps", "weight_decay"} <= set(pg) and set(pg["params"]) == set(st)
         # DCP -> one-shard checkpoint -> TP=2 resume, bit-exact parameters
         ck2 = os.path.join(d, "imported")
         ckpt_export.import_dcp(out, ck2, MODEL)

@@ -42,7 +42,8 @@ def test_fsdp_chapter_checkpoint_resume(tmp_path):
     r = _torchrun("04-fully-sharded-data-parallel", base + ["--max-steps", "2"])
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     ck = tmp_path / "fs" / "checkpoint"
-    assert (ck / "index.json").exists() and (ck / "shard_r00000.pt").exists() and (ck / "shard_r00001.pt").exists()
+    # the reference's tree: torch DCP written by every rank (train/dcp_ckpt.py)
+    assert (ck / ".metadata").exists() and (ck / "__0_0.distcp").exists() and (ck / "__1_0.distcp").exists()
     r = _torchrun("04-fully-sharded-data-parallel", base + ["--max-steps", "4"])
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "Resuming" in out, out[-3000:]
@@ -157,9 +158,10 @@ def test_pp_chapter_runs_and_checkpoint_reshards_to_no_pp(tmp_path):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "pipeline stage 1/2" in out
-    meta = json.loads((tmp_path / "pp" / "checkpoint" / "index.json").read_text())
-    names = {e[0] for f in meta["files"] for e in f["index"]}
-    assert "layers.1.mlp.gate_up_proj.weight" in names and "layers.0.mlp.gate_up_proj.weight" in names
+    from torch.distributed.checkpoint import FileSystemReader
+
+    names = set(FileSystemReader(str(tmp_path / "pp" / "checkpoint")).read_metadata().state_dict_metadata)
+    assert {"model.model.layers.1.mlp.up_proj.weight", "model.model.layers.0.mlp.gate_proj.weight"} <= names
     r = _torchrun("02-distributed-data-parallel", base + ["--max-steps", "4"])
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "Resuming" in out, out[-3000:]

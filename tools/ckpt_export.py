@@ -184,7 +184,18 @@ def export_dcp(ckpt_dir, out, model, with_optimizer=False):
                                  "exp_avg_sq": spill(vs[hn])}
     state = {"model": model_sd}
     if with_optimizer:
-        state["optimizer"] = {"state": opt_state, "param_groups": [{"params": list(opt_state)}]}
+        # torch AdamW's full param_group (the reference resumes through get_state_dict + dcp.load +
+        # set_state_dict, 04-fully-sharded-data-parallel/train_llm.py:133-146); lr from the run's
+        # lr_scheduler.pt next to checkpoint/ when present
+        from dtg.train.dcp_ckpt import _adamw_group
+
+        group = _adamw_group(None)
+        sched = Path(ckpt_dir).parent / "lr_scheduler.pt"
+        if sched.exists():
+            last = torch.load(sched, weights_only=True).get("_last_lr")
+            if last:
+                group["lr"] = float(last[0])
+        state["optimizer"] = {"state": opt_state, "param_groups": [dict(group, params=list(opt_state))]}
     dcp.save(state, checkpoint_id=str(out), no_dist=True)
     import shutil
 
