@@ -9,7 +9,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 tag=${1:-r5_405b_2d}
 runs=${2:-"8:8 4:4"}
-O=gpurun_out/$tag
+O=$GRAFT_REPO_ROOT/gpurun_out/$tag
 mkdir -p $O
 export TMPDIR=/tmp
 ( while true; do echo "[405b_2d] alive $(date +%T) $(grep MemAvailable /proc/meminfo)"; sleep 30; done ) & HB=$!
