@@ -69,6 +69,7 @@ def parse(argv=None):
                     help="1: per-bucket AdamW (and ZeRO all-gather) on a side stream during backward (measured +0.2%% on 1 GPU, off)")
     ap.add_argument("--lr", type=float, default=3e-5)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
+    ap.add_argument("--profile-out", default="", help="torch.profiler table path (default gpurun_out/torch_profile.txt)")
     ap.add_argument("--backend", default=None, help="process-group backend override (default: nccl=RCCL on GPU)")
     ap.add_argument("--tunableop", choices=["off", "use", "tune"], default="use",
                     help="PyTorch TunableOp for the hipBLASLt GEMMs: 'use' loads the committed per-shape "
@@ -294,14 +295,18 @@ def throughput_phase(args, torch, dist, device, world, rank, cuda):
     if args.profile_steps > 0 and cuda:
         from torch.profiler import ProfilerActivity, profile
 
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
             for i in range(args.profile_steps):
                 step(i)
             torch.cuda.synchronize()
         if rank == 0:
-            os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-            with open(os.path.join(ROOT, "gpurun_out", "torch_profile.txt"), "w") as fp:
-                fp.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+            out = args.profile_out or os.path.join(ROOT, "gpurun_out", "torch_profile.txt")
+            os.makedirs(os.path.dirname(out), exist_ok=True)
+            with open(out, "w") as fp:
+                fp.write(f"# {args.profile_steps} steps; CUDA time per op and input shape\n")
+                fp.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=80,
+                                                                           max_name_column_width=40,
+                                                                           max_shapes_column_width=70))
     fake = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0) > 1
     # a fake-world rehearsal computes on buffers no collective filled: its loss means nothing
     if not fake and not loss_in_band(loss_val, cfg.vocab_size):

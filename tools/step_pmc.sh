@@ -26,7 +26,7 @@ for p in A B C; do
   [ -z "$ctrs" ] && continue
   echo "[step_pmc] pass $p"
   timeout -s KILL 300 rocprofv3 --pmc $ctrs -d "$out/$p" -o run --output-format csv -- \
-      python3 bench.py --steps 1 --warmup 1 --fsdp-mem-steps 0 > "$out/$p.log" 2>&1 \
+      python3 bench.py --steps 1 --warmup 1 --fsdp-mem-steps 0 --ref-steps 0 > "$out/$p.log" 2>&1 \
       || { tail -20 "$out/$p.log"; exit 1; }
 done
 echo "[step_pmc] done"
