@@ -539,6 +539,211 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Forward, one wave per SIMD ("f64"): the CDNA guide's persistent 4-wave structure (App. B,
+// "4-wave, one-wave-per-SIMD, persistent") in plain HIP.  A workgroup is 4 waves and the CU's
+// only one (__launch_bounds__(256, 1): the whole 512-entry register file per lane); a work item
+// is a 256-row query block of one (sequence, head), and every wave owns 64 of its rows as two
+// 32-row blocks A (rows 32w..) and B (rows 128 + 32w..; interleaved so the causal diagonal costs
+// every wave about the same).  Each K fragment read from LDS feeds two MFMAs (A and B), each V
+// fragment two more: half the LDS read traffic per MFMA of the 2-wave kernel above, whose
+// 32-row waves re-read every K / V fragment per 32 queries.  Workgroups are persistent (one per
+// CU) and take items from a device counter, heaviest (latest causal) blocks first, so the
+// launch has no tail of idle CUs and no per-item launch cost.
+// Numerics are those of fwd_kernel: same tiles (64 keys), same lazy rescale, same f32 sums.
+constexpr int kF64Rows = 256;
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void fwd64_kernel(FwdParams P, int* __restrict__ queue, int nqb, int nseq) {
+  constexpr int RB = 2 * D;
+  constexpr int TILE = kFwdBK * RB;
+  constexpr int NC = D / 16;
+  constexpr int ND = D / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1 | Q (256 rows)]
+  char* const qsm = smem + 4 * TILE;
+  __shared__ int item_sh;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int nitems = nqb * nseq * P.hq;
+  int koff[NC], toa[ND], tob[ND];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
+#pragma unroll
+  for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
+
+  if (threadIdx.x == 0) item_sh = atomicAdd(queue, 1);
+  __syncthreads();
+  int item = item_sh;
+  while (item < nitems) {
+    __syncthreads();  // every lane has read item_sh
+    if (threadIdx.x == 0) item_sh = atomicAdd(queue, 1);  // the next item, read after this one
+    const int per_z = nseq * P.hq;
+    const int zz = item / per_z, rem = item - zz * per_z;
+    const int seq = rem / P.hq, head = grid_head(rem - seq * P.hq, P.hq, P.hkv);
+    const int qb = CAUSAL ? nqb - 1 - zz : zz;  // heaviest blocks first
+    const int s0 = P.cu[seq];
+    const int seqlen = P.cu[seq + 1] - s0;
+    const int q0 = qb * kF64Rows;
+    if (q0 < seqlen) {
+      const int kvh = head / (P.hq / P.hkv);
+      const int qa = q0 + 32 * w, qbb = q0 + 128 + 32 * w;  // first rows of blocks A and B
+      const int kv_end = CAUSAL ? min(seqlen, q0 + kF64Rows) : seqlen;
+      const int ntiles = (kv_end + kFwdBK - 1) / kFwdBK;
+      // a block skips the tiles above its diagonal (wave-uniform); B is always the later block
+      const int lastA = CAUSAL ? min(ntiles - 1, (qa + 31) / kFwdBK) : ntiles - 1;
+      const uint16_t* kbase = P.k + (int64_t)s0 * P.sk + (int64_t)kvh * D;
+      const uint16_t* vbase = P.v + (int64_t)s0 * P.sv + (int64_t)kvh * D;
+      {
+        Stager<kF64Rows, D, 256> sq;
+        sq.load(P.q + (int64_t)(s0 + q0) * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
+        sq.store(qsm);
+      }
+      Stager<kFwdBK, D, 256> sk, sv;
+      sk.load(kbase, P.sk, seqlen);
+      sv.load(vbase, P.sv, seqlen);
+      sk.store(smem);
+      sv.store(smem + TILE);
+      __syncthreads();
+      bf16x8 qf[2][NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        qf[0][c] = lds_frag(qsm + 32 * w * RB + koff[c]);
+        qf[1][c] = lds_frag(qsm + (128 + 32 * w) * RB + koff[c]);
+      }
+      f32x16 acc[2][ND];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int d = 0; d < ND; ++d) acc[b][d] = f32x16{};
+      float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+      const int row[2] = {qa + r, qbb + r};
+
+      // one 64-key tile for blocks A and B (BOTH) or B alone
+      auto tile_step = [&](int t, auto buf, auto both_c) {
+        constexpr int BUF = decltype(buf)::value;
+        constexpr bool BOTH = decltype(both_c)::value;
+        constexpr int B0 = BOTH ? 0 : 1;
+        const int kt0 = t * kFwdBK;
+        const bool more = t + 1 < ntiles;
+        if (more) {
+          const int nk = kt0 + kFwdBK;
+          sk.load(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk);
+          sv.load(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk);
+        }
+        const char* K = smem + BUF * 2 * TILE;
+        const char* V = K + TILE;
+        f32x16 s[2][2];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+          for (int b = B0; b < 2; ++b) s[b][kt] = f32x16{};
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const bf16x8 kf = lds_frag(K + kt * 32 * RB + koff[c]);
+#pragma unroll
+            for (int b = B0; b < 2; ++b) s[b][kt] = mfma(kf, qf[b][c], s[b][kt]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 pf[2][4];
+#pragma unroll
+        for (int b = B0; b < 2; ++b) {
+          const int wq0 = b ? qbb : qa;
+          if ((CAUSAL && kt0 + kFwdBK - 1 > wq0) || kt0 + kFwdBK > seqlen) {
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+              const int lim = (CAUSAL ? min(row[b], seqlen - 1) : seqlen - 1) - (kt0 + 32 * kt + 4 * h);
+#pragma unroll
+              for (int i = 0; i < 16; ++i) s[b][kt][i] = acc_row0(i) > lim ? -INFINITY : s[b][kt][i];
+            }
+          }
+          float mx = s[b][0][0];
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[b][kt][i]);
+          mx = pair_max(mx) * P.c2;
+          if (__builtin_amdgcn_ballot_w64(mx > m[b] + kRescaleThreshold) != 0) {
+            const float mn = fmaxf(m[b], mx);
+            const float alpha = (mn == -INFINITY) ? 1.f : fexp2(m[b] - mn);
+            l[b] *= alpha;
+#pragma unroll
+            for (int d = 0; d < ND; ++d) acc[b][d] *= alpha;
+            m[b] = mn;
+          }
+          const float mu = (m[b] == -INFINITY) ? 0.f : m[b];
+          float rs = 0.f;
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const float p = fexp2(__builtin_fmaf(s[b][kt][i], P.c2, -mu));
+              s[b][kt][i] = p;
+              rs += p;
+            }
+          l[b] += rs;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pf[b][j] = pack8(s[b][j >> 1], j & 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const char* vb = V + 16 * j * RB;
+          bf16x8 vt[ND];
+#pragma unroll
+          for (int d = 0; d < ND; ++d) vt[d] = tr_frag_at(vb + toa[d], vb + tob[d]);
+#pragma unroll
+          for (int d = 0; d < ND; ++d)
+#pragma unroll
+            for (int b = B0; b < 2; ++b) acc[b][d] = mfma(vt[d], pf[b][j], acc[b][d]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) {
+          char* nb = smem + (1 - BUF) * 2 * TILE;
+          sk.store(nb);
+          sv.store(nb + TILE);
+        }
+        __syncthreads();
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      using BT = std::integral_constant<bool, true>;
+      using BF = std::integral_constant<bool, false>;
+      int t = 0;
+      for (; t + 1 <= lastA; t += 2) {  // both blocks, two tiles per trip (immediate buffer offsets)
+        tile_step(t, I0{}, BT{});
+        tile_step(t + 1, I1{}, BT{});
+      }
+      if (t <= lastA) {
+        tile_step(t, I0{}, BT{});
+        ++t;
+        if (t < ntiles) {
+          tile_step(t, I1{}, BF{});
+          ++t;
+        }
+      }
+      for (; t + 1 < ntiles; t += 2) {  // block B alone (causal diagonal); t is even here
+        tile_step(t, I0{}, BF{});
+        tile_step(t + 1, I1{}, BF{});
+      }
+      if (t < ntiles) tile_step(t, I0{}, BF{});
+
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float lt = pair_sum(l[b]);
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        uint16_t* op = P.o + ((int64_t)(s0 + min(row[b], seqlen - 1)) * P.hq + head) * D;
+        store_rows_wide<ND>(acc[b], inv, op, row[b] < seqlen);
+        if (row[b] < seqlen && h == 0)
+          P.lse[(int64_t)head * P.T + s0 + row[b]] = (lt > 0.f) ? (m[b] + log2f(lt)) * kLn2 : -INFINITY;
+      }
+    }
+    __syncthreads();  // the next item's index is in item_sh; LDS is free for its prologue
+    item = item_sh;
+  }
+}
+
 struct BwdParams {
   const uint16_t *q, *k, *v, *dout, *o;
   int64_t sq, sk, sv;  // token strides of q, k, v (dout and o are contiguous [T, Hq, D])
@@ -1284,6 +1489,29 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
   const char* variant = std::getenv("DTG_FA_FWD");
   const bool wide = !(variant != nullptr && variant[0] == 'n');
   const bool qlds = !(variant != nullptr && (variant[0] == 'n' || variant[0] == 'w'));
+  // DTG_FA_FWD=f64: the one-wave-per-SIMD persistent kernel (fwd64_kernel); plain causal /
+  // non-causal self-attention only (no window, key ranges, dropout or stamps)
+  const bool f64 = variant != nullptr && variant[0] == 'f';
+  if (f64 && drop == nullptr && P.window == 0 && P.kstart == nullptr && stamps == nullptr) {
+    const int nqb64 = (int)((max_seqlen + fa::kF64Rows - 1) / fa::kF64Rows);
+    const int64_t nitems = (int64_t)nqb64 * nseq * hq;
+    DTG_CHECK(nitems < (1ll << 31), "flash_attn: too many work items");
+    auto queue = at::zeros({1}, q.options().dtype(at::kInt));
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, q.device().index());
+    ncu = std::max(ncu, 1);
+    const int grid64 = (int)std::min<int64_t>(nitems, ncu);
+    const size_t lds64 = 4 * fa::kFwdBK * D * 2 + fa::kF64Rows * D * 2;
+#define DTG_FWD64(DD, C)                                                                                    \
+  do { set_lds_limit((const void*)&fa::fwd64_kernel<DD, C>, lds64);                                        \
+       hipLaunchKernelGGL((fa::fwd64_kernel<DD, C>), dim3(grid64), dim3(256), lds64, stream(), P,           \
+                          queue.data_ptr<int>(), nqb64, nseq); } while (0)
+    if (D == 128) { if (causal) DTG_FWD64(128, true); else DTG_FWD64(128, false); }
+    else { if (causal) DTG_FWD64(64, true); else DTG_FWD64(64, false); }
+#undef DTG_FWD64
+    DTG_LAUNCH_CHECK();
+    return {o, lse};
+  }
   const size_t lds = 4 * fa::kFwdBK * D * 2;
 #define DTG_FWD(DD, C, W, Q)                                                              \
   do { set_lds_limit((const void*)&fa::fwd_kernel<DD, C, W, Q>, lds);                        \

@@ -25,4 +25,14 @@ for cfg in dp8 tp8; do
       || { tail -20 "$O/torch_$cfg.log"; exit 1; }
   tail -1 "$O/torch_$cfg.log"
 done
+
+if [ "${FA64:-1}" = "1" ]; then
+  echo "[r5] f64 forward numerics + A/B"
+  timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "fwd_variants" -x -q --timeout 120 \
+      --timeout-method thread > "$O/f64_pytest.log" 2>&1 || { tail -30 "$O/f64_pytest.log"; exit 1; }
+  tail -2 "$O/f64_pytest.log"
+  timeout -k 10 300 python -u tools/bench_attention.py --ab v0,f64 > "$O/f64_ab.jsonl" 2>&1 \
+      || { tail -20 "$O/f64_ab.jsonl"; exit 1; }
+  cat "$O/f64_ab.jsonl"
+fi
 echo "[r5] done"
