@@ -245,6 +245,39 @@ struct Stager {
   }
 };
 
+// LDS-DMA copy of R rows x W bf16 (token stride `stride`) into the swizzled LDS image of Stager:
+// `buffer_load_dwordx4 ... lds` writes each lane's 16 bytes at M0 + 16 * lane, i.e. one 1-KiB
+// piece per wave-instruction, so a lane fetches the chunk whose swizzled place in the image is
+// its own position in the piece (a per-lane source address, CDNA guide App. B 'gather into
+// LDS').  No staging registers and no ds_write; rows at or past `nvalid` read as zeros from the
+// descriptor's range check.  Completion is the issuing wave's vmcnt (a __syncthreads drains it).
+template <int R, int W>
+struct DmaStager {
+  static constexpr int NCH = W / 8;            // 16-byte chunks per row
+  static constexpr int ROWS_PER_PIECE = 64 / NCH;
+  static constexpr int PIECES = R / ROWS_PER_PIECE;
+  static_assert(PIECES % 4 == 0, "pieces split over 4 waves");
+  __device__ __forceinline__ static void issue(const uint16_t* base, int64_t stride, int nvalid, char* tile) {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bytes = nvalid > 0 ? static_cast<int>((nvalid - 1) * stride * 2 + W * 2) : 0;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, bytes);
+    const int s2 = static_cast<int>(stride) * 2;
+    const int prow = lane / NCH, pc = lane % NCH;
+#pragma unroll
+    for (int j = 0; j < PIECES / 4; ++j) {
+      const int p = w * (PIECES / 4) + j;
+      const int row = p * ROWS_PER_PIECE + prow;
+      int sw;
+      if constexpr (NCH == 16) sw = ((row & 3) << 2) | ((row >> 2) & 3);
+      else sw = ((row & 1) << 2) | ((row >> 1) & 3);
+      const int ch = pc ^ sw;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(tile + p * 1024), 16,
+                                               row * s2 + ch * 16, 0, 0, 0);
+    }
+  }
+};
+
 // One lane's 16-byte slices of a row: elements [16c + 8h, +8) for c < D/16 (zero if !ok).
 template <int NC>
 __device__ __forceinline__ void load_row_frags(const uint16_t* row, bool ok, int h, bf16x8* out) {
@@ -740,6 +773,333 @@ __global__ __launch_bounds__(256, 1) void fwd64_kernel(FwdParams P, int* __restr
       }
     }
     __syncthreads();  // the next item's index is in item_sh; LDS is free for its prologue
+    item = item_sh;
+  }
+}
+
+// Software-pipelined form of fwd64_kernel ("p64"): with one wave per SIMD no partner wave
+// fills the matrix pipe while a wave runs its softmax, so the wave overlaps its own phases (CDNA
+// guide T15 / App. B): iteration i issues
+//   phase 1: S(i+1) = K(i+1) Q^T (32 MFMAs)      beside  the second half of softmax(i) -> P(i)
+//   phase 2: O += V(i)^T P(i)^T  (32 MFMAs)      beside  the first half of softmax(i+1)
+// as straight-line blocks (no branches inside; the rare lazy rescale of O and the causal /
+// sequence-end masks run between the phases), so the scheduler can interleave MFMAs and VALU.
+// The rescale is deferred to the next iteration's head: O and l still hold tile i's terms at the
+// old max when softmax(i+1) raises it, and both are multiplied exactly once, before anything at
+// the new max is added (T13's hazard).  K runs one tile ahead of V in the LDS ring.  Tiles on
+// the causal diagonal of the work item (where the blocks of a wave stop at different tiles) take
+// fwd64's non-pipelined step.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void fwd64p_kernel(FwdParams P, int* __restrict__ queue, int nqb, int nseq) {
+  constexpr int RB = 2 * D;
+  constexpr int TILE = kFwdBK * RB;
+  constexpr int NC = D / 16;
+  constexpr int ND = D / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1 | Q (256 rows)]
+  char* const qsm = smem + 4 * TILE;
+  __shared__ int item_sh;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int nitems = nqb * nseq * P.hq;
+  int koff[NC], toa[ND], tob[ND];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
+#pragma unroll
+  for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
+
+  if (threadIdx.x == 0) item_sh = atomicAdd(queue, 1);
+  __syncthreads();
+  int item = item_sh;
+  while (item < nitems) {
+    __syncthreads();
+    if (threadIdx.x == 0) item_sh = atomicAdd(queue, 1);
+    const int per_z = nseq * P.hq;
+    const int zz = item / per_z, rem = item - zz * per_z;
+    const int seq = rem / P.hq, head = grid_head(rem - seq * P.hq, P.hq, P.hkv);
+    const int qb = CAUSAL ? nqb - 1 - zz : zz;
+    const int s0 = P.cu[seq];
+    const int seqlen = P.cu[seq + 1] - s0;
+    const int q0 = qb * kF64Rows;
+    if (q0 < seqlen) {
+      const int kvh = head / (P.hq / P.hkv);
+      const int qa = q0 + 32 * w, qbb = q0 + 128 + 32 * w;
+      const int kv_end = CAUSAL ? min(seqlen, q0 + kF64Rows) : seqlen;
+      const int ntiles = (kv_end + kFwdBK - 1) / kFwdBK;
+      const int lastA = CAUSAL ? min(ntiles - 1, (qa + 31) / kFwdBK) : ntiles - 1;
+      // tiles [0, F): both blocks of every wave active -> pipelined; [F, ntiles): the diagonal
+      const int F = CAUSAL ? min(ntiles, q0 / kFwdBK + 1) : ntiles;
+      const uint16_t* kbase = P.k + (int64_t)s0 * P.sk + (int64_t)kvh * D;
+      const uint16_t* vbase = P.v + (int64_t)s0 * P.sv + (int64_t)kvh * D;
+      using KV = DmaStager<kFwdBK, D>;
+      DmaStager<kF64Rows, D>::issue(P.q + (int64_t)(s0 + q0) * P.sq + (int64_t)head * D, P.sq, seqlen - q0, qsm);
+      KV::issue(kbase, P.sk, seqlen, smem);
+      KV::issue(vbase, P.sv, seqlen, smem + TILE);
+      if (ntiles > 1) KV::issue(kbase + (int64_t)kFwdBK * P.sk, P.sk, seqlen - kFwdBK, smem + 2 * TILE);
+      __syncthreads();
+      // Q stays in LDS for the item (register budget: O, two S tiles and P are live at once);
+      // each k-step reads the two Q fragments and the two K fragments for its four MFMAs
+      const char* qrow[2] = {qsm + 32 * w * RB, qsm + (128 + 32 * w) * RB};
+      f32x16 acc[2][ND];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int d = 0; d < ND; ++d) acc[b][d] = f32x16{};
+      float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+      float alpha[2] = {1.f, 1.f}, rsp[2] = {0.f, 0.f};
+      bool pend[2] = {false, false};
+      const int row[2] = {qa + r, qbb + r};
+      f32x16 sE[2][2], sO[2][2];  // S of even / odd tiles: [block][32-key half]
+      bf16x8 pf[2][4];            // P of the tile PV consumes (keys 0..31 packed by sm_start, 32..63 by sm_finish)
+      bf16x8 pn[2][2];            // keys 0..31 of the next tile's P, packed as soon as exponentiated
+
+      auto qk = [&](const char* K, f32x16 (&sn)[2][2]) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) sn[b][kt] = f32x16{};
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const bf16x8 qa_ = lds_frag(qrow[0] + koff[c]);
+          const bf16x8 qb_ = lds_frag(qrow[1] + koff[c]);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            const bf16x8 kf = lds_frag(K + kt * 32 * RB + koff[c]);
+            sn[0][kt] = mfma(kf, qa_, sn[0][kt]);
+            sn[1][kt] = mfma(kf, qb_, sn[1][kt]);
+          }
+        }
+      };
+      auto mask = [&](int t, f32x16 (&sn)[2][2]) {
+        const int kt0 = t * kFwdBK;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int wq0 = b ? qbb : qa;
+          if ((CAUSAL && kt0 + kFwdBK - 1 > wq0) || kt0 + kFwdBK > seqlen) {
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+              const int lim = (CAUSAL ? min(row[b], seqlen - 1) : seqlen - 1) - (kt0 + 32 * kt + 4 * h);
+#pragma unroll
+              for (int i = 0; i < 16; ++i) sn[b][kt][i] = acc_row0(i) > lim ? -INFINITY : sn[b][kt][i];
+            }
+          }
+        }
+      };
+      // first half of the softmax: row max, lazy-rescale decision (deferred), exps of keys 0..31
+      auto sm_start = [&](f32x16 (&sn)[2][2]) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          float mx = sn[b][0][0];
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sn[b][kt][i]);
+          mx = pair_max(mx) * P.c2;
+          const bool grow = __builtin_amdgcn_ballot_w64(mx > m[b] + kRescaleThreshold) != 0;
+          const float mn = grow ? fmaxf(m[b], mx) : m[b];
+          alpha[b] = (mn == -INFINITY) ? 1.f : fexp2(m[b] - mn);
+          pend[b] = grow;
+          m[b] = mn;
+          const float mu = (mn == -INFINITY) ? 0.f : mn;
+          float rs = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float p = fexp2(__builtin_fmaf(sn[b][0][i], P.c2, -mu));
+            sn[b][0][i] = p;
+            rs += p;
+          }
+          rsp[b] = rs;
+          pn[b][0] = pack8(sn[b][0], 0);
+          pn[b][1] = pack8(sn[b][0], 1);
+        }
+      };
+      // second half: exps of keys 32..63, row sums into l, P packed to bf16 fragments
+      auto sm_finish = [&](f32x16 (&sc)[2][2]) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const float mu = (m[b] == -INFINITY) ? 0.f : m[b];
+          float rs = rsp[b];
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float p = fexp2(__builtin_fmaf(sc[b][1][i], P.c2, -mu));
+            sc[b][1][i] = p;
+            rs += p;
+          }
+          l[b] += rs;
+          pf[b][0] = pn[b][0];
+          pf[b][1] = pn[b][1];
+          pf[b][2] = pack8(sc[b][1], 0);
+          pf[b][3] = pack8(sc[b][1], 1);
+        }
+      };
+      auto rescale = [&]() {  // O and l of the blocks whose max rose: exactly once, before new terms
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (pend[b]) {
+            l[b] *= alpha[b];
+#pragma unroll
+            for (int d = 0; d < ND; ++d) acc[b][d] *= alpha[b];
+            pend[b] = false;
+          }
+        }
+      };
+      auto pv = [&](const char* V) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const char* vb = V + 16 * j * RB;
+          bf16x8 vt[ND];
+#pragma unroll
+          for (int d = 0; d < ND; ++d) vt[d] = tr_frag_at(vb + toa[d], vb + tob[d]);
+#pragma unroll
+          for (int d = 0; d < ND; ++d)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[b][d] = mfma(vt[d], pf[b][j], acc[b][d]);
+        }
+      };
+      // prologue of the pipeline: S(0) and the first half of its softmax
+      qk(smem, sE);
+      mask(0, sE);
+      sm_start(sE);
+      pend[0] = pend[1] = false;  // O and l are still zero
+
+      auto iter = [&](int i, auto buf, auto next_c, f32x16 (&sc)[2][2], f32x16 (&sn)[2][2]) {
+        constexpr int BUF = decltype(buf)::value;  // LDS stage of tile i (and of K(i+2))
+        constexpr bool NEXT = decltype(next_c)::value;
+        // K(i+2) over K(i) (read in the previous iteration), V(i+1) over V(i-1): both slots free
+        if (i + 2 <= F && i + 2 < ntiles)
+          KV::issue(kbase + (int64_t)(i + 2) * kFwdBK * P.sk, P.sk, seqlen - (i + 2) * kFwdBK, smem + BUF * 2 * TILE);
+        if (i + 1 < ntiles)
+          KV::issue(vbase + (int64_t)(i + 1) * kFwdBK * P.sv, P.sv, seqlen - (i + 1) * kFwdBK,
+                    smem + (1 - BUF) * 2 * TILE + TILE);
+        rescale();
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (NEXT) qk(smem + (1 - BUF) * 2 * TILE, sn);  // K(i+1)
+        sm_finish(sc);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (NEXT) mask(i + 1, sn);
+        __builtin_amdgcn_sched_barrier(0);
+        pv(smem + BUF * 2 * TILE + TILE);  // V(i)
+        if constexpr (NEXT) sm_start(sn);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();  // drains this wave's DMAs (vmcnt) and orders every wave's reads before reuse
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      using BT = std::integral_constant<bool, true>;
+      using BF = std::integral_constant<bool, false>;
+      int i = 0;
+      for (; i + 2 < F; i += 2) {
+        iter(i, I0{}, BT{}, sE, sO);
+        iter(i + 1, I1{}, BT{}, sO, sE);
+      }
+      if (F - i == 2) {
+        iter(i, I0{}, BT{}, sE, sO);
+        iter(i + 1, I1{}, BF{}, sO, sE);
+      } else {
+        iter(i, I0{}, BF{}, sE, sO);
+      }
+
+      // the causal diagonal: fwd64's step (blocks stop at different tiles)
+      auto tile_step = [&](int t, auto buf, auto both_c) {
+        constexpr int BUF = decltype(buf)::value;
+        constexpr bool BOTH = decltype(both_c)::value;
+        constexpr int B0 = BOTH ? 0 : 1;
+        const int kt0 = t * kFwdBK;
+        if (t + 1 < ntiles) {  // both slots of the other stage were last read by step t - 1
+          const int nk = kt0 + kFwdBK;
+          char* nb = smem + (1 - BUF) * 2 * TILE;
+          KV::issue(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk, nb);
+          KV::issue(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk, nb + TILE);
+        }
+        const char* K = smem + BUF * 2 * TILE;
+        const char* V = K + TILE;
+        f32x16 s[2][2];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+          for (int b = B0; b < 2; ++b) s[b][kt] = f32x16{};
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const bf16x8 kf = lds_frag(K + kt * 32 * RB + koff[c]);
+#pragma unroll
+            for (int b = B0; b < 2; ++b) s[b][kt] = mfma(kf, lds_frag(qrow[b] + koff[c]), s[b][kt]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int b = B0; b < 2; ++b) {
+          const int wq0 = b ? qbb : qa;
+          if ((CAUSAL && kt0 + kFwdBK - 1 > wq0) || kt0 + kFwdBK > seqlen) {
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+              const int lim = (CAUSAL ? min(row[b], seqlen - 1) : seqlen - 1) - (kt0 + 32 * kt + 4 * h);
+#pragma unroll
+              for (int q = 0; q < 16; ++q) s[b][kt][q] = acc_row0(q) > lim ? -INFINITY : s[b][kt][q];
+            }
+          }
+          float mx = s[b][0][0];
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) mx = fmaxf(mx, s[b][kt][q]);
+          mx = pair_max(mx) * P.c2;
+          if (__builtin_amdgcn_ballot_w64(mx > m[b] + kRescaleThreshold) != 0) {
+            const float mn = fmaxf(m[b], mx);
+            const float al = (mn == -INFINITY) ? 1.f : fexp2(m[b] - mn);
+            l[b] *= al;
+#pragma unroll
+            for (int d = 0; d < ND; ++d) acc[b][d] *= al;
+            m[b] = mn;
+          }
+          const float mu = (m[b] == -INFINITY) ? 0.f : m[b];
+          float rs = 0.f;
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const float p = fexp2(__builtin_fmaf(s[b][kt][q], P.c2, -mu));
+              s[b][kt][q] = p;
+              rs += p;
+            }
+          l[b] += rs;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pf[b][j] = pack8(s[b][j >> 1], j & 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const char* vb = V + 16 * j * RB;
+          bf16x8 vt[ND];
+#pragma unroll
+          for (int d = 0; d < ND; ++d) vt[d] = tr_frag_at(vb + toa[d], vb + tob[d]);
+#pragma unroll
+          for (int d = 0; d < ND; ++d)
+#pragma unroll
+            for (int b = B0; b < 2; ++b) acc[b][d] = mfma(vt[d], pf[b][j], acc[b][d]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+      };
+      for (int t = F; t < ntiles; ++t) {
+        const bool both = t <= lastA;
+        if (t & 1) {
+          if (both) tile_step(t, I1{}, BT{}); else tile_step(t, I1{}, BF{});
+        } else {
+          if (both) tile_step(t, I0{}, BT{}); else tile_step(t, I0{}, BF{});
+        }
+      }
+
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float lt = pair_sum(l[b]);
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        uint16_t* op = P.o + ((int64_t)(s0 + min(row[b], seqlen - 1)) * P.hq + head) * D;
+        store_rows_wide<ND>(acc[b], inv, op, row[b] < seqlen);
+        if (row[b] < seqlen && h == 0)
+          P.lse[(int64_t)head * P.T + s0 + row[b]] = (lt > 0.f) ? (m[b] + log2f(lt)) * kLn2 : -INFINITY;
+      }
+    }
+    __syncthreads();
     item = item_sh;
   }
 }
@@ -1491,7 +1851,7 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
   const bool qlds = !(variant != nullptr && (variant[0] == 'n' || variant[0] == 'w'));
   // DTG_FA_FWD=f64: the one-wave-per-SIMD persistent kernel (fwd64_kernel); plain causal /
   // non-causal self-attention only (no window, key ranges, dropout or stamps)
-  const bool f64 = variant != nullptr && variant[0] == 'f';
+  const bool f64 = variant != nullptr && (variant[0] == 'f' || variant[0] == 'p');
   if (f64 && drop == nullptr && P.window == 0 && P.kstart == nullptr && stamps == nullptr) {
     const int nqb64 = (int)((max_seqlen + fa::kF64Rows - 1) / fa::kF64Rows);
     const int64_t nitems = (int64_t)nqb64 * nseq * hq;
@@ -1506,8 +1866,16 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
   do { set_lds_limit((const void*)&fa::fwd64_kernel<DD, C>, lds64);                                        \
        hipLaunchKernelGGL((fa::fwd64_kernel<DD, C>), dim3(grid64), dim3(256), lds64, stream(), P,           \
                           queue.data_ptr<int>(), nqb64, nseq); } while (0)
-    if (D == 128) { if (causal) DTG_FWD64(128, true); else DTG_FWD64(128, false); }
+#define DTG_FWD64P(DD, C)                                                                                   \
+  do { set_lds_limit((const void*)&fa::fwd64p_kernel<DD, C>, lds64);                                       \
+       hipLaunchKernelGGL((fa::fwd64p_kernel<DD, C>), dim3(grid64), dim3(256), lds64, stream(), P,          \
+                          queue.data_ptr<int>(), nqb64, nseq); } while (0)
+    if (variant[0] == 'p') {
+      if (D == 128) { if (causal) DTG_FWD64P(128, true); else DTG_FWD64P(128, false); }
+      else { if (causal) DTG_FWD64P(64, true); else DTG_FWD64P(64, false); }
+    } else if (D == 128) { if (causal) DTG_FWD64(128, true); else DTG_FWD64(128, false); }
     else { if (causal) DTG_FWD64(64, true); else DTG_FWD64(64, false); }
+#undef DTG_FWD64P
 #undef DTG_FWD64
     DTG_LAUNCH_CHECK();
     return {o, lse};

@@ -435,7 +435,7 @@ def test_flash_attn_d64_mha(cuda, seqlens):
     _attn_case(cuda, seqlens, hq=4, hkv=4, D=64, causal=True)
 
 
-@pytest.mark.parametrize("variant", ["narrow", "wide", "qlds", "f64"])
+@pytest.mark.parametrize("variant", ["narrow", "wide", "qlds", "f64", "p64"])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attn_fwd_variants(cuda, variant, causal, monkeypatch):
     """Every forward variant (DTG_FA_FWD, read per call) against the fp32 reference, including
