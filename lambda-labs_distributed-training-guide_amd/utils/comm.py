@@ -7,6 +7,8 @@ by the TP/SP functions and the DDP/ZeRO/FSDP engines.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -71,6 +73,28 @@ def rs_input_buffer(group, shape, dtype, stage_bytes: int = 0):
     return c.rs_input_buffer(shape, dtype, stage_bytes)
 
 
+# DTG_FAKE_WORLD rehearsals (utils/dist.py): the fake process group returns at once and leaves
+# every output untouched -- uninitialised memory, whose bf16 reading holds NaN / Inf patterns that
+# poison the run after one step (and NaN operands draw less MFMA power than real data, so the
+# rehearsal's timings would flatter it).  These fills stand in for the other ranks with this
+# rank's data: a gather writes x into every chunk, a reduce-scatter keeps this rank's own chunk.
+# The cost is one device copy of the collective's output -- the local write traffic the real
+# collective has too -- so a rehearsal's step includes it.
+_FAKE = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0) > 1
+
+
+def fake_fill_gather(out: torch.Tensor, x: torch.Tensor, group=None) -> None:
+    if _FAKE and backend_of(group) == "fake":
+        n = world(group)
+        out.view(n, -1).copy_(x.reshape(1, -1).expand(n, -1))
+
+
+def fake_fill_scatter(out: torch.Tensor, x: torch.Tensor, group=None) -> None:
+    if _FAKE and backend_of(group) == "fake":
+        n, r = world(group), rank(group)
+        out.view(-1).copy_(x.reshape(n, -1)[r])
+
+
 def _xgmi_for(group, x: torch.Tensor, nbytes: int):
     c = _XGMI.get(group)
     if c is not None and x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and c.fits(nbytes):
@@ -87,6 +111,7 @@ def all_gather_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
     if c is not None:
         return c.all_gather_into(out, x)
     dist.all_gather_into_tensor(out, x, group=group)
+    fake_fill_gather(out, x, group)
     return out
 
 
@@ -119,6 +144,7 @@ def reduce_scatter_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
         c.release_slot(x, None)  # stream-ordered: the slot is free for the next producer
         return out
     dist.reduce_scatter_tensor(out, x, group=group)
+    fake_fill_scatter(out, x, group)
     return out
 
 
@@ -140,6 +166,8 @@ def all_to_all_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
         return full[:, r].reshape(x.shape).contiguous()
     out = torch.empty_like(x)
     dist.all_to_all_single(out, x, group=group)
+    if _FAKE and backend_of(group) == "fake":
+        out.copy_(x)
     return out
 
 
@@ -158,12 +186,16 @@ def all_gather_stack_async(x: torch.Tensor, group=None):
     if backend_of(group) == "gloo":
         dist.all_gather(list(out.unbind(0)), x, group=group)
         return out, _DoneWork()
-    return out, dist.all_gather_into_tensor(out, x, group=group, async_op=True)
+    work = dist.all_gather_into_tensor(out, x, group=group, async_op=True)
+    fake_fill_gather(out, x, group)
+    return out, work
 
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group=None, async_op=False):
     """Flat all-gather: out.numel() == shard.numel() * world."""
-    return dist.all_gather_into_tensor(out, shard, group=group, async_op=async_op)
+    work = dist.all_gather_into_tensor(out, shard, group=group, async_op=async_op)
+    fake_fill_gather(out, shard, group)
+    return work
 
 
 class _DoneWork:
@@ -182,7 +214,9 @@ def reduce_scatter_into(out: torch.Tensor, full: torch.Tensor, group=None, async
         n = out.numel()
         out.copy_(full.view(-1)[r * n:(r + 1) * n].view_as(out))
         return _DoneWork() if async_op else None
-    return dist.reduce_scatter_tensor(out, full, group=group, async_op=async_op)
+    work = dist.reduce_scatter_tensor(out, full, group=group, async_op=async_op)
+    fake_fill_scatter(out, full, group)
+    return work
 
 
 # ------------------------------------------------------------------------------------------------
@@ -238,7 +272,9 @@ def all_gather_dim0_into_async(out: torch.Tensor, x: torch.Tensor, group=None):
     if backend_of(group) == "gloo":
         dist.all_gather_into_tensor(out, x, group=group)
         return _DoneWork()
-    return dist.all_gather_into_tensor(out, x, group=group, async_op=True)
+    work = dist.all_gather_into_tensor(out, x, group=group, async_op=True)
+    fake_fill_gather(out, x, group)
+    return work
 
 
 def reduce_scatter_dim0_into_async(out: torch.Tensor, x: torch.Tensor, group=None):
@@ -259,4 +295,6 @@ def reduce_scatter_dim0_into_async(out: torch.Tensor, x: torch.Tensor, group=Non
         r, rows = rank(group), out.shape[0]
         out.copy_(y[r * rows:(r + 1) * rows])
         return _DoneWork()
-    return dist.reduce_scatter_tensor(out, x, group=group, async_op=True)
+    work = dist.reduce_scatter_tensor(out, x, group=group, async_op=True)
+    fake_fill_scatter(out, x, group)
+    return work

@@ -290,3 +290,23 @@ def test_fake_world_runs_one_rank_of_a_larger_job(tmp_path):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "'global_step': 2" in out, out[-3000:]
+
+
+def test_fake_world_2d_rehearsal_stays_finite(tmp_path):
+    """DTG_FAKE_WORLD=8 with chapter 07's 2-D mesh (tp 2 x dp 4): the fake group's collectives
+    leave their outputs untouched, so utils/comm.py fills them with this rank's data; without
+    that the sequence-parallel gathers read uninitialised memory and the loss turns NaN after
+    one step.  Every logged loss is finite."""
+    import math
+    import re
+
+    env = dict(os.environ, DTG_FAKE_WORLD="8", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "train_llm.py", "-e", "fw2d", "-m", "llama-tiny-d128", "-b", "2", "-s", "64", "-d",
+           "synthetic", "--save-dir", str(tmp_path), "--ckpt-freq", "1000", "--max-steps", "3", "--log-freq", "1",
+           "--num-workers", "0", "--tp", "2", "--cpu-offload", "on", "--offload-params", "off"]
+    r = subprocess.run(cmd, cwd=os.path.join(ROOT, "07-2d-parallel"), env=env, capture_output=True, text=True,
+                       timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    losses = [float(x) for x in re.findall(r"'running_loss': ([0-9.eEna+-]+)", out)]
+    assert len(losses) >= 3 and all(math.isfinite(x) for x in losses), losses
