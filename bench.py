@@ -371,9 +371,17 @@ def bucket_sweep(args, torch, dist, device, world, rank, cuda):
                           device=device)
         if world > 1:
             dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        # every replica must hold bit-identical weights after the steps (over the copy engines on
+        # a real node: the cross-device check of the shared-buffer path, csrc/comm/xgmi.hip)
+        csum = torch.tensor([replica_checksum(engine, torch)], dtype=torch.float64, device=device)
+        sums = [torch.zeros_like(csum) for _ in range(world)] if world > 1 else [csum]
+        if world > 1:
+            dist.all_gather(sums, csum)
+        sums = [float(t.item()) for t in sums]
         out.append({"bucket_mb": mb, "dp_comm": getattr(engine, "dp_comm", "rccl"),
                     "buckets": len(engine.space.buckets) if hasattr(engine, "space") else None,
-                    "ms_per_step": round(float(ms.item()), 2)})
+                    "ms_per_step": round(float(ms.item()), 2),
+                    "replicas_consistent": None if sums[0] != sums[0] else len(set(sums)) == 1})
         del model, engine, opt, ids_all, step
         close_job(job, torch)
         import gc
@@ -489,12 +497,19 @@ def _xgmi_sweep(torch, dist, device, world, cuda, sizes):
     try:
         from dtg.parallel.xgmi import XgmiCommunicator
 
+        from dtg.utils import comm
+
         xc = XgmiCommunicator(None, capacity_bytes=max(sizes) << 20, device=device)
+        gen = torch.Generator(device=device).manual_seed(1000 + dist.get_rank())
         for mib in sizes:
             n = (mib << 20) // 2 // world * world
-            x = torch.randn(n, device=device).to(torch.bfloat16)
+            x = torch.randn(n, device=device, generator=gen).to(torch.bfloat16)  # differs per rank
             shard = torch.empty(n // world, device=device, dtype=torch.bfloat16)
             full = torch.empty(n, device=device, dtype=torch.bfloat16)
+            # cross-device correctness on a real node (every xGMI test of the suite shares one GPU):
+            # the process group's result of the same message is the reference
+            ref_shard = comm.reduce_scatter_dim0(x, None).float()
+            ref_full = None
             for eng in ("kernel", "dma"):
                 xc.gather_engine = eng
                 for op, fn in (("reduce_scatter", lambda: xc.reduce_scatter_into(shard, x)),
@@ -502,14 +517,20 @@ def _xgmi_sweep(torch, dist, device, world, cuda, sizes):
                     iters = 5 if mib >= 128 else 10
                     fn()
                     _sync(dist, world, cuda)
+                    if op == "reduce_scatter":  # sums in another order: bf16-rounding tolerance
+                        check = {"max_rel_err": float((shard.float() - ref_shard).abs().max() /
+                                                      ref_shard.abs().max().clamp_min(1e-30))}
+                        ref_full = comm.all_gather_dim0(shard, None)
+                    else:  # pure copies: bit-identical
+                        check = {"equal": bool(torch.equal(full, ref_full))}
                     t0 = time.perf_counter()
                     for _ in range(iters):
                         fn()
                     _sync(dist, world, cuda)
                     dt = (time.perf_counter() - t0) / iters
                     rows.append({"op": f"{op}_xgmi_{eng}", "mib": mib, "us": round(dt * 1e6, 1),
-                                 "busbw_gbs": round(n * 2 / dt / 1e9 * (world - 1) / world, 4)})
-            del x, shard, full
+                                 "busbw_gbs": round(n * 2 / dt / 1e9 * (world - 1) / world, 4), **check})
+            del x, shard, full, ref_shard, ref_full
         xc.check()
     except Exception as e:  # a diagnostic: never lose the run's JSON line over it
         rows.append({"op": "xgmi", "error": repr(e)[:300]})

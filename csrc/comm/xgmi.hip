@@ -529,9 +529,19 @@ void all_reduce(int64_t id, const at::Tensor& inout, int64_t offset) {
 // pulls at arbitrary byte ranges of the peers' copies: a reduce-scatter pulls this rank's slice
 // of a bucket from every peer into a local scratch and sums it; an all-gather pulls every peer's
 // updated slice straight into place.  Only the one-wave barrier kernel and the local reduce
-// touch the shader array.  Memory is ordinary (cached) device memory: a producer kernel's
-// results are written back at its end, before the barrier kernel that follows it on the stream
-// signals the peers.
+// touch the shader array.  Memory is ordinary (cached, coarse-grained) device memory, unlike the
+// uncached workspace above, because no kernel here reads a peer's copy while that peer may still
+// be writing it.  The workspace is read by pull KERNELS that poll peer flags mid-kernel, which
+// needs fine-grained (uncached) memory.  Here every cross-device access is a copy-engine
+// transfer, and each one is separated from the kernels that produce or consume the data by
+// kernel boundaries.  Coarse-grained memory is coherent at those boundaries:
+//  * producer side: the kernel that wrote a bucket ends with a release that writes its dirty L2
+//    lines back to HBM, and only then does the barrier kernel after it on the stream signal the
+//    peers whose copy engines read the bucket;
+//  * consumer side: copy-engine writes go to HBM, not into this GPU's L2, and the next kernel that
+//    reads the destination starts with an acquire that invalidates the L2's stale lines.
+// (All xGMI tests so far share one GPU, so this is the HIP coarse-grained rule, not yet a
+// cross-device measurement; the bench's N > 1 xGMI child checks replica checksums on a real node.)
 
 // Own allocation; the tensor's deleter frees it (peers keep their mapping until they close it).
 at::Tensor alloc_shared(int64_t id, int64_t nbytes) {

@@ -361,7 +361,6 @@ class FullyShard:
                 u.gathered = True
                 return
             u.gather_work = dist.all_gather_into_tensor(u.full, shard, group=self.group, async_op=True)
-            comm.fake_fill_gather(u.full, shard, self.group)
         u._gather_src = shard  # keep the (H2D) source alive until the gather completes
 
     def _wait_gather(self, u: _Unit):

@@ -73,20 +73,15 @@ def rs_input_buffer(group, shape, dtype, stage_bytes: int = 0):
     return c.rs_input_buffer(shape, dtype, stage_bytes)
 
 
-# DTG_FAKE_WORLD rehearsals (utils/dist.py): the fake process group returns at once and leaves
-# every output untouched -- uninitialised memory, whose bf16 reading holds NaN / Inf patterns that
-# poison the run after one step (and NaN operands draw less MFMA power than real data, so the
-# rehearsal's timings would flatter it).  These fills stand in for the other ranks with this
-# rank's data: a gather writes x into every chunk, a reduce-scatter keeps this rank's own chunk.
-# The cost is one device copy of the collective's output -- the local write traffic the real
-# collective has too -- so a rehearsal's step includes it.
+# DTG_FAKE_WORLD rehearsals (utils/dist.py): the fake process group returns at once.  Its
+# gathers write the local input into every chunk of the output, but its reduce-scatters and
+# all-to-alls leave the output untouched: uninitialised memory, whose bf16 reading holds NaN / Inf
+# patterns that poison the run (and NaN operands draw less power in the power-limited GEMMs, so
+# a rehearsal on them times 12-14 % fast, profiles/r5/405b_fill/).  These fills stand in for the
+# other ranks with this rank's data: a reduce-scatter keeps this rank's own chunk of its input, an
+# all-to-all returns its input -- one device copy of the output, the local write traffic the real
+# collective has too.
 _FAKE = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0) > 1
-
-
-def fake_fill_gather(out: torch.Tensor, x: torch.Tensor, group=None) -> None:
-    if _FAKE and backend_of(group) == "fake":
-        n = world(group)
-        out.view(n, -1).copy_(x.reshape(1, -1).expand(n, -1))
 
 
 def fake_fill_scatter(out: torch.Tensor, x: torch.Tensor, group=None) -> None:
@@ -111,7 +106,6 @@ def all_gather_dim0(x: torch.Tensor, group=None) -> torch.Tensor:
     if c is not None:
         return c.all_gather_into(out, x)
     dist.all_gather_into_tensor(out, x, group=group)
-    fake_fill_gather(out, x, group)
     return out
 
 
@@ -187,14 +181,12 @@ def all_gather_stack_async(x: torch.Tensor, group=None):
         dist.all_gather(list(out.unbind(0)), x, group=group)
         return out, _DoneWork()
     work = dist.all_gather_into_tensor(out, x, group=group, async_op=True)
-    fake_fill_gather(out, x, group)
     return out, work
 
 
 def all_gather_into(out: torch.Tensor, shard: torch.Tensor, group=None, async_op=False):
     """Flat all-gather: out.numel() == shard.numel() * world."""
     work = dist.all_gather_into_tensor(out, shard, group=group, async_op=async_op)
-    fake_fill_gather(out, shard, group)
     return work
 
 
@@ -273,7 +265,6 @@ def all_gather_dim0_into_async(out: torch.Tensor, x: torch.Tensor, group=None):
         dist.all_gather_into_tensor(out, x, group=group)
         return _DoneWork()
     work = dist.all_gather_into_tensor(out, x, group=group, async_op=True)
-    fake_fill_gather(out, x, group)
     return work
 
 

@@ -37,8 +37,9 @@ def init_distributed(backend: Optional[str] = None, timeout_minutes: int = 30, l
     rank = _env_int("RANK", "OMPI_COMM_WORLD_RANK", "SLURM_PROCID", "PMI_RANK", default=0)
     world = _env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "SLURM_NTASKS", "PMI_SIZE", default=1)
     # DTG_FAKE_WORLD=W (one process, no launcher): run as rank 0 of a W-rank job whose other ranks
-    # are PyTorch's `fake` process group -- every collective returns at once with its output
-    # untouched.  Shard sizes, gathered buffers, allocations and per-rank compute are those of a
+    # are PyTorch's `fake` process group -- every collective returns at once (gathers replicate
+    # the local input; utils/comm.py fills the reduce-scatter / all-to-all outputs it leaves
+    # untouched).  Shard sizes, gathered buffers, allocations and per-rank compute are those of a
     # real W-rank job; the numerics are not (a memory / per-rank-compute rehearsal only).
     fake_world = int(os.environ.get("DTG_FAKE_WORLD", "0") or 0)
     if fake_world > 1:
