@@ -332,7 +332,11 @@ def replica_checksum(engine, torch):
         return float("nan")
     if hasattr(engine, "wait_param_gather"):
         engine.wait_param_gather()
-    return float(space.param_buf.double().sum().item())
+    buf = space.param_buf.view(-1)
+    tot = torch.zeros((), dtype=torch.float64, device=buf.device)
+    for i in range(0, buf.numel(), 1 << 26):  # 512 MB of f64 at a time (a whole-buffer copy is 8 B/param)
+        tot += buf[i:i + (1 << 26)].double().sum()
+    return float(tot.item())
 
 
 def bucket_sweep(args, torch, dist, device, world, rank, cuda):
