@@ -351,6 +351,14 @@ def bucket_sweep(args, torch, dist, device, world, rank, cuda):
     if cuda and args.parallel == "zero" and args.sweep_other_dp_comm and (other == "rccl" or not args.xgmi_child):
         runs.append((args.bucket_mb, other))  # the other ZeRO transport at the default bucket size
     for mb, dpc in runs:
+        # the sweep rebuilds the whole job per size: stop between runs once the diagnostic budget
+        # is spent (every rank decides from the same broadcast clock, so all skip together)
+        late = torch.tensor([float(time.time() - T_START > args.diag_budget_s)], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.broadcast(late, src=0)
+        if late.item() > 0:
+            out.append({"bucket_mb": mb, "dp_comm": dpc, "skipped": "diagnostic budget spent"})
+            continue
         try:
             job = build_job(args, torch, device, cuda, bucket_mb=mb, dp_comm=dpc)
         except Exception as e:  # a diagnostic row: never lose the run's JSON line over it

@@ -24,7 +24,7 @@ for spec in $runs; do
   (cd 07-2d-parallel && DTG_FAKE_WORLD=8 OMP_NUM_THREADS=$SHARE timeout -k 10 560 python -u train_llm.py \
      -e r405_2d -m meta-llama/Llama-3.1-405B --num-layers $depth -b $b -s 4096 -d synthetic --num-workers 1 \
      --tp $tp --save-dir /tmp/dtg405_2d --ckpt-freq 100000 --max-steps 4 --log-freq 1 --cpu-offload on \
-     --offload-params off --activation-checkpointing on --pin-numa on --cpu-share $SHARE > $log 2>&1)
+     --offload-params off --activation-checkpointing on --pin-numa on --cpu-share $SHARE ${EXTRA:-} > $log 2>&1)
   rc=$?
   echo "tp=$tp b=$b depth=$depth rc=$rc"
   grep -E "global_step': [34]," $log | grep -oE "'(tok/s|time/forward|time/backward|time/update|time/total|peak_alloc_gb|peak_reserved_gb|offload/[a-z0-9_]+|host/[a-z_]+)': [0-9.]+" | tr '\n' ' '; echo

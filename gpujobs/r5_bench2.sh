@@ -9,9 +9,12 @@ O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r5_bench2}
 mkdir -p "$O"
 export TMPDIR=/tmp
 t0=$(date +%s)
+# the gloo steps (host-staged 16 GB gradients) run ~14 s each with no output: keep the call alive
+( while true; do sleep 50; echo "[bench2] alive $(( $(date +%s) - t0 )) s"; done ) & HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 DTG_SHARED_DEVICE=1 timeout -k 10 560 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29631 bench.py --gpus 2 --backend gloo --batch-size 8 \
-    --steps 5 --warmup 2 > "$O/bench2.log" 2>&1 || { tail -30 "$O/bench2.log"; exit 1; }
+    --steps 3 --warmup 1 > "$O/bench2.log" 2>&1 || { tail -30 "$O/bench2.log"; exit 1; }
 echo "wall_outside_s=$(( $(date +%s) - t0 ))" | tee "$O/wall.txt"
 grep '^{' "$O/bench2.log" | tail -1 > "$O/bench2.json"
 python3 -c "

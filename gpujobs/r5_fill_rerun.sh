@@ -10,7 +10,7 @@ mkdir -p "$O"
 export TMPDIR=/tmp
 for cfg in dp8 tp8; do
   extra=""; [ "$cfg" = "tp8" ] && extra="--tp 8"
-  DTG_FAKE_WORLD=8 timeout -k 10 300 python3 bench.py --gpus 8 $extra --steps 10 --warmup 3 --ref-steps 0 \
+  DTG_FAKE_WORLD=8 timeout -k 10 300 python3 bench.py --gpus 8 $extra --steps 10 --warmup 3 --ref-steps 0 ${EXTRA:-} \
       --fsdp-mem-steps 0 > "$O/bench_$cfg.log" 2>&1 || { tail -20 "$O/bench_$cfg.log"; exit 1; }
   tail -1 "$O/bench_$cfg.log" | cut -c1-400
 done
