@@ -190,7 +190,16 @@ def _chunk_ctx(rc: RunCtx, rows: int) -> RunCtx:
 class _VocabParallelEmbedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, w, vstart):
+        from ..utils.comm import _FAKE
+
         local = ids - vstart
+        if _FAKE:
+            # DTG_FAKE_WORLD rehearsal: the other ranks' rows of this sum never arrive, so a token
+            # outside this shard would keep an all-zero hidden state -- for the first token of a
+            # sequence through every layer (it attends only to itself), and each RMSNorm backward
+            # then multiplies its gradient by 1/sqrt(eps) until bf16 overflows
+            # (profiles/r5/fake_nan/).  Every token takes a row of this shard instead (same cost).
+            local = torch.remainder(local, w.shape[0])
         mask = (local < 0) | (local >= w.shape[0])
         local = local.masked_fill(mask, 0)
         out = torch.nn.functional.embedding(local, w)

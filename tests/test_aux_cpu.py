@@ -310,3 +310,25 @@ def test_fake_world_2d_rehearsal_stays_finite(tmp_path):
     assert r.returncode == 0, out[-3000:]
     losses = [float(x) for x in re.findall(r"'running_loss': ([0-9.eEna+-]+)", out)]
     assert len(losses) >= 3 and all(math.isfinite(x) for x in losses), losses
+
+
+def test_fake_world_vocab_parallel_embedding_has_no_zero_rows(monkeypatch):
+    """Under DTG_FAKE_WORLD the vocab-parallel embedding's sum over TP ranks never arrives, so a
+    token outside this rank's shard would get an all-zero row.  The first token of a sequence then
+    stays zero through every layer, and the RMSNorm backward overflows bf16
+    (profiles/r5/fake_nan/).  In the rehearsal every token takes a row of this shard; outside it,
+    the masking is unchanged."""
+    import torch
+
+    from dtg.models import llama
+    from dtg.utils import comm
+
+    w = torch.randn(16, 8)
+    ids = torch.arange(64)  # vocab 64 over 4 ranks; this rank holds rows 16..31
+    monkeypatch.setattr(comm, "_FAKE", False)
+    real = llama._VocabParallelEmbedding.apply(ids, w, 16)
+    assert int((real.abs().sum(1) == 0).sum()) == 48
+    monkeypatch.setattr(comm, "_FAKE", True)
+    fake = llama._VocabParallelEmbedding.apply(ids, w, 16)
+    assert bool((fake.abs().sum(1) > 0).all())
+    assert torch.equal(fake[16:32], real[16:32])
