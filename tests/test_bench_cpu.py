@@ -222,3 +222,21 @@ def test_bench_diagnostic_budget_skips_phases():
     for name in ("collectives", "bucket_sweep", "fsdp_mem"):
         assert "budget" in rec["diagnostic_errors"][name]
     assert "collectives" not in rec and "fsdp_mem" not in rec
+
+
+def test_bucket_sweep_stops_between_runs_once_the_budget_is_spent():
+    """The bucket sweep rebuilds the whole job per size, so it checks the diagnostic budget
+    before every run, not only when the phase starts (a 2-rank 8B rehearsal's sweep ran 264 s
+    past a phase start at 107 s, profiles/r5/bench2/)."""
+    import argparse
+    import sys as _sys
+
+    import torch
+
+    _sys.path.insert(0, ROOT)
+    import bench
+
+    args = argparse.Namespace(bucket_sweep_mb="1,4", batch_size=2, seq_len=32, dp_comm="rccl", parallel="zero",
+                              sweep_other_dp_comm=0, xgmi_child=0, bucket_mb=4, diag_budget_s=-1.0, sweep_steps=1)
+    out = bench.bucket_sweep(args, torch, None, torch.device("cpu"), 1, 0, False)
+    assert [r.get("skipped") for r in out] == ["diagnostic budget spent"] * 2
