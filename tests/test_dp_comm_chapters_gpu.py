@@ -26,7 +26,8 @@ def _run(tmp_path, chapter, dp_comm):
     r = subprocess.run(cmd, cwd=os.path.join(ROOT, chapter), env=env, capture_output=True, text=True, timeout=240)
     log = r.stdout + r.stderr
     assert r.returncode == 0, log[-3000:]
-    losses = [float(x) for x in re.findall(r"'running_loss': ([0-9.eE+-]+)", log)]
+    # rank 0's per-step losses (both ranks log, and their lines interleave in any order)
+    losses = [float(x) for x in re.findall(r"\[rank=0\][^\n]*'global_step': [1-9][0-9]*,[^\n]*'running_loss': ([0-9.eE+-]+)", log)]
     assert len(losses) >= 4, log[-3000:]
     return losses[:4], log
 
