@@ -123,6 +123,29 @@ __device__ __forceinline__ void tile_coords(int gc, int64_t n_row_tiles, int64_t
   ct = first + in % width;
 }
 
+// 8 x 8 transpose of 16-bit values held in registers: v[i] = row i on entry, column i on exit.
+// Three butterfly stages (elements, pairs, quads); only the first needs byte permutes, the other
+// two move whole dwords.
+__device__ __forceinline__ void transpose8x8(u16x8 (&v)[8]) {
+  u16x8 t[8], u[8];
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    t[i] = __builtin_shufflevector(v[i], v[i + 1], 0, 8, 2, 10, 4, 12, 6, 14);
+    t[i + 1] = __builtin_shufflevector(v[i], v[i + 1], 1, 9, 3, 11, 5, 13, 7, 15);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = (k & 1) + 4 * (k >> 1);  // 0, 1, 4, 5
+    u[i] = __builtin_shufflevector(t[i], t[i + 2], 0, 1, 8, 9, 4, 5, 12, 13);
+    u[i + 2] = __builtin_shufflevector(t[i], t[i + 2], 2, 3, 10, 11, 6, 7, 14, 15);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = __builtin_shufflevector(u[i], u[i + 4], 0, 1, 2, 3, 8, 9, 10, 11);
+    v[i + 4] = __builtin_shufflevector(u[i], u[i + 4], 4, 5, 6, 7, 12, 13, 14, 15);
+  }
+}
+
 constexpr int kDefaultTileGroup = 0;
 
 // Column-band width for tile_coords (DTG_TILE_GROUP, read per call; 0 = 2-D grid).

@@ -146,6 +146,58 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
   }
 }
 
+// Register-blocked form (DTG_SWIGLU_TILE=reg): no LDS.  Every lane owns an 8-token x 8-feature
+// block -- 16-B row loads of g, u and dh, f32 math, 16-B row stores of dg and du, then the three
+// transposed outputs through an in-register 8 x 8 transpose (transpose8x8) as 16-B column stores.
+// A wave's 64 lanes cover 64 tokens x 64 features (8 lanes per 128 contiguous bytes of every row
+// they load or store); 4 waves per workgroup cover 128 x 128.
+__global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(
+    const uint16_t* __restrict__ dh, const uint16_t* __restrict__ gu, int64_t gu_stride,
+    uint16_t* __restrict__ dgu, uint16_t* __restrict__ dguT, uint16_t* __restrict__ hT, int64_t T, int I, int gc) {
+  int64_t rt, ct;
+  tile_coords(gc, (T + 127) / 128, (I + 127) / 128, rt, ct);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t t0 = rt * 128 + (w >> 1) * 64 + (lane >> 3) * 8;  // first token of this lane's block
+  const int c0 = (int)ct * 128 + (w & 1) * 64 + (lane & 7) * 8;    // and first feature
+  if (t0 >= T || c0 >= I) return;  // T and I are multiples of 8: a block is wholly in or out
+  u16x8 vg[8], vu[8], vd[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint16_t* row = gu + (t0 + i) * gu_stride + c0;
+    vg[i] = *reinterpret_cast<const u16x8*>(row);
+    vu[i] = *reinterpret_cast<const u16x8*>(row + I);
+    vd[i] = *reinterpret_cast<const u16x8*>(dh + (t0 + i) * I + c0);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    u16x8 dg, du, h;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = bf2f(vg[i][j]), u = bf2f(vu[i][j]), d = bf2f(vd[i][j]);
+      const float sg = sigmoidf_(g);
+      const float silu = g * sg;
+      du[j] = f2bf(d * silu);
+      dg[j] = f2bf(d * u * sg * (1.f + g * (1.f - sg)));
+      h[j] = f2bf(silu * u);
+    }
+    uint16_t* o = dgu + (t0 + i) * 2 * I + c0;
+    *reinterpret_cast<u16x8*>(o) = dg;
+    *reinterpret_cast<u16x8*>(o + I) = du;
+    vg[i] = dg;  // the inputs of row i are dead: reuse their registers for the outputs
+    vu[i] = du;
+    vd[i] = h;
+  }
+  transpose8x8(vg);
+  transpose8x8(vu);
+  transpose8x8(vd);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    *reinterpret_cast<u16x8*>(dguT + (int64_t)(c0 + j) * T + t0) = vg[j];
+    *reinterpret_cast<u16x8*>(dguT + (int64_t)(I + c0 + j) * T + t0) = vu[j];
+    *reinterpret_cast<u16x8*>(hT + (int64_t)(c0 + j) * T + t0) = vd[j];
+  }
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& dh_, const at::Tensor& gu) {
   auto dh = dh_.contiguous();
   DTG_CHECK_CUDA_BF16(gu);
@@ -173,6 +225,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& dh
     else if (!std::strcmp(te, "128x128")) tt = 128, tf = 128;
   }
   const int gc = tile_group_env(kDefaultTileGroup);
+  if (te && !std::strcmp(te, "reg")) {
+    swiglu_bwd_t_reg_kernel<<<tile_grid(gc, (T + 127) / 128, (I + 127) / 128), 256, 0, stream()>>>(
+        bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu), bf16_mut(dguT), bf16_mut(hT), T, I, gc);
+    DTG_LAUNCH_CHECK();
+    return {dgu, dguT, hT};
+  }
   const dim3 grid = tile_grid(gc, (T + tt - 1) / tt, (I + tf - 1) / tf);
   const size_t lds = 3 * (size_t)tt * (tf + 2) * sizeof(uint16_t);
 #define DTG_SG_LAUNCH(TT_, TF_)                                                                            \

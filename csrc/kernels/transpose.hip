@@ -17,7 +17,7 @@
 namespace dtg {
 
 // Tiles are TR (input rows = tokens) x TC (input columns) with 256 threads; each side moves
-// 16-byte vectors along its contiguous dimension.  64 x 64 (default) and 128 x 128 tiles
+// 16-byte vectors along its contiguous dimension.  64 x 64 (DTG_TRANSPOSE_TILE=64) and 128 x 128 tiles
 // (DTG_TRANSPOSE_TILE=128: 256-B output row segments) measured equal on the full 8B step
 // (same-box A/B, profiles/r1_s36_*); the wide [T, 2I] case alone favours 128 by ~3 %.
 template <int TR, int TC>
@@ -58,6 +58,28 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __r
   }
 }
 
+// Register-blocked transpose (DTG_TRANSPOSE_TILE=reg): no LDS.  Every lane moves one 8 x 8 block
+// -- eight 16-B row loads, an in-register transpose, eight 16-B column stores -- and a wave's 64
+// lanes cover a 64 x 64 tile (4 waves: 128 x 128 per workgroup).  Eight lanes read 128
+// contiguous bytes of one input row per load instruction, and eight lanes write 128 contiguous
+// bytes of one output row per store instruction.
+__global__ __launch_bounds__(256) void transpose_bf16_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx,
+                                                                 uint16_t* __restrict__ out, int64_t R, int64_t C,
+                                                                 int gc) {
+  int64_t rt, ct;
+  tile_coords(gc, (R + 127) / 128, (C + 127) / 128, rt, ct);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r = rt * 128 + (w >> 1) * 64 + (lane >> 3) * 8;  // this lane's first input row
+  const int64_t c = ct * 128 + (w & 1) * 64 + (lane & 7) * 8;    // and first input column
+  if (r >= R || c >= C) return;  // R and C are multiples of 8: a block is wholly in or out
+  u16x8 v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const u16x8*>(x + (r + i) * ldx + c);
+  transpose8x8(v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) *reinterpret_cast<u16x8*>(out + (c + j) * R + r) = v[j];
+}
+
 at::Tensor transpose2d(const at::Tensor& x) {
   DTG_CHECK_CUDA_BF16(x);
   DTG_CHECK(x.dim() == 2 && x.stride(1) == 1, "transpose2d: x must be 2-D with unit column stride");
@@ -69,9 +91,15 @@ at::Tensor transpose2d(const at::Tensor& x) {
   auto out = at::empty({C, R}, x.options());
   if (R == 0 || C == 0) return out;
   const char* te = std::getenv("DTG_TRANSPOSE_TILE");  // per call: tests and A/B runs switch it in-process
-  const int tile = te ? std::atoi(te) : 64;
+  // default: the register-blocked kernel (+2 % on [T, 4096], +12 % on [T, 28672] against the
+  // 64 x 64 LDS tile, same-process A/B in profiles/r5/transpose/)
+  const bool reg = te == nullptr || te[0] == 'r';
+  const int tile = reg ? 0 : std::atoi(te);
   const int gc = tile_group_env(kDefaultTileGroup);
-  if (tile == 64) {
+  if (reg) {
+    const dim3 grid = tile_grid(gc, (R + 127) / 128, (C + 127) / 128);
+    transpose_bf16_reg_kernel<<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C, gc);
+  } else if (tile == 64) {
     const dim3 grid = tile_grid(gc, (R + 63) / 64, (C + 63) / 64);
     transpose_bf16_kernel<64, 64><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C, gc);
   } else {

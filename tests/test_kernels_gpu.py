@@ -82,7 +82,7 @@ def test_swiglu(cuda):
     _close(dops.swiglu_bwd(dh.to(cuda), gu.to(cuda)), dops.swiglu_bwd(dh, gu), 3e-2, 2e-2, "swiglu bwd")
 
 
-@pytest.mark.parametrize("tile", ["64", "128"])
+@pytest.mark.parametrize("tile", ["64", "128", "reg"])
 @pytest.mark.parametrize("group", ["0", "3", "16"])
 @pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (4096, 6144, 6144), (1000, 520, 528), (8, 8, 8), (136, 7000, 7000)])
 def test_transpose2d(cuda, R, C, ld, group, tile, monkeypatch):
@@ -121,7 +121,7 @@ def test_transpose_mats_batched(cuda):
 
 
 @pytest.mark.parametrize("group", ["0", "3", "16"])
-@pytest.mark.parametrize("tile", ["64x64", "64x128", "128x64", "128x128"])
+@pytest.mark.parametrize("tile", ["64x64", "64x128", "128x64", "128x128", "reg"])
 @pytest.mark.parametrize("T,I", [(64, 64), (4096, 1792), (520, 136)])
 def test_swiglu_bwd_t(cuda, T, I, tile, group, monkeypatch):
     monkeypatch.setenv("DTG_SWIGLU_TILE", tile)

@@ -59,11 +59,11 @@ def main():
     }
     # A/B pairs run twice in alternating order (A B A B) against clock drift
     for rep in (1, 2):
-        for tl in ("64x64", "64x128", "128x64", "128x128"):
+        for tl in ("64x64", "64x128", "128x64", "128x128", "reg"):
             cases[f"swiglu_bwd_t (dgu, dgu^T, h^T) tile {tl} #{rep}"] = (
                 lambda tl=tl: (os.environ.__setitem__("DTG_SWIGLU_TILE", tl), ops.swiglu_bwd_t(dh, gu)),
                 (3 + 5) * T * I * E)
-        for tt in ("64", "128"):
+        for tt in ("64", "128", "reg"):
             def tr(src, tt=tt):
                 os.environ["DTG_TRANSPOSE_TILE"] = tt
                 return ops.transpose2d(src)
