@@ -15,6 +15,8 @@
 
 #include "common.h"
 
+#include <cstring>
+
 namespace dtg {
 
 template <typename T>
@@ -366,6 +368,83 @@ __global__ __launch_bounds__(NT) void adamw_t_kernel(uint16_t* __restrict__ p, f
   }
 }
 
+// Register-blocked form (the default; DTG_ADAMT_KERNEL=lds selects the kernel above): no LDS, no barriers.  The same
+// 64 x TC tile walk (one tile per workgroup of TC threads, i.e. TC / 64 waves); every lane owns an
+// 8 x 8 block: eight 16-B row vectors of p, g, m, v in, the update in f32, p / m / v rows out,
+// and -- for a matrix with a transposed copy -- the updated block through an in-register 8 x 8
+// transpose (transpose8x8) to eight 16-B rows of W^T.  Eight lanes cover 128 contiguous bytes of
+// every row they load or store.  Matrices with a W^T have rows and columns that are multiples of
+// 8 (the engine's descriptor builder), so their blocks are whole; the W^T-less rows (norm
+// weights, odd vocabularies) may end mid-block and are bounds-checked per row.
+template <typename ST, bool MASTER, int TC>
+__global__ __launch_bounds__(TC) void adamw_t_reg_kernel(uint16_t* __restrict__ p, float* __restrict__ master,
+                                                         const uint16_t* __restrict__ g, ST* __restrict__ m,
+                                                         ST* __restrict__ v, uint16_t* __restrict__ pt,
+                                                         const MatDesc* __restrict__ mats, int nmats, AdamHyper h,
+                                                         const float* __restrict__ dev_hyper) {
+  if (dev_hyper != nullptr) {
+    h.lr = dev_hyper[0];
+    h.bc1 = dev_hyper[1];
+    h.bc2_sqrt = dev_hyper[2];
+  }
+  const float step_size = h.lr / h.bc1;
+  const float decay = 1.f - h.lr * h.wd;
+  const int64_t t = blockIdx.x;
+  int lo = 0, hi = nmats - 1;  // the matrix whose tiles include t
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (mats[mid].tile0 <= t) lo = mid; else hi = mid - 1;
+  }
+  const MatDesc md = mats[lo];
+  const int64_t lt = t - md.tile0;
+  const int64_t ntc = (md.cols + TC - 1) / TC;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r = (lt / ntc) * kAtRows + (lane >> 3) * 8;
+  const int64_t c = (lt % ntc) * TC + 64 * w + (lane & 7) * 8;
+  if (r >= md.rows || c >= md.cols) return;
+  const int nr = md.rows - r < 8 ? (int)(md.rows - r) : 8;  // 8 except at a W^T-less row end
+  using PT = typename std::conditional<MASTER, float, uint16_t>::type;
+  Raw8<PT> pr[8];
+  Raw8<uint16_t> gr[8];
+  Raw8<ST> mr[8], vr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < nr) {
+      const int64_t k = md.off + (r + i) * md.cols + c;
+      if constexpr (MASTER) pr[i].load(master + k); else pr[i].load(p + k);
+      gr[i].load(g + k);
+      mr[i].load(m + k);
+      vr[i].load(v + k);
+    }
+  }
+  u16x8 pb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < nr) {
+      const int64_t k = md.off + (r + i) * md.cols + c;
+      float pv[8], mv[8], vv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pv[j] = pr[i][j];
+        mv[j] = mr[i][j];
+        vv[j] = vr[i][j];
+        adam_elem(pv[j], gr[i][j] * h.grad_scale, mv[j], vv[j], h, step_size, decay);
+      }
+      st8<ST>(m + k, mv);
+      st8<ST>(v + k, vv);
+      if (MASTER) st8<float>(master + k, pv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[i][j] = f2bf(pv[j]);
+      *reinterpret_cast<u16x8*>(p + k) = pb[i];
+    }
+  }
+  if (md.toff >= 0) {  // whole 8 x 8 blocks (rows and columns are multiples of 8)
+    transpose8x8(pb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *reinterpret_cast<u16x8*>(pt + md.toff + (c + j) * md.rows + r) = pb[j];
+  }
+}
+
 void adamw_t_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g, const at::Tensor& m,
               const at::Tensor& v, const at::Tensor& pt, const at::Tensor& mats, int64_t ntiles, double lr,
               double beta1, double beta2, double eps, double wd, int64_t step, double grad_scale,
@@ -412,6 +491,31 @@ void adamw_t_(const at::Tensor& p, const c10::optional<at::Tensor>& master, cons
   uint16_t* ptp = bf16_mut(pt);
   const bool sb = m.scalar_type() == at::kBFloat16;
   DTG_CHECK(sb || m.scalar_type() == at::kFloat, "adamw_t_: states must be bf16 or f32");
+  // default: the register-blocked kernel (5.98 vs 5.54 TB/s over 8 Llama-3-8B layers against the
+  // LDS kernel at its best tile, profiles/r5/transpose/); DTG_ADAMT_KERNEL=lds selects the LDS one
+  const char* ke = std::getenv("DTG_ADAMT_KERNEL");  // per call: A/B runs switch it in-process
+  if (ke == nullptr || std::strcmp(ke, "lds") != 0) {
+    DTG_CHECK(ntiles < (int64_t(1) << 31), "adamw_t_: too many tiles");
+#define DTG_ADAMT_REG(ST, MASTER, TC)                                                                       \
+  adamw_t_reg_kernel<ST, MASTER, TC><<<(unsigned)ntiles, TC, 0, stream()>>>(                                \
+      bf16_mut(p), mp, gp, reinterpret_cast<ST*>(m.data_ptr()), reinterpret_cast<ST*>(v.data_ptr()), ptp, md, nm, \
+      h, hp)
+#define DTG_ADAMT_REG_TC(ST, MASTER)                                 \
+  do {                                                                \
+    if (tile_cols == 64) DTG_ADAMT_REG(ST, MASTER, 64);               \
+    else if (tile_cols == 128) DTG_ADAMT_REG(ST, MASTER, 128);        \
+    else DTG_ADAMT_REG(ST, MASTER, 256);                              \
+  } while (0)
+    if (has_master) {
+      if (sb) DTG_ADAMT_REG_TC(uint16_t, true); else DTG_ADAMT_REG_TC(float, true);
+    } else {
+      if (sb) DTG_ADAMT_REG_TC(uint16_t, false); else DTG_ADAMT_REG_TC(float, false);
+    }
+#undef DTG_ADAMT_REG_TC
+#undef DTG_ADAMT_REG
+    DTG_LAUNCH_CHECK();
+    return;
+  }
 #define DTG_ADAMT_LAUNCH(ST, MASTER, TC, NT)                                                              \
   adamw_t_kernel<ST, MASTER, TC, NT><<<(int)std::min<int64_t>(ntiles, 256 * 32 * 256 / NT), NT, 0, stream()>>>( \
       bf16_mut(p), mp, gp, reinterpret_cast<ST*>(m.data_ptr()), reinterpret_cast<ST*>(v.data_ptr()), ptp, md, nm, \

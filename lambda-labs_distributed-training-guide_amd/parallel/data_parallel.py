@@ -156,8 +156,9 @@ class DataParallel:
         import math
 
         sp = self.space
-        # adamw_t_ tile width (64 x TC tiles; DTG_ADAMT_TC = 64 | 128 | 256; 128 measured fastest, profiles/r3/s07)
-        self._wt_tc = int(os.environ.get("DTG_ADAMT_TC", "128"))
+        # adamw_t_ tile width (64 x TC tiles; DTG_ADAMT_TC = 64 | 128 | 256).  256: the register-
+        # blocked kernel's fastest walk (profiles/r5/transpose/; the LDS kernel's was 128, r3/s07)
+        self._wt_tc = int(os.environ.get("DTG_ADAMT_TC", "256"))
         rows_desc, slots, toff, tile0 = [], {}, 0, 0
         for i in range(len(sp.names)):
             shape, off = sp.shapes[i], sp.offsets[i]

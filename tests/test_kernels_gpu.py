@@ -244,14 +244,16 @@ def test_adamw(cuda, state_dtype, master, n):
         assert (tp.detach().float() - pm.float()).abs().max().item() <= 2 * 2**-7 * tp.detach().float().abs().max().item()
 
 
+@pytest.mark.parametrize("kernel", ["lds", "reg"])
 @pytest.mark.parametrize("tile_cols", [64, 128, 256])
 @pytest.mark.parametrize("state_dtype,master", [(torch.bfloat16, False), (torch.float32, True)])
-def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master, tile_cols):
-    """adamw_t_ (update + W^T of every listed matrix, 64 x 64 LDS tiles, edge tiles, [1, n]
-    rows without a copy) == adamw_ on the same elements, bitwise; copies == W^T exactly;
-    elements outside the listed matrices untouched."""
+def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master, tile_cols, kernel, monkeypatch):
+    """adamw_t_ (update + W^T of every listed matrix; LDS tiles or register-blocked 8 x 8 blocks;
+    edge tiles, [1, n] rows and a 13-row matrix without a copy) == adamw_ on the same elements,
+    bitwise; copies == W^T exactly; elements outside the listed matrices untouched."""
+    monkeypatch.setenv("DTG_ADAMT_KERNEL", kernel)
     torch.manual_seed(0)
-    shapes = [(192, 320), (1, 136), (72, 200), (1024, 64)]  # 72 x 200: partial edge tiles
+    shapes = [(192, 320), (1, 136), (72, 200), (1024, 64), (13, 128)]  # 72 x 200: partial edge tiles
     offs, o = [], 0
     for r, c in shapes:
         offs.append(o)
@@ -265,10 +267,10 @@ def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master, tile_co
     ref = [t.clone() if t is not None else None for t in (p, g, m, v, mw)]
     desc, toff, tile0 = [], 0, 0
     for (r, c), off in zip(shapes, offs):
-        t = toff if r > 1 else -1
+        t = toff if r > 1 and r % 8 == 0 else -1  # W^T copies only for whole 8-row blocks
         desc.append([off, r, c, t, tile0])
         tile0 += -(-r // 64) * -(-c // tile_cols)
-        if r > 1:
+        if t >= 0:
             toff += r * c
     pt = torch.zeros(toff, dtype=torch.bfloat16, device=cuda)
     mats = torch.tensor(desc, dtype=torch.long, device=cuda)

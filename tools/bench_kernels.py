@@ -89,8 +89,13 @@ def main():
         pw, gw = torch.randn(nt, **bf), torch.randn(nt, **bf)
         mw, vw, ptw = torch.zeros(nt, **bf), torch.zeros(nt, **bf), torch.empty(nt, **bf)
         mats = torch.tensor(desc, dtype=torch.long, device=dev)
-        runs = {f"adamw_t_ 64x{tc} (+W^T)": (lambda: ops.adamw_t_(pw, None, gw, mw, vw, ptw, mats, tile0, 1e-4, 0.9,
-                                                               0.999, 1e-8, 0.01, 3, 1.0, None, tc), 16 * nt)}
+        def at_(kern, tc=tc, mats=mats, tile0=tile0):
+            os.environ["DTG_ADAMT_KERNEL"] = kern
+            ops.adamw_t_(pw, None, gw, mw, vw, ptw, mats, tile0, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0, None, tc)
+        runs = {}
+        for rep in (1, 2):  # A B A B against clock drift
+            runs[f"adamw_t_ 64x{tc} (+W^T) lds #{rep}"] = (lambda: at_("lds"), 16 * nt)
+            runs[f"adamw_t_ 64x{tc} (+W^T) reg #{rep}"] = (lambda: at_("reg"), 16 * nt)
         if tc == 64:
             for un, wg in ((2, 16), (4, 16), (2, 8), (4, 8), (2, 32), (4, 4)):
                 def lin(un=un, wg=wg):
@@ -100,7 +105,7 @@ def main():
         if tc == 128:  # the tile walk with no transposed copies (toff = -1): layout effect alone
             mats_nt = mats.clone()
             mats_nt[:, 3] = -1
-            runs["adamw_t_ 64x128 tile walk, no W^T"] = (lambda: ops.adamw_t_(
+            runs["adamw_t_ 64x128 tile walk, no W^T"] = (lambda: os.environ.__setitem__("DTG_ADAMT_KERNEL", "lds") or ops.adamw_t_(
                 pw, None, gw, mw, vw, ptw, mats_nt, tile0, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0, None, tc), 14 * nt)
         for name, (fn, nbytes) in runs.items():
             if a.only and not any(o in name for o in a.only.split(',')):
