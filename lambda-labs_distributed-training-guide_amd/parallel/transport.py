@@ -14,7 +14,8 @@ job's own group at the job's own message sizes, at startup, instead of being a h
 Each candidate runs its collectives `warmup` + `iters` times; the time of the SLOWEST rank is the
 candidate's time (MAX all-reduce), so every rank picks the same winner.  A candidate is also
 checked against RCCL's result on integer-valued data (sums exact in any order): one that raises
-or disagrees is recorded with its error and never picked.  RCCL comes first and wins ties.
+or disagrees is recorded with its error and never picked.  RCCL comes first and wins ties; an
+alternative must be at least 10 % faster than RCCL to be picked (`MARGIN`).
 The table ({name: {"us": .., "error": ..}}) is logged by the trainer and recorded by the bench
 (`tp_comm_calibration` / `dp_comm_calibration`).
 
@@ -100,13 +101,24 @@ def measure(builders: Dict[str, Callable[[], Candidate]], group, device, warmup:
     return table
 
 
-def pick(table: Dict[str, dict], default: str = "rccl") -> str:
-    """Fastest candidate with a time; ties go to the earlier one (RCCL first)."""
+# An alternative to RCCL must be this much faster to be picked (DTG_TRANSPORT_MARGIN).  RCCL is the
+# transport with cross-device mileage; the direct-peer paths are verified against it at startup
+# but have run only with every rank on one GPU so far, so a near-tie stays with RCCL.
+MARGIN = float(os.environ.get("DTG_TRANSPORT_MARGIN", "0.10"))
+
+
+def pick(table: Dict[str, dict], default: str = "rccl", margin: float = None) -> str:
+    """Fastest candidate with a time; ties go to the earlier one (RCCL first), and a candidate
+    other than `default` must beat the default's time by `margin` (a fraction)."""
+    margin = MARGIN if margin is None else margin
     best, best_us = default, math.inf
     for name, row in table.items():
         us = row.get("us")
         if us is not None and us < best_us:
             best, best_us = name, us
+    d_us = table.get(default, {}).get("us")
+    if best != default and d_us is not None and best_us > d_us * (1.0 - margin):
+        return default
     return best
 
 

@@ -1,6 +1,6 @@
 """Transport selection by measurement (`--tp-comm auto` / `--dp-comm auto`, parallel/transport.py)
 on gloo ranks with stubbed timings: the slowest rank's time decides, every rank picks the same
-transport, a candidate that fails on any rank is never picked, RCCL wins ties."""
+transport, a candidate that fails on any rank is never picked, RCCL wins ties and near-ties (margin)."""
 import math
 
 import pytest
@@ -45,6 +45,10 @@ def test_pick_prefers_rccl_on_ties_and_without_data():
     assert pick({"rccl": {"us": 10.0}, "xgmi-dma": {"us": 10.0}}) == "rccl"
     assert pick({"rccl": {"us": None}, "xgmi-dma": {"us": None}}) == "rccl"
     assert pick({"rccl": {"us": 12.0}, "xgmi-dma": {"us": 9.0}}) == "xgmi-dma"
+    # an alternative within the margin of RCCL (10 % by default) does not displace it
+    assert pick({"rccl": {"us": 10.0}, "xgmi-dma": {"us": 9.5}}) == "rccl"
+    assert pick({"rccl": {"us": 10.0}, "xgmi-dma": {"us": 9.5}}, margin=0.0) == "xgmi-dma"
+    assert pick({"rccl": {"us": None}, "xgmi-dma": {"us": 9.5}}) == "xgmi-dma"
 
 
 def _cpu_auto(rank, world):
