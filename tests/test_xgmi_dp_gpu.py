@@ -133,23 +133,29 @@ def _fsdp_train(rank, world, dp_comm, resident=False):
     return {k: v.float().cpu() for k, v in sd.items()}, losses
 
 
-def _fsdp_twice(rank, world, dp_comm, resident):
-    a = _fsdp_train(rank, world, dp_comm, resident)
+def _fsdp_layouts(rank, world, dp_comm):
+    """Both offload layouts in one spawn: the non-resident one twice (reproducibility), the
+    resident one once."""
+    a = _fsdp_train(rank, world, dp_comm, False)
     torch.cuda.empty_cache()
-    return a, _fsdp_train(rank, world, dp_comm, resident)
+    b = _fsdp_train(rank, world, dp_comm, False)
+    torch.cuda.empty_cache()
+    return a, b, _fsdp_train(rank, world, dp_comm, True)
 
 
-@pytest.mark.parametrize("world,resident", [(4, False), (4, True)])  # 8 ranks: the ZeRO test
-def test_fsdp_xgmi_dma_matches_single_and_is_reproducible(cuda, world, resident):
-    """FSDP unit all-gathers / gradient reduce-scatters as copy-engine pulls (shared shard buffers
-    and gradient pool; the resident-offload layout gathers from the HBM shard copy): matches the
-    single-process run, identical on every rank, bitwise reproducible (two runs in one spawn)."""
+def test_fsdp_xgmi_dma_matches_single_and_is_reproducible(cuda):
+    """FSDP unit all-gathers / gradient reduce-scatters as copy-engine pulls at 4 ranks (shared
+    shard buffers and gradient pool; the resident-offload layout gathers from the HBM shard copy):
+    both layouts match the single-process run on every rank, and the non-resident one is bitwise
+    reproducible (two runs in one spawn; 8 ranks: the ZeRO test)."""
+    world = 4
     ref, _ = _fsdp_train(0, 1, "rccl")
-    res = run_distributed(_fsdp_twice, world, "xgmi-dma", resident)
+    res = run_distributed(_fsdp_layouts, world, "xgmi-dma")
     for r in range(world):
-        a, b = res[r]
+        a, b, c = res[r]
         for n, v in ref.items():
-            rel = ((a[0][n] - v).norm() / v.norm().clamp_min(1e-12)).item()
-            assert rel < 3e-2, (world, r, n, rel)
+            for layout, got in (("host", a), ("resident", c)):
+                rel = ((got[0][n] - v).norm() / v.norm().clamp_min(1e-12)).item()
+                assert rel < 3e-2, (layout, r, n, rel)
             assert torch.equal(a[0][n], b[0][n]), (r, n)
         assert a[1] == b[1]
