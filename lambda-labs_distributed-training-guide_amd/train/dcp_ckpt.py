@@ -234,10 +234,17 @@ def _planners():
 
 
 def _adamw_group(optimizer):
+    """torch AdamW's full param_group (without "params"): the hyper-parameters of this run, plus
+    every extra plain-valued key the optimizer carries (e.g. the scheduler's `initial_lr`, which
+    the reference's `get_state_dict` also asks for on resume)."""
     g = optimizer.param_groups[0] if optimizer is not None else {}
-    return {"lr": float(g.get("lr", 0.0)), "betas": tuple(g.get("betas", (0.9, 0.999))), "eps": float(g.get("eps", 1e-8)),
-            "weight_decay": float(g.get("weight_decay", 0.01)), "amsgrad": False, "foreach": None, "maximize": False,
-            "capturable": False, "differentiable": False, "fused": True, "decoupled_weight_decay": True}
+    out = {"lr": float(g.get("lr", 0.0)), "betas": tuple(g.get("betas", (0.9, 0.999))), "eps": float(g.get("eps", 1e-8)),
+           "weight_decay": float(g.get("weight_decay", 0.01)), "amsgrad": False, "foreach": None, "maximize": False,
+           "capturable": False, "differentiable": False, "fused": True, "decoupled_weight_decay": True}
+    for k, v in g.items():
+        if k not in out and k != "params" and isinstance(v, (bool, int, float, str, tuple, type(None))):
+            out[k] = v
+    return out
 
 
 def save_dcp(ckpt_dir, engine, optimizer, cfg, global_step=None):
@@ -262,6 +269,11 @@ def save_dcp(ckpt_dir, engine, optimizer, cfg, global_step=None):
         for hf, hshape, offs, sizes, views in _chunks(engine, cfg, keep):
             if hf == "lm_head.weight" and tied:
                 continue
+            if hf == "model.embed_tokens.weight" and tied:
+                # an HF model with tied embeddings still lists `lm_head.weight` in its state dict
+                # (not in its optimizer state): the reference's resume asks for that key
+                tensors.append(("model.lm_head.weight", hshape, offs, views["p"]))
+                mappings["model.lm_head.weight"] = ("model", "lm_head.weight")
             fqns.add(hf)
             for key, path, t in ((f"model.{hf}", ("model", hf), views["p"]),
                                  (f"optimizer.state.{hf}.exp_avg", ("optimizer", "state", hf, "exp_avg"), views["m"]),
@@ -282,8 +294,13 @@ def save_dcp(ckpt_dir, engine, optimizer, cfg, global_step=None):
     if rank0:
         names = sorted(set().union(*[set(x) for x in all_fqns]))
         group = dict(_adamw_group(optimizer), params=names)
-        objects["optimizer.param_groups"] = [group]
-        mappings["optimizer.param_groups"] = ("optimizer", "param_groups")
+        # one BYTE_IO item per field, under the keys torch's flatten_state_dict gives a one-group
+        # AdamW state dict (`optimizer.param_groups.0.lr`, ...), so a stock `dcp.load` of
+        # get_state_dict()'s optimizer state finds every key
+        for k, v in group.items():
+            key = f"optimizer.param_groups.0.{k}"
+            objects[key] = v
+            mappings[key] = ("optimizer", "param_groups", 0, k)
     writer = FileSystemWriter(str(ckpt_dir), single_file_per_rank=True, sync_files=True)
     dcp.save({}, storage_writer=writer, planner=SavePlanner(tensors, objects, mappings), no_dist=not multi)
     if rank0:

@@ -109,8 +109,9 @@ def test_dcp_2d_checkpoint_is_torch_readable_and_resumes_bit_exact(tmp_path):
     assert model_sd["model.layers.0.self_attn.k_proj.weight"].shape == (nkv * d_, cfg.hidden_size)
     assert model_sd["model.layers.0.mlp.gate_proj.weight"].shape == (cfg.intermediate_size, cfg.hidden_size)
     assert model_sd["model.norm.weight"].shape == (cfg.hidden_size,)
-    if cfg.tie_word_embeddings:  # the reference's tied models keep only the embedding
-        assert "lm_head.weight" not in model_sd
+    if cfg.tie_word_embeddings:  # an HF tied model's state dict lists both names; only one has AdamW state
+        assert torch.equal(model_sd["lm_head.weight"], model_sd["model.embed_tokens.weight"])
+        assert "lm_head.weight" not in opt_sd["state"]
     else:
         assert model_sd["lm_head.weight"].shape == (cfg.vocab_size, cfg.hidden_size)
     assert all(torch.isfinite(v).all() for v in model_sd.values())
@@ -118,7 +119,7 @@ def test_dcp_2d_checkpoint_is_torch_readable_and_resumes_bit_exact(tmp_path):
     assert set(st) == {"exp_avg", "exp_avg_sq", "step"} and float(st["step"]) == 2.0
     (pg,) = opt_sd["param_groups"]
     assert pg["lr"] == pytest.approx(1e-2) and tuple(pg["betas"]) == (0.9, 0.999) and pg["eps"] == pytest.approx(1e-3)
-    assert set(pg["params"]) == set(model_sd)
+    assert set(pg["params"]) == set(model_sd) - ({"lm_head.weight"} if cfg.tie_word_embeddings else set())
     shapes = {k: tuple(v.shape) for k, v in model_sd.items()}
     # resume on other layouts: every loaded element equals the stored one
     for world, tp, kind in ((1, 1, "fsdp"), (2, 1, "fsdp"), (2, 2, "fsdp"), (2, 1, "zero")):
@@ -129,9 +130,13 @@ def test_dcp_2d_checkpoint_is_torch_readable_and_resumes_bit_exact(tmp_path):
         assert all(x[1] == 2 for x in dumps) and dumps[0][2]["global_step"] == 2
         got = _assemble([x[0] for x in dumps], "p", shapes)
         m = _assemble([x[0] for x in dumps], "m", shapes)
+        v2 = _assemble([x[0] for x in dumps], "v", shapes)
         for k, v in model_sd.items():
+            if k not in opt_sd["state"]:  # the tied head
+                continue
             assert torch.equal(got[k], v), (world, tp, kind, k)
             assert torch.equal(m[k], st_k := opt_sd["state"][k]["exp_avg"]), (world, tp, kind, k, st_k.shape)
+            assert torch.equal(v2[k], opt_sd["state"][k]["exp_avg_sq"]), (world, tp, kind, k)
 
 
 def _dtg_roundtrip(rank, world, d):
