@@ -50,23 +50,45 @@ def _device_sync(device):
         torch.cuda.synchronize(device)
 
 
+def _all_ok(ok: bool, group, dev) -> bool:
+    """Every rank's flag, AND-reduced (a collective every rank issues whatever happened locally)."""
+    t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64,
+                     device=dev if (dev.type == "cuda" and dist.get_backend(group) == "nccl") else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item() > 0.5)
+
+
 def time_candidate(c: Candidate, group, device, warmup: int = 2, iters: int = 5) -> float:
-    """Seconds per iteration on this rank (group-synchronised start, device-synchronised end)."""
-    for _ in range(warmup):
-        c.run()
-    _device_sync(device)
-    dist.barrier(group=group)
+    """Seconds per iteration on this rank (group-synchronised start, device-synchronised end).
+    The start is an AND-reduce of "my warmup worked", issued by every rank even when its warmup
+    raised, so a rank-local failure cannot leave its peers waiting in a collective."""
+    dev = torch.device(device)
+    err = None
+    try:
+        for _ in range(warmup):
+            c.run()
+        _device_sync(dev)
+    except Exception as e:  # noqa: BLE001 - re-raised after the group agreed
+        err = e
+    if not _all_ok(err is None, group, dev):
+        raise err if err is not None else RuntimeError("warmup failed on another rank")
     t0 = time.perf_counter()
     for _ in range(iters):
         c.run()
-    _device_sync(device)
+    _device_sync(dev)
     return (time.perf_counter() - t0) / iters
 
 
 def measure(builders: Dict[str, Callable[[], Candidate]], group, device, warmup: int = 2, iters: int = 5,
             time_fn: Optional[Callable[[Candidate], float]] = None) -> Dict[str, dict]:
     """{name: {"us": slowest-rank microseconds or None, "error": str?}} in `builders` order.
-    `time_fn(candidate) -> seconds` replaces the timing (tests stub it)."""
+    `time_fn(candidate) -> seconds` replaces the timing (tests stub it).
+
+    Every rank issues the same collectives whatever fails locally: after build() an AND-reduce
+    decides whether anyone times the candidate (a rank whose build raised still joins it), the
+    timing starts with another AND-reduce (time_candidate), and a MAX-reduce of the time ends it.
+    (A build() that raises BEFORE its own internal exchange, on some ranks only, is the one case
+    this cannot cover -- which is why the trainer calibrates in a child job, `resolve_isolated`.)"""
     table: Dict[str, dict] = {}
     dev = torch.device(device) if device is not None else torch.device("cpu")
     for name, build in builders.items():
@@ -75,18 +97,22 @@ def measure(builders: Dict[str, Callable[[], Candidate]], group, device, warmup:
         cand = None
         try:
             cand = build()
-            secs = time_fn(cand) if time_fn is not None else time_candidate(cand, group, dev, warmup, iters)
-            if cand.verify is not None and not cand.verify():
-                err, secs = "result differs from RCCL's", math.inf
         except Exception as e:  # noqa: BLE001 - recorded in the table, the candidate is not picked
-            err, secs = repr(e)[:300], math.inf
-        finally:
-            if cand is not None and cand.close is not None:
-                try:
-                    cand.close()
-                except Exception as e:  # noqa: BLE001
-                    err = err or f"close: {e!r}"[:300]
-                    secs = math.inf
+            err = repr(e)[:300]
+        built = _all_ok(err is None, group, dev)
+        if built:
+            try:
+                secs = time_fn(cand) if time_fn is not None else time_candidate(cand, group, dev, warmup, iters)
+                if cand.verify is not None and not cand.verify():
+                    err, secs = "result differs from RCCL's", math.inf
+            except Exception as e:  # noqa: BLE001
+                err, secs = repr(e)[:300], math.inf
+        if cand is not None and cand.close is not None:
+            try:
+                cand.close()
+            except Exception as e:  # noqa: BLE001
+                err = err or f"close: {e!r}"[:300]
+                secs = math.inf
         # the slowest rank bounds the job; a failure anywhere (inf) rules the candidate out everywhere
         t = torch.tensor([secs if math.isfinite(secs) else 1e30], dtype=torch.float64,
                          device=dev if (dev.type == "cuda" and dist.get_backend(group) == "nccl") else "cpu")
@@ -283,11 +309,157 @@ def resolve(flag: str, kind: str, group, device, msg_bytes: int, timeout_s: floa
     if flag != "auto":
         return flag, None
     choice, table = select(kind, group, device, msg_bytes, timeout_s)
-    if log is not None and table:
-        log(f"{kind} transport calibration at {msg_bytes / 2**20:.1f} MiB: "
-            + ", ".join(f"{k} {v['us']} us" + (f" ({v['error']})" if "error" in v else "") for k, v in table.items())
-            + f" -> {choice}")
+    _log_table(log, kind, msg_bytes, table, choice)
     return choice, table
+
+
+# ------------------------------------------------------------------------------------------
+# calibration in a child job (the trainer's `auto`)
+# ------------------------------------------------------------------------------------------
+CHILD_TIMEOUT = float(os.environ.get("DTG_TRANSPORT_CHILD_TIMEOUT", "180"))
+_CHILD_SCRIPT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_transport_child.py")
+
+
+def _log_table(log, kind, msg_bytes, table, choice):
+    if log is None or not table:
+        return
+    rows = []
+    for k, v in table.items():
+        s = f"{k} {v.get('us')} us"
+        if v.get("error"):
+            s += f" ({v['error']})"
+        elif v.get("note"):
+            s += f" ({v['note']})"
+        rows.append(s)
+    log(f"{kind} transport calibration at {msg_bytes / 2**20:.1f} MiB: " + ", ".join(rows) + f" -> {choice}")
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def child_command(world: int, spec: dict) -> list:
+    """`torchrun --nproc-per-node world _transport_child.py <spec>` on this node's GPUs."""
+    import json
+    import sys
+
+    stub = os.environ.get("DTG_TRANSPORT_CHILD_CMD")
+    if stub:  # tests: a JSON argv that stands in for the child job
+        return list(json.loads(stub))
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", _CHILD_SCRIPT, json.dumps(spec)]
+
+
+def run_child(world: int, spec: dict, timeout: float) -> dict:
+    """Run the calibration child job (own session, killed whole on timeout) -> its JSON record
+    {"choice", "table"} or {"error", "stderr_tail"}."""
+    import json
+    import signal
+    import subprocess
+
+    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+            "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+    try:
+        pr = subprocess.Popen(child_command(world, spec), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=env, start_new_session=True)
+    except Exception as e:  # noqa: BLE001
+        return {"error": f"calibration child did not start: {e!r}"[:300]}
+    try:
+        out, err = pr.communicate(timeout=max(1.0, timeout))
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(pr.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        out, err = pr.communicate()
+        return {"error": f"calibration child timed out ({timeout:.0f} s)", "stderr_tail": (err or "")[-400:]}
+    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+    if pr.returncode != 0 or not lines:
+        return {"error": f"calibration child exited {pr.returncode}", "stderr_tail": (err or "")[-400:]}
+    try:
+        rec = json.loads(lines[-1])
+    except ValueError as e:
+        return {"error": f"calibration child printed no JSON record: {e}"}
+    if rec.get("choice") not in CANDIDATES[spec["kind"]]:
+        return {"error": f"calibration child picked {rec.get('choice')!r}"}
+    return rec
+
+
+def resolve_isolated(flag: str, kind: str, device, msg_bytes: int, mesh=(1, 0), timeout_s: float = None,
+                     log=None, child_timeout: float = None) -> tuple:
+    """`--tp-comm` / `--dp-comm` for the trainer: like `resolve`, but the measurement (and with it
+    the xGMI library's first cross-device IPC contact) runs in a CHILD job on the same GPUs --
+    `torchrun --nproc-per-node W parallel/_transport_child.py` started by rank 0 -- so a peer
+    mapping that faults, or a collective that hangs, ends the child, never the training processes.
+    Rank 0 broadcasts the child's pick; on any child failure or timeout every rank takes RCCL and
+    the error is logged and returned in the table.  `mesh` = (k, axis) names the child's group:
+    `make_mesh(k)[axis]` (k = 1: the whole world).  Collective over the default group.
+
+    Off the GPU, on a non-RCCL group (gloo rehearsals) and on multi-node jobs (the child can only
+    start this node's ranks) the process group's own collectives are used without measuring."""
+    if flag != "auto":
+        return flag, None
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return "rccl", {}
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    world = dist.get_world_size()
+    forced = bool(os.environ.get("DTG_TRANSPORT_CHILD_CMD"))
+    if not forced:
+        note = None
+        if dev.type != "cuda":
+            note = "CPU: the process group's backend is the only transport"
+        elif dist.get_backend() != "nccl" and os.environ.get("DTG_TRANSPORT_CALIBRATE") != "1":
+            note = "non-RCCL process group: not calibrated (DTG_TRANSPORT_CALIBRATE=1 forces it)"
+        elif int(os.environ.get("LOCAL_WORLD_SIZE", world)) != world:
+            note = "multi-node job: the calibration child only reaches this node's GPUs"
+        if note is not None:
+            table = {"rccl": {"us": None, "note": note}}
+            _log_table(log, kind, msg_bytes, table, "rccl")
+            return "rccl", table
+    spec = {"kind": kind, "msg_bytes": int(msg_bytes), "mesh": [int(mesh[0]), int(mesh[1])],
+            "timeout_s": timeout_s}
+    box = [None]
+    if dist.get_rank() == 0:
+        box[0] = run_child(world, spec, CHILD_TIMEOUT if child_timeout is None else child_timeout)
+    dist.broadcast_object_list(box, src=0)
+    rec = box[0] or {"error": "no record"}
+    if "error" in rec:
+        table = {"rccl": {"us": None, "note": "fallback: calibration child failed"},
+                 "child": {"us": None, "error": rec["error"] + (f" | {rec['stderr_tail'][-200:]}"
+                                                                if rec.get("stderr_tail") else "")}}
+        _log_table(log, kind, msg_bytes, table, "rccl")
+        return "rccl", table
+    _log_table(log, kind, msg_bytes, rec["table"], rec["choice"])
+    return rec["choice"], rec["table"]
+
+
+def child_main(argv) -> int:
+    """The calibration child job: one rank per GPU, `select(kind)` on the requested group, rank 0
+    prints {"choice", "table"}."""
+    import json
+
+    from ..utils.dist import init_distributed
+
+    spec = json.loads(argv[0])
+    # the trainer's own bootstrap: one GPU per rank over RCCL (or the DTG_SHARED_DEVICE rehearsal)
+    _, _, _, dev = init_distributed()
+    k, axis = spec["mesh"]
+    group = None
+    if k > 1:
+        from .tensor_parallel import make_mesh
+
+        group = make_mesh(k)[axis]
+    choice, table = select(spec["kind"], group, dev, spec["msg_bytes"], spec.get("timeout_s"))
+    if dist.get_rank() == 0:
+        print(json.dumps({"choice": choice, "table": table}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
 
 
 def tp_message_bytes(batch: int, seq: int, hidden: int, esz: int = 2) -> int:
@@ -295,5 +467,5 @@ def tp_message_bytes(batch: int, seq: int, hidden: int, esz: int = 2) -> int:
     return int(batch) * int(seq) * int(hidden) * esz
 
 
-__all__: List[str] = ["Candidate", "measure", "pick", "select", "resolve", "tp_builders", "dp_builders",
-                      "tp_message_bytes", "CANDIDATES"]
+__all__: List[str] = ["Candidate", "measure", "pick", "select", "resolve", "resolve_isolated", "tp_builders",
+                      "dp_builders", "tp_message_bytes", "CANDIDATES"]

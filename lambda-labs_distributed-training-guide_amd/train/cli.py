@@ -58,12 +58,14 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     if chapter == "07":
         p.add_argument("--tp", default=8, type=int)
     if chapter in ("06", "07"):
-        p.add_argument("--tp-comm", default="auto", choices=["auto", "rccl", "xgmi", "xgmi-dma"],
+        p.add_argument("--tp-comm", default="rccl", choices=["auto", "rccl", "xgmi", "xgmi-dma"],
                        help="TP/SP all-gather / reduce-scatter / all-reduce: RCCL, or the direct-peer xGMI "
                             "library (csrc/comm/xgmi.hip; one node per TP group); xgmi-dma moves the "
                             "all-gathers and reduce-scatters on the copy engines, one stream per peer (no CU "
                             "time under the overlapped GEMMs); auto = whichever of the three is fastest at this "
-                            "job's message size on the TP group, timed at startup (parallel/transport.py)")
+                            "job's message size on the TP group, timed at startup in a child job on the same GPUs "
+                            "(parallel/transport.py; RCCL if the child fails).  Default rccl: the direct-peer "
+                            "paths have not yet been validated across devices")
         p.add_argument("--tp-comm-mb", default=256, type=int, help="xGMI workspace per rank (largest TP message)")
         p.add_argument("--tp-comm-timeout", default=None, type=float,
                        help="seconds an xGMI barrier waits for a peer before the collective fails (default: "
@@ -107,10 +109,11 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                         "parameters after every update (param) or both (on); each check syncs the device")
     g.add_argument("--bucket-mb", default=256, type=int, help="gradient bucket size for DDP/ZeRO")
     if chapter in ("02", "04", "05", "07"):
-        g.add_argument("--dp-comm", default="auto", choices=["auto", "rccl", "xgmi-dma"],
+        g.add_argument("--dp-comm", default="rccl", choices=["auto", "rccl", "xgmi-dma"],
                        help="ZeRO / FSDP collectives: RCCL, or copy-engine pulls between the ranks' shared shard / "
                             "gradient buffers over xGMI (one node; no CU time under the overlapped compute); "
-                            "auto = the faster of the two at this job's bucket / layer size, timed at startup")
+                            "auto = the faster of the two at this job's bucket / layer size, timed at startup in a "
+                            "child job (RCCL if the child fails).  Default rccl, as for --tp-comm")
     if chapter == "02":
         g.add_argument("--dp-mode", default="zero", choices=["ddp", "zero"],
                        help="zero: sharded optimizer (reference's ZeroRedundancyOptimizer); ddp: replicated")

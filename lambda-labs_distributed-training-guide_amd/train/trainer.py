@@ -142,7 +142,9 @@ def _resolve_dp_comm(args, chapter, cfg, device, dp_group, world, fsdp, pp, nseq
     job's message size (ZeRO: one gradient bucket; FSDP: one decoder layer's flat parameters).
     Only ZeRO and FSDP have a copy-engine path; everything else is RCCL without measuring."""
     zero = chapter == "02" and getattr(args, "dp_mode", "zero") == "zero" and pp == 1 and nseq == 1
-    if device.type != "cuda" or world == 1 or not (zero or fsdp) or getattr(args, "cpu_offload", "off") == "on":
+    forced = bool(os.environ.get("DTG_TRANSPORT_CHILD_CMD"))  # tests: the child path on CPU
+    if (device.type != "cuda" and not forced) or world == 1 or not (zero or fsdp) or \
+            getattr(args, "cpu_offload", "off") == "on":
         return "rccl"
     from ..parallel import transport
 
@@ -152,7 +154,13 @@ def _resolve_dp_comm(args, chapter, cfg, device, dp_group, world, fsdp, pp, nseq
         tp = max(1, getattr(args, "tp", 1)) if chapter == "07" else 1
         emb = cfg.vocab_size * cfg.hidden_size * (1 if getattr(cfg, "tie_word_embeddings", False) else 2)
         msg = 2 * ((cfg.num_params() - emb) // max(1, cfg.num_hidden_layers)) // tp
-    choice, args.dp_comm_calibration = transport.resolve("auto", "dp", dp_group, device, msg, log=LOGGER.info)
+    if chapter == "07":
+        mesh = (max(1, getattr(args, "tp", 1)), 0)
+    elif getattr(args, "sharding", "full") == "hybrid":
+        mesh = (args.shard_size or int(os.environ.get("LOCAL_WORLD_SIZE", torch.cuda.device_count() or 1)), 1)
+    else:
+        mesh = (1, 0)
+    choice, args.dp_comm_calibration = transport.resolve_isolated("auto", "dp", device, msg, mesh=mesh, log=LOGGER.info)
     return choice
 
 
@@ -176,8 +184,9 @@ def _build(args, chapter, device, world):
 
             chunks = max(1, getattr(args, "tp_overlap_chunks", 2))
             msg = transport.tp_message_bytes(args.batch_size, args.seq_length, cfg.hidden_size) // chunks
-            args.tp_comm, args.tp_comm_calibration = transport.resolve(
-                "auto", "tp", tp_group, device, msg, xgmi_timeout(getattr(args, "tp_comm_timeout", None)), LOGGER.info)
+            args.tp_comm, args.tp_comm_calibration = transport.resolve_isolated(
+                "auto", "tp", device, msg, mesh=(tp, 1), timeout_s=xgmi_timeout(getattr(args, "tp_comm_timeout", None)),
+                log=LOGGER.info)
         if getattr(args, "tp_comm", "rccl").startswith("xgmi") and tp_group is not None and device.type == "cuda":
             from ..parallel.xgmi import XgmiCommunicator
             from ..utils import comm as _comm

@@ -188,3 +188,24 @@ def test_offload_grad_ring_auto_policy(monkeypatch):
     assert _grad_ring_auto(args, model, None, offload_params=True) == 4  # 8 ranks x 8 MB > 85 % of 50 MB
     args.grad_accum = 2
     assert _grad_ring_auto(args, model, None, offload_params=False) == 0
+
+
+@pytest.mark.slow
+def test_dp_comm_auto_child_crash_trains_on_rccl(tmp_path):
+    """--dp-comm auto calibrates in a child job (parallel/transport.py resolve_isolated); a child
+    that crashes leaves the trainer on RCCL (the process group), with the error logged, and the
+    run trains to the end (VERDICT r5 next #3)."""
+    env_stub = json.dumps([sys.executable, "-c", "import sys; sys.stderr.write('boom'); sys.exit(7)"])
+    os.environ["DTG_TRANSPORT_CHILD_CMD"] = env_stub
+    try:
+        r = _torchrun("02-distributed-data-parallel",
+                      ["-e", "auto", "-d", "synthetic", "-m", "llama-tiny", "-s", "32", "--num-samples", "32",
+                       "--save-dir", str(tmp_path), "--log-freq", "1", "--ckpt-freq", "100", "--num-workers", "0",
+                       "--max-steps", "2", "--dp-comm", "auto"])
+    finally:
+        del os.environ["DTG_TRANSPORT_CHILD_CMD"]
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "dp transport calibration" in out and "calibration child exited 7" in out and "-> rccl" in out, out[-3000:]
+    recs = [json.loads(line) for line in (tmp_path / "auto" / "metrics-rank0.jsonl").read_text().splitlines()]
+    assert len(recs) == 2

@@ -63,16 +63,70 @@ def test_resolve_on_cpu_is_the_process_group():
     assert explicit == ("xgmi", None)
 
 
-def test_trainer_and_bench_default_to_auto():
+def test_trainer_defaults_to_rccl_and_bench_to_auto():
+    """The trainer's chapters default to RCCL (auto is opt-in and runs in a child job); the bench
+    keeps auto, which it has always calibrated in a child job."""
     import bench
     from dtg.train.cli import get_parser
 
     for ch in ("06", "07"):
         a = get_parser(ch).parse_args(["-e", "x", "-d", "synthetic", "-m", "llama-tiny"])
-        assert a.tp_comm == "auto"
+        assert a.tp_comm == "rccl"
     for ch in ("02", "04", "05", "07"):
         a = get_parser(ch).parse_args(["-e", "x", "-d", "synthetic", "-m", "llama-tiny"])
-        assert a.dp_comm == "auto"
+        assert a.dp_comm == "rccl"
     b = bench.parse([])
     assert b.tp_comm == "auto" and b.dp_comm == "auto"
     assert math.isfinite(b.deadline_s) and b.diag_budget_s < b.deadline_s
+
+
+def _isolated(rank, world, stub, timeout):
+    import json
+    import os
+
+    from dtg.parallel import transport
+
+    os.environ["DTG_TRANSPORT_CHILD_CMD"] = json.dumps(stub)
+    logged = []
+    out = transport.resolve_isolated("auto", "tp", "cpu", 8 << 20, mesh=(world, 1), log=logged.append,
+                                     child_timeout=timeout)
+    return out, logged
+
+
+def test_isolated_calibration_child_crash_falls_back_to_rccl():
+    import sys
+
+    res = run_distributed(_isolated, 2, [sys.executable, "-c", "import sys; sys.exit(3)"], 60)
+    for (choice, table), logged in res:
+        assert choice == "rccl"
+        assert "exited 3" in table["child"]["error"]
+    assert "-> rccl" in res[0][1][0] and "exited 3" in res[0][1][0]
+
+
+def test_isolated_calibration_child_timeout_falls_back_to_rccl():
+    import sys
+
+    res = run_distributed(_isolated, 2, [sys.executable, "-c", "import time; time.sleep(30)"], 2)
+    assert all(c == "rccl" and "timed out" in t["child"]["error"] for (c, t), _ in res)
+
+
+def test_isolated_calibration_every_rank_takes_the_childs_pick():
+    import json
+    import sys
+
+    rec = {"choice": "xgmi-dma", "table": {"rccl": {"us": 30.0}, "xgmi": {"us": 25.0}, "xgmi-dma": {"us": 20.0}}}
+    res = run_distributed(_isolated, 2, [sys.executable, "-c", f"print({json.dumps(json.dumps(rec))})"], 60)
+    assert [c for (c, _), _ in res] == ["xgmi-dma", "xgmi-dma"]
+    bad = dict(rec, choice="nvlink")
+    res = run_distributed(_isolated, 2, [sys.executable, "-c", f"print({json.dumps(json.dumps(bad))})"], 60)
+    assert all(c == "rccl" and "picked 'nvlink'" in t["child"]["error"] for (c, t), _ in res)
+
+
+def test_real_calibration_child_runs_on_cpu():
+    """The real child script under torchrun (2 gloo ranks on the CPU: the process group's own
+    collectives, recorded with the CPU note)."""
+    from dtg.parallel import transport
+
+    rec = transport.run_child(2, {"kind": "dp", "msg_bytes": 1 << 20, "mesh": [1, 0], "timeout_s": None}, 240)
+    assert rec.get("choice") == "rccl", rec
+    assert "CPU" in rec["table"]["rccl"]["note"]
