@@ -118,6 +118,13 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
         g.add_argument("--dp-mode", default="zero", choices=["ddp", "zero"],
                        help="zero: sharded optimizer (reference's ZeroRedundancyOptimizer); ddp: replicated")
     g.add_argument("--activation-checkpointing", default="on" if chapter == "05" else "off", choices=["on", "off"])
+    g.add_argument("--ac-layers", default="all",
+                   help="with --activation-checkpointing on: how many decoder layers recompute their forward "
+                        "(the first N of this rank's stack; the others keep their activations).  all = every "
+                        "layer (the reference); N; auto = after step 1, as few as the measured peak, the "
+                        "per-layer activation size and --ac-budget-gb allow (agreed over all ranks)")
+    g.add_argument("--ac-budget-gb", default=270.0, type=float,
+                   help="HBM budget (GB per GPU) --ac-layers auto plans against (MI355X: 288 GB)")
     g.add_argument("--reshard-after-forward", default="on", choices=["on", "off"])
     g.add_argument("--num-workers", default=1, type=int)
     g.add_argument("--prefetch-factor", default=2, type=int)

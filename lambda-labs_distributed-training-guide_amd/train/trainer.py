@@ -29,7 +29,7 @@ from tqdm import tqdm
 
 from .. import data as dtg_data
 from ..models import build_model, count_valid_labels, resolve_config
-from ..parallel.checkpointing import apply_activation_checkpointing
+from ..parallel.checkpointing import apply_activation_checkpointing, checkpointed_count
 from ..parallel.data_parallel import DataParallel, FlatAdamW
 from ..utils import comm as ucomm
 from ..utils import dist as udist
@@ -247,8 +247,14 @@ def _build(args, chapter, device, world):
         model._dtg_layer_offset = stage.layer_range[0]  # checkpoints use global layer names
         model._dtg_pp = stage
         LOGGER.info(f"pipeline stage {stage.stage}/{pp}: layers [{stage.layer_range[0]}, {stage.layer_range[1]})")
+    model._dtg_ac_auto = None
     if args.activation_checkpointing == "on":
-        apply_activation_checkpointing(model)
+        spec = str(getattr(args, "ac_layers", "all"))
+        apply_activation_checkpointing(model, count=None if spec in ("all", "auto") else int(spec))
+        if spec == "auto":
+            model._dtg_ac_auto = {"tp": tp_group.size() if tp_group is not None else 1}
+        LOGGER.info(f"activation checkpointing: {checkpointed_count(model)} of {len(model.layers)} layers"
+                    + (" (auto: re-planned after step 1 against --ac-budget-gb)" if spec == "auto" else ""))
     LOGGER.info(f"{sum(p.numel() for p in model.parameters()) / 1e9:.3f}B parameters (this rank's shard of TP)")
     LOGGER.info(f"Before engine: {get_mem_stats(device)}")
     if fsdp:
@@ -500,6 +506,9 @@ def run(chapter: str, argv=None):
                 torch.distributed.all_reduce(loss_sum, group=model._dtg_seq[1])
             state["global_step"] += 1
             state["epoch_step"] += 1
+            if model._dtg_ac_auto is not None:
+                _plan_ac_layers(args, model, cfg, device, model._dtg_ac_auto["tp"], seq_length)
+                model._dtg_ac_auto = None
             # host read of the xGMI communicators' pinned error words (no device sync): a peer
             # lost in this step's barriers stops the job here, not at the next log step
             ucomm.poll_xgmi()
@@ -532,6 +541,8 @@ def run(chapter: str, argv=None):
                 }
                 if getattr(engine, "cpu_offload", False):
                     info.update(_offload_info(engine))
+                if args.activation_checkpointing == "on":
+                    info["ac/layers"] = checkpointed_count(model)
                 LOGGER.info(info)
                 sink.log(info, state["global_step"])
                 if device.type == "cuda":
@@ -559,6 +570,36 @@ def run(chapter: str, argv=None):
     mgr.finalize()
     ucomm.check_xgmi()
     return state
+
+
+def _plan_ac_layers(args, model, cfg, device, tp: int, seq_length: int, peak_bytes=None) -> int:
+    """--ac-layers auto, after the first step: keep checkpointed only as many layers as the HBM
+    budget requires.  The step's peak (every layer checkpointed) is measured; each layer released
+    adds its activations (layer_activation_bytes, x1.25) minus its checkpointed input.  Every rank
+    takes the largest count any rank needs (a recompute re-issues the layer's TP collectives).
+    Returns the number of checkpointed layers."""
+    import torch.distributed as dist
+
+    from ..parallel.checkpointing import ac_layers_for_budget, layer_activation_bytes, set_checkpointed_layers
+
+    n_ckpt = checkpointed_count(model)
+    if peak_bytes is None:
+        if device.type != "cuda":
+            LOGGER.info("--ac-layers auto: no HBM to plan against off the GPU; every layer stays checkpointed")
+            return n_ckpt
+        peak_bytes = torch.cuda.max_memory_reserved(device)
+    per_layer = layer_activation_bytes(cfg, args.batch_size, seq_length, tp)
+    inp = 2 * cfg.hidden_size * args.batch_size * seq_length // max(1, tp)
+    keep = ac_layers_for_budget(len(model.layers), n_ckpt, int(peak_bytes), int(args.ac_budget_gb * 1e9), per_layer, inp)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([keep], dtype=torch.int64,
+                         device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        keep = int(t.item())
+    set_checkpointed_layers(model, keep)
+    LOGGER.info(f"--ac-layers auto: step-1 peak {peak_bytes / 1e9:.1f} GB, budget {args.ac_budget_gb:g} GB, "
+                f"{per_layer / 1e9:.2f} GB per released layer -> {keep} of {len(model.layers)} layers checkpointed")
+    return keep
 
 
 def _offload_info(engine) -> dict:

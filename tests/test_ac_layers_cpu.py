@@ -1,0 +1,117 @@
+"""Activation checkpointing with a layer budget (`--ac-layers N|auto`, parallel/checkpointing.py;
+VERDICT r5 next #1): checkpointing any subset of the layers leaves every gradient bitwise equal to
+checkpointing all of them (and to none); the budget arithmetic releases as many layers as the
+HBM headroom holds; the trainer runs chapter 05 with a partial count and with auto.
+
+Reference: /root/reference/05-training-llama-405b/train_llm.py:122-126 (every layer)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from _dist import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _grads(count, n_layers=4, ac=True):
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.checkpointing import apply_activation_checkpointing, checkpointed_count
+
+    cfg = resolve_config("llama-tiny", num_hidden_layers=n_layers)
+    torch.manual_seed(0)
+    m = build_model(cfg, device="cpu", dtype=torch.bfloat16)
+    if ac:
+        apply_activation_checkpointing(m, count=count)
+        assert checkpointed_count(m) == (n_layers if count is None else min(count, n_layers))
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, cfg.vocab_size, (2, 64), generator=g)
+    loss = m(input_ids=ids, labels=ids).loss
+    loss.backward()
+    return loss.detach(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+
+
+def test_partial_checkpointing_is_bitwise_full_checkpointing():
+    ref_loss, ref = _grads(None)
+    for count in (0, 1, 3):
+        loss, got = _grads(count)
+        assert torch.equal(loss, ref_loss)
+        assert got.keys() == ref.keys()
+        for k in ref:
+            assert torch.equal(got[k], ref[k]), (count, k)
+    loss, got = _grads(None, ac=False)
+    assert torch.equal(loss, ref_loss) and all(torch.equal(got[k], ref[k]) for k in ref)
+
+
+def test_set_checkpointed_layers_switches_between_steps():
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.checkpointing import (apply_activation_checkpointing, checkpointed_count,
+                                            set_checkpointed_layers)
+
+    cfg = resolve_config("llama-tiny", num_hidden_layers=4)
+    m = build_model(cfg, device="cpu", dtype=torch.float32)
+    apply_activation_checkpointing(m)
+    fwd = [layer.forward for layer in m.layers]
+    set_checkpointed_layers(m, 1)
+    assert [layer._dtg_checkpointed for layer in m.layers] == [True, False, False, False]
+    assert [layer.forward for layer in m.layers] == fwd  # wrapped once, switched by the flag
+    set_checkpointed_layers(m, 4)
+    assert checkpointed_count(m) == 4
+
+
+def test_budget_releases_what_the_headroom_holds():
+    from dtg.models import resolve_config
+    from dtg.parallel.checkpointing import ac_layers_for_budget, layer_activation_bytes
+
+    GB = 10 ** 9
+    # 100 checkpointed layers, 128 GB peak, 270 GB budget, 1.7 GB per layer, 0.13 GB input
+    keep = ac_layers_for_budget(100, 100, 128 * GB, 270 * GB, int(1.7 * GB), int(0.13 * GB))
+    assert keep == 100 - int((142 * GB) // int((1.7 - 0.13) * GB * 1.25))
+    assert ac_layers_for_budget(100, 100, 280 * GB, 270 * GB, GB, 0) == 100  # over budget: all stay
+    assert ac_layers_for_budget(10, 10, 1 * GB, 270 * GB, GB, 0) == 0       # everything fits
+    cfg = resolve_config("meta-llama/Llama-3.1-405B")
+    b = layer_activation_bytes(cfg, 4, 4096, tp=4)  # the tp 4 x dp 2 one-node recipe
+    assert 1.8e9 < b < 2.4e9
+
+
+def test_plan_ac_layers_with_a_measured_peak():
+    import argparse
+
+    from dtg.models import build_model, resolve_config
+    from dtg.parallel.checkpointing import apply_activation_checkpointing, layer_activation_bytes
+    from dtg.train.trainer import _plan_ac_layers
+
+    cfg = resolve_config("llama-tiny", num_hidden_layers=8)
+    m = build_model(cfg, device="cpu", dtype=torch.float32)
+    apply_activation_checkpointing(m)
+    per = layer_activation_bytes(cfg, 2, 128)
+    inp = 2 * cfg.hidden_size * 2 * 128
+    args = argparse.Namespace(batch_size=2, ac_budget_gb=(1e9 + 3.5 * (per - inp) * 1.25) / 1e9)
+    keep = _plan_ac_layers(args, m, cfg, torch.device("cpu"), 1, 128, peak_bytes=int(1e9))
+    assert keep == 5 and [layer._dtg_checkpointed for layer in m.layers] == [True] * 5 + [False] * 3
+
+
+def _torchrun(chapter_dir, args, nproc=2, timeout=400):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, chapter_dir, "train_llm.py")] + args
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=dict(os.environ, OMP_NUM_THREADS="1"))
+
+
+@pytest.mark.slow
+def test_chapter05_partial_ac_matches_full_ac(tmp_path):
+    losses = {}
+    for spec in ("all", "1", "auto"):
+        r = _torchrun("05-training-llama-405b",
+                      ["-e", f"ac{spec}", "-d", "synthetic", "-m", "llama-tiny", "-s", "64", "--num-samples", "64",
+                       "--save-dir", str(tmp_path), "--log-freq", "1", "--ckpt-freq", "100", "--num-workers", "0",
+                       "--max-steps", "3", "--cpu-offload", "off", "--ac-layers", spec])
+        out = r.stdout + r.stderr
+        assert r.returncode == 0, out[-3000:]
+        recs = [json.loads(x) for x in (tmp_path / f"ac{spec}" / "metrics-rank0.jsonl").read_text().splitlines()]
+        losses[spec] = [x["running_loss"] for x in recs]
+        assert recs[0]["ac/layers"] == (1 if spec == "1" else 2)
+    assert losses["1"] == losses["all"] == losses["auto"]
