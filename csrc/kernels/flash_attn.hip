@@ -145,7 +145,7 @@ constexpr int acc_row0(int reg) { return (reg & 3) + 8 * (reg >> 2); }
 // Attention-probability dropout (GPT-2's attn_pdrop), regenerated in the backward
 // instead of stored.  The keep decision of (query q, key k) -- sequence-relative indices of
 // sequence s0 = cu[seq], query head hd -- is byte (k & 3) of word (q & 3) of
-//     Philox4x32-10(counter = {k & ~3, s0 + (q & ~3), hd, offset}, key = seed)
+//     Philox4x32-10(counter = {k & ~3, s0 + (q & ~3), hd, offset lo}, key = {seed lo, seed hi ^ offset hi})
 // compared with thr = round(keep * 256): kept iff byte < thr, so the keep probability is exactly
 // thr / 256 and kept probabilities are scaled by 256 / thr (unbiased).  One Philox call covers a
 // 4 x 4 (query, key) block, which matches both accumulator layouts: a forward / dQ lane owns one
@@ -169,7 +169,7 @@ __device__ __forceinline__ DropCfg resolve_drop(const DropCfg& in) {
   DropCfg d = in;
   if (d.rng != nullptr) {
     d.k0 = d.rng[0];
-    d.k1 = d.rng[1];
+    d.k1 = d.rng[1] ^ d.rng[3];  // the offset's high word keys the generator (no wrap at 2^32)
     d.off = d.rng[2];
   }
   return d;
@@ -242,39 +242,6 @@ struct Stager {
     const int o = off<W>(threadIdx.x / NCH, threadIdx.x % NCH);
 #pragma unroll
     for (int i = 0; i < PER; ++i) *reinterpret_cast<u16x8*>(tile + o + i * RSTEP * W * 2) = regs[i];
-  }
-};
-
-// LDS-DMA copy of R rows x W bf16 (token stride `stride`) into the swizzled LDS image of Stager:
-// `buffer_load_dwordx4 ... lds` writes each lane's 16 bytes at M0 + 16 * lane, i.e. one 1-KiB
-// piece per wave-instruction, so a lane fetches the chunk whose swizzled place in the image is
-// its own position in the piece (a per-lane source address, CDNA guide App. B 'gather into
-// LDS').  No staging registers and no ds_write; rows at or past `nvalid` read as zeros from the
-// descriptor's range check.  Completion is the issuing wave's vmcnt (a __syncthreads drains it).
-template <int R, int W>
-struct DmaStager {
-  static constexpr int NCH = W / 8;            // 16-byte chunks per row
-  static constexpr int ROWS_PER_PIECE = 64 / NCH;
-  static constexpr int PIECES = R / ROWS_PER_PIECE;
-  static_assert(PIECES % 4 == 0, "pieces split over 4 waves");
-  __device__ __forceinline__ static void issue(const uint16_t* base, int64_t stride, int nvalid, char* tile) {
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int bytes = nvalid > 0 ? static_cast<int>((nvalid - 1) * stride * 2 + W * 2) : 0;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, bytes);
-    const int s2 = static_cast<int>(stride) * 2;
-    const int prow = lane / NCH, pc = lane % NCH;
-#pragma unroll
-    for (int j = 0; j < PIECES / 4; ++j) {
-      const int p = w * (PIECES / 4) + j;
-      const int row = p * ROWS_PER_PIECE + prow;
-      int sw;
-      if constexpr (NCH == 16) sw = ((row & 3) << 2) | ((row >> 2) & 3);
-      else sw = ((row & 1) << 2) | ((row >> 1) & 3);
-      const int ch = pc ^ sw;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(tile + p * 1024), 16,
-                                               row * s2 + ch * 16, 0, 0, 0);
-    }
   }
 };
 
@@ -375,7 +342,7 @@ constexpr int kFwdBK = 64;   // keys per K/V tile
 
 // WIN: sliding-window instantiation (only launched with P.window > 0); without it every window
 // term folds to a compile-time 0 and the kernel is the plain causal one.
-template <int D, bool CAUSAL, bool WIDE, bool QLDS, bool WIN = false, bool DROP = false>
+template <int D, bool CAUSAL, bool WIN = false, bool DROP = false>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   [[maybe_unused]] const DropCfg dcfg = DROP ? resolve_drop(P.drop) : P.drop;
   constexpr int RB = 2 * D;
@@ -399,12 +366,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   const int qrow = q0 + 32 * w + r;  // this lane's query (sequence-relative)
 
   bf16x8 qf[NC];  // Q^T fragments for all k-steps
-  // QLDS: Q rows arrive as whole 256-B lines (the K/V stager's coalesced buffer loads) and are
-  // turned into fragments through LDS, instead of fragment-shaped loads (32 rows x 32 B per
-  // instruction) straight to registers.
+  // Q rows arrive as whole 256-B lines (the K/V stager's coalesced buffer loads) and are turned
+  // into fragments through LDS (fragment-shaped loads straight to registers, 32 rows x 32 B per
+  // instruction, were slower: profiles/r3).
   Stager<kFwdBQ, D, 256> sq;
-  if constexpr (QLDS) sq.load(P.q + (int64_t)(s0 + q0) * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
-  else load_row_frags<NC>(P.q + (int64_t)(s0 + min(qrow, seqlen - 1)) * P.sq + (int64_t)head * D, qrow < seqlen, h, qf);
+  sq.load(P.q + (int64_t)(s0 + q0) * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
   int koff[NC], toa[ND], tob[ND];
 #pragma unroll
   for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
@@ -427,15 +393,13 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   Stager<kFwdBK, D, 256> sk, sv;
   sk.load(kbase + (int64_t)t_begin * kFwdBK * P.sk, P.sk, klen - t_begin * kFwdBK);
   sv.load(vbase + (int64_t)t_begin * kFwdBK * P.sv, P.sv, klen - t_begin * kFwdBK);
-  if constexpr (QLDS) sq.store(smem + 2 * TILE);  // the second K/V buffer is free until tile 0 ends
+  sq.store(smem + 2 * TILE);  // the second K/V buffer is free until tile 0 ends
   sk.store(smem);
   sv.store(smem + TILE);
   __syncthreads();
-  if constexpr (QLDS) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) qf[c] = lds_frag(smem + 2 * TILE + 32 * w * RB + koff[c]);
-    __syncthreads();  // every wave holds its Q before tile 0 restages that buffer
-  }
+  for (int c = 0; c < NC; ++c) qf[c] = lds_frag(smem + 2 * TILE + 32 * w * RB + koff[c]);
+  __syncthreads();  // every wave holds its Q before tile 0 restages that buffer
   fa_stamp(P.stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), 1);
 
   const int wave_q0 = q0 + 32 * w, wave_qmax = wave_q0 + 31;
@@ -547,560 +511,13 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
   const float lt = pair_sum(l);
   const float inv = (lt > 0.f ? 1.f / lt : 0.f) * (DROP ? P.drop.scale : 1.f);
   uint16_t* op = P.o + ((int64_t)(s0 + min(qrow, seqlen - 1)) * P.hq + head) * D;
-  if constexpr (WIDE) {
-    store_rows_wide<ND>(acc, inv, op, qrow < seqlen);
-  } else if (qrow < seqlen) {
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        ushort4 v;
-        v.x = f2bf(acc[d][4 * g4 + 0] * inv);
-        v.y = f2bf(acc[d][4 * g4 + 1] * inv);
-        v.z = f2bf(acc[d][4 * g4 + 2] * inv);
-        v.w = f2bf(acc[d][4 * g4 + 3] * inv);
-        *reinterpret_cast<ushort4*>(op + 32 * d + 8 * g4 + 4 * h) = v;
-      }
-    }
-  }
+  store_rows_wide<ND>(acc, inv, op, qrow < seqlen);
   if (qrow < seqlen && h == 0)
     P.lse[(int64_t)head * P.T + s0 + qrow] = (lt > 0.f) ? (m + log2f(lt)) * kLn2 : -INFINITY;
   if (P.stamps != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     fa_stamp(P.stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), 3);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Forward, one wave per SIMD ("f64"): the CDNA guide's persistent 4-wave structure (App. B,
-// "4-wave, one-wave-per-SIMD, persistent") in plain HIP.  A workgroup is 4 waves and the CU's
-// only one (__launch_bounds__(256, 1): the whole 512-entry register file per lane); a work item
-// is a 256-row query block of one (sequence, head), and every wave owns 64 of its rows as two
-// 32-row blocks A (rows 32w..) and B (rows 128 + 32w..; interleaved so the causal diagonal costs
-// every wave about the same).  Each K fragment read from LDS feeds two MFMAs (A and B), each V
-// fragment two more: half the LDS read traffic per MFMA of the 2-wave kernel above, whose
-// 32-row waves re-read every K / V fragment per 32 queries.  Workgroups are persistent (one per
-// CU) and take items from a device counter, heaviest (latest causal) blocks first, so the
-// launch has no tail of idle CUs and no per-item launch cost.
-// Numerics are those of fwd_kernel: same tiles (64 keys), same lazy rescale, same f32 sums.
-constexpr int kF64Rows = 256;
-
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void fwd64_kernel(FwdParams P, int* __restrict__ queue, int nqb, int nseq) {
-  constexpr int RB = 2 * D;
-  constexpr int TILE = kFwdBK * RB;
-  constexpr int NC = D / 16;
-  constexpr int ND = D / 32;
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1 | Q (256 rows)]
-  char* const qsm = smem + 4 * TILE;
-  __shared__ int item_sh;
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int nitems = nqb * nseq * P.hq;
-  int koff[NC], toa[ND], tob[ND];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
-#pragma unroll
-  for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
-
-  if (threadIdx.x == 0) item_sh = atomicAdd(queue, 1);
-  __syncthreads();
-  int item = item_sh;
-  while (item < nitems) {
-    __syncthreads();  // every lane has read item_sh
-    if (threadIdx.x == 0) item_sh = atomicAdd(queue, 1);  // the next item, read after this one
-    const int per_z = nseq * P.hq;
-    const int zz = item / per_z, rem = item - zz * per_z;
-    const int seq = rem / P.hq, head = grid_head(rem - seq * P.hq, P.hq, P.hkv);
-    const int qb = CAUSAL ? nqb - 1 - zz : zz;  // heaviest blocks first
-    const int s0 = P.cu[seq];
-    const int seqlen = P.cu[seq + 1] - s0;
-    const int q0 = qb * kF64Rows;
-    if (q0 < seqlen) {
-      const int kvh = head / (P.hq / P.hkv);
-      const int qa = q0 + 32 * w, qbb = q0 + 128 + 32 * w;  // first rows of blocks A and B
-      const int kv_end = CAUSAL ? min(seqlen, q0 + kF64Rows) : seqlen;
-      const int ntiles = (kv_end + kFwdBK - 1) / kFwdBK;
-      // a block skips the tiles above its diagonal (wave-uniform); B is always the later block
-      const int lastA = CAUSAL ? min(ntiles - 1, (qa + 31) / kFwdBK) : ntiles - 1;
-      const uint16_t* kbase = P.k + (int64_t)s0 * P.sk + (int64_t)kvh * D;
-      const uint16_t* vbase = P.v + (int64_t)s0 * P.sv + (int64_t)kvh * D;
-      {
-        Stager<kF64Rows, D, 256> sq;
-        sq.load(P.q + (int64_t)(s0 + q0) * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
-        sq.store(qsm);
-      }
-      Stager<kFwdBK, D, 256> sk, sv;
-      sk.load(kbase, P.sk, seqlen);
-      sv.load(vbase, P.sv, seqlen);
-      sk.store(smem);
-      sv.store(smem + TILE);
-      __syncthreads();
-      bf16x8 qf[2][NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        qf[0][c] = lds_frag(qsm + 32 * w * RB + koff[c]);
-        qf[1][c] = lds_frag(qsm + (128 + 32 * w) * RB + koff[c]);
-      }
-      f32x16 acc[2][ND];
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int d = 0; d < ND; ++d) acc[b][d] = f32x16{};
-      float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-      const int row[2] = {qa + r, qbb + r};
-
-      // one 64-key tile for blocks A and B (BOTH) or B alone
-      auto tile_step = [&](int t, auto buf, auto both_c) {
-        constexpr int BUF = decltype(buf)::value;
-        constexpr bool BOTH = decltype(both_c)::value;
-        constexpr int B0 = BOTH ? 0 : 1;
-        const int kt0 = t * kFwdBK;
-        const bool more = t + 1 < ntiles;
-        if (more) {
-          const int nk = kt0 + kFwdBK;
-          sk.load(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk);
-          sv.load(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk);
-        }
-        const char* K = smem + BUF * 2 * TILE;
-        const char* V = K + TILE;
-        f32x16 s[2][2];
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-          for (int b = B0; b < 2; ++b) s[b][kt] = f32x16{};
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            const bf16x8 kf = lds_frag(K + kt * 32 * RB + koff[c]);
-#pragma unroll
-            for (int b = B0; b < 2; ++b) s[b][kt] = mfma(kf, qf[b][c], s[b][kt]);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        bf16x8 pf[2][4];
-#pragma unroll
-        for (int b = B0; b < 2; ++b) {
-          const int wq0 = b ? qbb : qa;
-          if ((CAUSAL && kt0 + kFwdBK - 1 > wq0) || kt0 + kFwdBK > seqlen) {
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-              const int lim = (CAUSAL ? min(row[b], seqlen - 1) : seqlen - 1) - (kt0 + 32 * kt + 4 * h);
-#pragma unroll
-              for (int i = 0; i < 16; ++i) s[b][kt][i] = acc_row0(i) > lim ? -INFINITY : s[b][kt][i];
-            }
-          }
-          float mx = s[b][0][0];
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[b][kt][i]);
-          mx = pair_max(mx) * P.c2;
-          if (__builtin_amdgcn_ballot_w64(mx > m[b] + kRescaleThreshold) != 0) {
-            const float mn = fmaxf(m[b], mx);
-            const float alpha = (mn == -INFINITY) ? 1.f : fexp2(m[b] - mn);
-            l[b] *= alpha;
-#pragma unroll
-            for (int d = 0; d < ND; ++d) acc[b][d] *= alpha;
-            m[b] = mn;
-          }
-          const float mu = (m[b] == -INFINITY) ? 0.f : m[b];
-          float rs = 0.f;
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const float p = fexp2(__builtin_fmaf(s[b][kt][i], P.c2, -mu));
-              s[b][kt][i] = p;
-              rs += p;
-            }
-          l[b] += rs;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pf[b][j] = pack8(s[b][j >> 1], j & 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const char* vb = V + 16 * j * RB;
-          bf16x8 vt[ND];
-#pragma unroll
-          for (int d = 0; d < ND; ++d) vt[d] = tr_frag_at(vb + toa[d], vb + tob[d]);
-#pragma unroll
-          for (int d = 0; d < ND; ++d)
-#pragma unroll
-            for (int b = B0; b < 2; ++b) acc[b][d] = mfma(vt[d], pf[b][j], acc[b][d]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (more) {
-          char* nb = smem + (1 - BUF) * 2 * TILE;
-          sk.store(nb);
-          sv.store(nb + TILE);
-        }
-        __syncthreads();
-      };
-      using I0 = std::integral_constant<int, 0>;
-      using I1 = std::integral_constant<int, 1>;
-      using BT = std::integral_constant<bool, true>;
-      using BF = std::integral_constant<bool, false>;
-      int t = 0;
-      for (; t + 1 <= lastA; t += 2) {  // both blocks, two tiles per trip (immediate buffer offsets)
-        tile_step(t, I0{}, BT{});
-        tile_step(t + 1, I1{}, BT{});
-      }
-      if (t <= lastA) {
-        tile_step(t, I0{}, BT{});
-        ++t;
-        if (t < ntiles) {
-          tile_step(t, I1{}, BF{});
-          ++t;
-        }
-      }
-      for (; t + 1 < ntiles; t += 2) {  // block B alone (causal diagonal); t is even here
-        tile_step(t, I0{}, BF{});
-        tile_step(t + 1, I1{}, BF{});
-      }
-      if (t < ntiles) tile_step(t, I0{}, BF{});
-
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const float lt = pair_sum(l[b]);
-        const float inv = lt > 0.f ? 1.f / lt : 0.f;
-        uint16_t* op = P.o + ((int64_t)(s0 + min(row[b], seqlen - 1)) * P.hq + head) * D;
-        store_rows_wide<ND>(acc[b], inv, op, row[b] < seqlen);
-        if (row[b] < seqlen && h == 0)
-          P.lse[(int64_t)head * P.T + s0 + row[b]] = (lt > 0.f) ? (m[b] + log2f(lt)) * kLn2 : -INFINITY;
-      }
-    }
-    __syncthreads();  // the next item's index is in item_sh; LDS is free for its prologue
-    item = item_sh;
-  }
-}
-
-// Software-pipelined form of fwd64_kernel ("p64"): with one wave per SIMD no partner wave
-// fills the matrix pipe while a wave runs its softmax, so the wave overlaps its own phases (CDNA
-// guide T15 / App. B): iteration i issues
-//   phase 1: S(i+1) = K(i+1) Q^T (32 MFMAs)      beside  the second half of softmax(i) -> P(i)
-//   phase 2: O += V(i)^T P(i)^T  (32 MFMAs)      beside  the first half of softmax(i+1)
-// as straight-line blocks (no branches inside; the rare lazy rescale of O and the causal /
-// sequence-end masks run between the phases), so the scheduler can interleave MFMAs and VALU.
-// The rescale is deferred to the next iteration's head: O and l still hold tile i's terms at the
-// old max when softmax(i+1) raises it, and both are multiplied exactly once, before anything at
-// the new max is added (T13's hazard).  K runs one tile ahead of V in the LDS ring.  Tiles on
-// the causal diagonal of the work item (where the blocks of a wave stop at different tiles) take
-// fwd64's non-pipelined step.
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void fwd64p_kernel(FwdParams P, int* __restrict__ queue, int nqb, int nseq) {
-  constexpr int RB = 2 * D;
-  constexpr int TILE = kFwdBK * RB;
-  constexpr int NC = D / 16;
-  constexpr int ND = D / 32;
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // [K0 | V0 | K1 | V1 | Q (256 rows)]
-  char* const qsm = smem + 4 * TILE;
-  __shared__ int item_sh;
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int nitems = nqb * nseq * P.hq;
-  int koff[NC], toa[ND], tob[ND];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) koff[c] = off<D>(r, 2 * c + h);
-#pragma unroll
-  for (int d = 0; d < ND; ++d) tr_offsets<D>(d, toa[d], tob[d]);
-
-  if (threadIdx.x == 0) item_sh = atomicAdd(queue, 1);
-  __syncthreads();
-  int item = item_sh;
-  while (item < nitems) {
-    __syncthreads();
-    if (threadIdx.x == 0) item_sh = atomicAdd(queue, 1);
-    const int per_z = nseq * P.hq;
-    const int zz = item / per_z, rem = item - zz * per_z;
-    const int seq = rem / P.hq, head = grid_head(rem - seq * P.hq, P.hq, P.hkv);
-    const int qb = CAUSAL ? nqb - 1 - zz : zz;
-    const int s0 = P.cu[seq];
-    const int seqlen = P.cu[seq + 1] - s0;
-    const int q0 = qb * kF64Rows;
-    if (q0 < seqlen) {
-      const int kvh = head / (P.hq / P.hkv);
-      const int qa = q0 + 32 * w, qbb = q0 + 128 + 32 * w;
-      const int kv_end = CAUSAL ? min(seqlen, q0 + kF64Rows) : seqlen;
-      const int ntiles = (kv_end + kFwdBK - 1) / kFwdBK;
-      const int lastA = CAUSAL ? min(ntiles - 1, (qa + 31) / kFwdBK) : ntiles - 1;
-      // tiles [0, F): both blocks of every wave active -> pipelined; [F, ntiles): the diagonal
-      const int F = CAUSAL ? min(ntiles, q0 / kFwdBK + 1) : ntiles;
-      const uint16_t* kbase = P.k + (int64_t)s0 * P.sk + (int64_t)kvh * D;
-      const uint16_t* vbase = P.v + (int64_t)s0 * P.sv + (int64_t)kvh * D;
-      using KV = DmaStager<kFwdBK, D>;
-      DmaStager<kF64Rows, D>::issue(P.q + (int64_t)(s0 + q0) * P.sq + (int64_t)head * D, P.sq, seqlen - q0, qsm);
-      KV::issue(kbase, P.sk, seqlen, smem);
-      KV::issue(vbase, P.sv, seqlen, smem + TILE);
-      if (ntiles > 1) KV::issue(kbase + (int64_t)kFwdBK * P.sk, P.sk, seqlen - kFwdBK, smem + 2 * TILE);
-      __syncthreads();
-      // Q stays in LDS for the item (register budget: O, two S tiles and P are live at once);
-      // each k-step reads the two Q fragments and the two K fragments for its four MFMAs
-      const char* qrow[2] = {qsm + 32 * w * RB, qsm + (128 + 32 * w) * RB};
-      f32x16 acc[2][ND];
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int d = 0; d < ND; ++d) acc[b][d] = f32x16{};
-      float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-      float alpha[2] = {1.f, 1.f}, rsp[2] = {0.f, 0.f};
-      bool pend[2] = {false, false};
-      const int row[2] = {qa + r, qbb + r};
-      f32x16 sE[2][2], sO[2][2];  // S of even / odd tiles: [block][32-key half]
-      bf16x8 pf[2][4];            // P of the tile PV consumes (keys 0..31 packed by sm_start, 32..63 by sm_finish)
-      bf16x8 pn[2][2];            // keys 0..31 of the next tile's P, packed as soon as exponentiated
-
-      auto qk = [&](const char* K, f32x16 (&sn)[2][2]) {
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt) sn[b][kt] = f32x16{};
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          const bf16x8 qa_ = lds_frag(qrow[0] + koff[c]);
-          const bf16x8 qb_ = lds_frag(qrow[1] + koff[c]);
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            const bf16x8 kf = lds_frag(K + kt * 32 * RB + koff[c]);
-            sn[0][kt] = mfma(kf, qa_, sn[0][kt]);
-            sn[1][kt] = mfma(kf, qb_, sn[1][kt]);
-          }
-        }
-      };
-      auto mask = [&](int t, f32x16 (&sn)[2][2]) {
-        const int kt0 = t * kFwdBK;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int wq0 = b ? qbb : qa;
-          if ((CAUSAL && kt0 + kFwdBK - 1 > wq0) || kt0 + kFwdBK > seqlen) {
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-              const int lim = (CAUSAL ? min(row[b], seqlen - 1) : seqlen - 1) - (kt0 + 32 * kt + 4 * h);
-#pragma unroll
-              for (int i = 0; i < 16; ++i) sn[b][kt][i] = acc_row0(i) > lim ? -INFINITY : sn[b][kt][i];
-            }
-          }
-        }
-      };
-      // first half of the softmax: row max, lazy-rescale decision (deferred), exps of keys 0..31
-      auto sm_start = [&](f32x16 (&sn)[2][2]) {
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          float mx = sn[b][0][0];
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sn[b][kt][i]);
-          mx = pair_max(mx) * P.c2;
-          const bool grow = __builtin_amdgcn_ballot_w64(mx > m[b] + kRescaleThreshold) != 0;
-          const float mn = grow ? fmaxf(m[b], mx) : m[b];
-          alpha[b] = (mn == -INFINITY) ? 1.f : fexp2(m[b] - mn);
-          pend[b] = grow;
-          m[b] = mn;
-          const float mu = (mn == -INFINITY) ? 0.f : mn;
-          float rs = 0.f;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float p = fexp2(__builtin_fmaf(sn[b][0][i], P.c2, -mu));
-            sn[b][0][i] = p;
-            rs += p;
-          }
-          rsp[b] = rs;
-          pn[b][0] = pack8(sn[b][0], 0);
-          pn[b][1] = pack8(sn[b][0], 1);
-        }
-      };
-      // second half: exps of keys 32..63, row sums into l, P packed to bf16 fragments
-      auto sm_finish = [&](f32x16 (&sc)[2][2]) {
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const float mu = (m[b] == -INFINITY) ? 0.f : m[b];
-          float rs = rsp[b];
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float p = fexp2(__builtin_fmaf(sc[b][1][i], P.c2, -mu));
-            sc[b][1][i] = p;
-            rs += p;
-          }
-          l[b] += rs;
-          pf[b][0] = pn[b][0];
-          pf[b][1] = pn[b][1];
-          pf[b][2] = pack8(sc[b][1], 0);
-          pf[b][3] = pack8(sc[b][1], 1);
-        }
-      };
-      auto rescale = [&]() {  // O and l of the blocks whose max rose: exactly once, before new terms
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          if (pend[b]) {
-            l[b] *= alpha[b];
-#pragma unroll
-            for (int d = 0; d < ND; ++d) acc[b][d] *= alpha[b];
-            pend[b] = false;
-          }
-        }
-      };
-      auto pv = [&](const char* V) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const char* vb = V + 16 * j * RB;
-          bf16x8 vt[ND];
-#pragma unroll
-          for (int d = 0; d < ND; ++d) vt[d] = tr_frag_at(vb + toa[d], vb + tob[d]);
-#pragma unroll
-          for (int d = 0; d < ND; ++d)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) acc[b][d] = mfma(vt[d], pf[b][j], acc[b][d]);
-        }
-      };
-      // prologue of the pipeline: S(0) and the first half of its softmax
-      qk(smem, sE);
-      mask(0, sE);
-      sm_start(sE);
-      pend[0] = pend[1] = false;  // O and l are still zero
-
-      auto iter = [&](int i, auto buf, auto next_c, f32x16 (&sc)[2][2], f32x16 (&sn)[2][2]) {
-        constexpr int BUF = decltype(buf)::value;  // LDS stage of tile i (and of K(i+2))
-        constexpr bool NEXT = decltype(next_c)::value;
-        // K(i+2) over K(i) (read in the previous iteration), V(i+1) over V(i-1): both slots free
-        if (i + 2 <= F && i + 2 < ntiles)
-          KV::issue(kbase + (int64_t)(i + 2) * kFwdBK * P.sk, P.sk, seqlen - (i + 2) * kFwdBK, smem + BUF * 2 * TILE);
-        if (i + 1 < ntiles)
-          KV::issue(vbase + (int64_t)(i + 1) * kFwdBK * P.sv, P.sv, seqlen - (i + 1) * kFwdBK,
-                    smem + (1 - BUF) * 2 * TILE + TILE);
-        rescale();
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (NEXT) qk(smem + (1 - BUF) * 2 * TILE, sn);  // K(i+1)
-        sm_finish(sc);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (NEXT) mask(i + 1, sn);
-        __builtin_amdgcn_sched_barrier(0);
-        pv(smem + BUF * 2 * TILE + TILE);  // V(i)
-        if constexpr (NEXT) sm_start(sn);
-        __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();  // drains this wave's DMAs (vmcnt) and orders every wave's reads before reuse
-      };
-      using I0 = std::integral_constant<int, 0>;
-      using I1 = std::integral_constant<int, 1>;
-      using BT = std::integral_constant<bool, true>;
-      using BF = std::integral_constant<bool, false>;
-      int i = 0;
-      for (; i + 2 < F; i += 2) {
-        iter(i, I0{}, BT{}, sE, sO);
-        iter(i + 1, I1{}, BT{}, sO, sE);
-      }
-      if (F - i == 2) {
-        iter(i, I0{}, BT{}, sE, sO);
-        iter(i + 1, I1{}, BF{}, sO, sE);
-      } else {
-        iter(i, I0{}, BF{}, sE, sO);
-      }
-
-      // the causal diagonal: fwd64's step (blocks stop at different tiles)
-      auto tile_step = [&](int t, auto buf, auto both_c) {
-        constexpr int BUF = decltype(buf)::value;
-        constexpr bool BOTH = decltype(both_c)::value;
-        constexpr int B0 = BOTH ? 0 : 1;
-        const int kt0 = t * kFwdBK;
-        if (t + 1 < ntiles) {  // both slots of the other stage were last read by step t - 1
-          const int nk = kt0 + kFwdBK;
-          char* nb = smem + (1 - BUF) * 2 * TILE;
-          KV::issue(kbase + (int64_t)nk * P.sk, P.sk, seqlen - nk, nb);
-          KV::issue(vbase + (int64_t)nk * P.sv, P.sv, seqlen - nk, nb + TILE);
-        }
-        const char* K = smem + BUF * 2 * TILE;
-        const char* V = K + TILE;
-        f32x16 s[2][2];
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-          for (int b = B0; b < 2; ++b) s[b][kt] = f32x16{};
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            const bf16x8 kf = lds_frag(K + kt * 32 * RB + koff[c]);
-#pragma unroll
-            for (int b = B0; b < 2; ++b) s[b][kt] = mfma(kf, lds_frag(qrow[b] + koff[c]), s[b][kt]);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int b = B0; b < 2; ++b) {
-          const int wq0 = b ? qbb : qa;
-          if ((CAUSAL && kt0 + kFwdBK - 1 > wq0) || kt0 + kFwdBK > seqlen) {
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-              const int lim = (CAUSAL ? min(row[b], seqlen - 1) : seqlen - 1) - (kt0 + 32 * kt + 4 * h);
-#pragma unroll
-              for (int q = 0; q < 16; ++q) s[b][kt][q] = acc_row0(q) > lim ? -INFINITY : s[b][kt][q];
-            }
-          }
-          float mx = s[b][0][0];
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) mx = fmaxf(mx, s[b][kt][q]);
-          mx = pair_max(mx) * P.c2;
-          if (__builtin_amdgcn_ballot_w64(mx > m[b] + kRescaleThreshold) != 0) {
-            const float mn = fmaxf(m[b], mx);
-            const float al = (mn == -INFINITY) ? 1.f : fexp2(m[b] - mn);
-            l[b] *= al;
-#pragma unroll
-            for (int d = 0; d < ND; ++d) acc[b][d] *= al;
-            m[b] = mn;
-          }
-          const float mu = (m[b] == -INFINITY) ? 0.f : m[b];
-          float rs = 0.f;
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-              const float p = fexp2(__builtin_fmaf(s[b][kt][q], P.c2, -mu));
-              s[b][kt][q] = p;
-              rs += p;
-            }
-          l[b] += rs;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pf[b][j] = pack8(s[b][j >> 1], j & 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const char* vb = V + 16 * j * RB;
-          bf16x8 vt[ND];
-#pragma unroll
-          for (int d = 0; d < ND; ++d) vt[d] = tr_frag_at(vb + toa[d], vb + tob[d]);
-#pragma unroll
-          for (int d = 0; d < ND; ++d)
-#pragma unroll
-            for (int b = B0; b < 2; ++b) acc[b][d] = mfma(vt[d], pf[b][j], acc[b][d]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
-      };
-      for (int t = F; t < ntiles; ++t) {
-        const bool both = t <= lastA;
-        if (t & 1) {
-          if (both) tile_step(t, I1{}, BT{}); else tile_step(t, I1{}, BF{});
-        } else {
-          if (both) tile_step(t, I0{}, BT{}); else tile_step(t, I0{}, BF{});
-        }
-      }
-
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const float lt = pair_sum(l[b]);
-        const float inv = lt > 0.f ? 1.f / lt : 0.f;
-        uint16_t* op = P.o + ((int64_t)(s0 + min(row[b], seqlen - 1)) * P.hq + head) * D;
-        store_rows_wide<ND>(acc[b], inv, op, row[b] < seqlen);
-        if (row[b] < seqlen && h == 0)
-          P.lse[(int64_t)head * P.T + s0 + row[b]] = (lt > 0.f) ? (m[b] + log2f(lt)) * kLn2 : -INFINITY;
-      }
-    }
-    __syncthreads();
-    item = item_sh;
   }
 }
 
@@ -1165,33 +582,9 @@ constexpr int kDqBK = 64;   // keys per K/V tile
 constexpr int kKvBK = 128;  // keys per workgroup (4 waves x 32)
 constexpr int kKvBQ = 32;   // query rows per item
 
-// delta[h, t] = rowsum(dO[t, h, :] * O[t, h, :]) in f32, for the concurrent backward (the dQ
-// and dK/dV kernels both read it, so neither has to run first).  A 256-thread block handles 16
-// consecutive tokens of one head: D/8 lanes per row, 16-byte loads, a D/8-lane shuffle sum and
-// one 64-byte store of the 16 results.
-template <int D>
-__global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ o,
-                                                        float* __restrict__ delta, int64_t T, int hq) {
-  constexpr int NCH = D / 8, ROWS = 256 / NCH;
-  const int head = blockIdx.y;
-  const int r = threadIdx.x / NCH, ch = threadIdx.x % NCH;
-  const int64_t t = (int64_t)blockIdx.x * ROWS + r;
-  float part = 0.f;
-  if (t < T) {
-    const int64_t base = (t * hq + head) * D + ch * 8;
-    const u16x8 a = *reinterpret_cast<const u16x8*>(dout + base);
-    const u16x8 b = *reinterpret_cast<const u16x8*>(o + base);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) part += bf2f(a[j]) * bf2f(b[j]);
-  }
-#pragma unroll
-  for (int x = 1; x < NCH; x <<= 1) part += __shfl_xor(part, x, 64);
-  if (ch == 0 && t < T) delta[(int64_t)head * T + t] = part;
-}
-
 // dQ = scale * sum_keys dS K, query-stationary (the forward's structure).  Also writes
 // delta = rowsum(dO * O) for its rows, which bwd_dkdv_kernel (launched after it) reads.
-template <int D, bool CAUSAL, int OCC, bool WIN = false, bool PRE_DELTA = false, bool DROP = false>
+template <int D, bool CAUSAL, int OCC, bool WIN = false, bool DROP = false>
 __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
   [[maybe_unused]] const DropCfg dcfg = DROP ? resolve_drop(P.drop) : P.drop;
   constexpr int RB = 2 * D;
@@ -1243,10 +636,10 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
     const int64_t srow = (int64_t)(s0 + q0);
     sq.load(P.q + srow * P.sq + (int64_t)head * D, P.sq, seqlen - q0);
     sdo.load(P.dout + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
-    if constexpr (!PRE_DELTA) so.load(P.o + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
+    so.load(P.o + (srow * P.hq + head) * D, (int64_t)P.hq * D, seqlen - q0);
     sk.load(kbase + (int64_t)t_begin * kDqBK * P.sk, P.sk, klen - t_begin * kDqBK);
     sv.load(vbase + (int64_t)t_begin * kDqBK * P.sv, P.sv, klen - t_begin * kDqBK);
-    if constexpr (!PRE_DELTA) {
+    {
       constexpr int NCH = D / 8, RSTEP = 256 / NCH, PER = kDqBQ / RSTEP;
       const int row0 = threadIdx.x / NCH, ch = threadIdx.x % NCH;
 #pragma unroll
@@ -1267,13 +660,10 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdParams P) {
       qf[c] = lds_frag(smem + 32 * w * RB + koff[c]);
       dof[c] = lds_frag(smem + QIMG + 32 * w * RB + koff[c]);
     }
-    if constexpr (PRE_DELTA) delta = qok ? P.delta[(int64_t)head * P.T + s0 + qrow] : 0.f;
-    else delta = rowd[32 * w + r];
+    delta = rowd[32 * w + r];
     __syncthreads();  // every wave holds its fragments before tile 0 overwrites the images
   }
-  if constexpr (!PRE_DELTA) {
-    if (qok && h == 0) P.delta[(int64_t)head * P.T + s0 + qrow] = delta;
-  }
+  if (qok && h == 0) P.delta[(int64_t)head * P.T + s0 + qrow] = delta;
   const float lse2 = qok ? P.lse[(int64_t)head * P.T + s0 + qrow] * kLog2e : 0.f;
 
   f32x16 acc[ND];
@@ -1779,12 +1169,46 @@ static fa::DropCfg make_drop(double p, int64_t seed, int64_t offset) {
   DTG_CHECK(p >= 0.0 && p < 1.0, "flash_attn dropout: p must be in [0, 1)");
   fa::DropCfg d{};
   d.k0 = (uint32_t)((uint64_t)seed & 0xffffffffu);
-  d.k1 = (uint32_t)((uint64_t)seed >> 32);
+  d.k1 = (uint32_t)((uint64_t)seed >> 32) ^ (uint32_t)((uint64_t)offset >> 32);
   d.off = (uint32_t)((uint64_t)offset & 0xffffffffu);
   d.thr = (int)std::lround((1.0 - p) * 256.0);
   d.thr = std::max(1, std::min(256, d.thr));
   d.scale = 256.f / (float)d.thr;
   return d;
+}
+
+// Launch tuning of the backward kernels, read ONCE from the environment when the extension loads
+// (DTG_FA_KV_SPLIT = N: dK/dV query-item split, 0 = auto; DTG_FA_KV_QB = 32 | 64: dK/dV query
+// rows per item; DTG_FA_OCC = 1 | 2: dQ waves per SIMD at head_dim 128; DTG_FA_KV_PF = 1 | 2:
+// dK/dV items staged ahead) -- never per launch.  Tests and A/B tools change them in-process with
+// the `flash_attn_tuning` op (dtg.ops.fa_tuning).
+struct Tuning {
+  int kv_split, kv_qb, dq_occ, kv_pf;
+};
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return (e != nullptr && e[0] != 0) ? std::atoi(e) : dflt;
+}
+static Tuning& tuning_slot() {
+  static Tuning t{std::max(0, env_int("DTG_FA_KV_SPLIT", 0)), env_int("DTG_FA_KV_QB", 64) == 32 ? 32 : 64,
+                  env_int("DTG_FA_OCC", 1) == 2 ? 2 : 1, env_int("DTG_FA_KV_PF", 1) == 2 ? 2 : 1};
+  return t;
+}
+static const Tuning& tuning() { return tuning_slot(); }
+static const bool kTuningLoaded = (tuning_slot(), true);  // at library load
+
+// (kv_split, kv_qb) -> the previous values; a negative argument leaves that knob unchanged.
+std::vector<int64_t> flash_attn_tuning(const at::Tensor& like, int64_t kv_split, int64_t kv_qb) {
+  (void)like;
+  (void)kTuningLoaded;
+  Tuning& t = tuning_slot();
+  std::vector<int64_t> old{t.kv_split, t.kv_qb};
+  if (kv_split >= 0) t.kv_split = (int)kv_split;
+  if (kv_qb >= 0) {
+    DTG_CHECK(kv_qb == 32 || kv_qb == 64, "flash_attn_tuning: kv_qb must be 32 or 64");
+    t.kv_qb = (int)kv_qb;
+  }
+  return old;
 }
 
 // Dynamic LDS above 64 KiB must be opted into per kernel (MI355X: 160 KiB per CU).
@@ -1844,66 +1268,19 @@ static std::tuple<at::Tensor, at::Tensor> flash_attn_fwd_impl(const at::Tensor& 
     *stamps = at::zeros({(int64_t)grid.x * grid.y * grid.z, 6}, q.options().dtype(at::kLong));
     P.stamps = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
   }
-  // DTG_FA_FWD=narrow: the round-1 row-per-lane dwordx2 epilogue (read per call: same-process A/B)
-  // DTG_FA_FWD=wide: row-per-lane Q fragment loads instead of the LDS-staged Q
-  const char* variant = std::getenv("DTG_FA_FWD");
-  const bool wide = !(variant != nullptr && variant[0] == 'n');
-  const bool qlds = !(variant != nullptr && (variant[0] == 'n' || variant[0] == 'w'));
-  // DTG_FA_FWD=f64: the one-wave-per-SIMD persistent kernel (fwd64_kernel); plain causal /
-  // non-causal self-attention only (no window, key ranges, dropout or stamps)
-  const bool f64 = variant != nullptr && (variant[0] == 'f' || variant[0] == 'p');
-  if (f64 && drop == nullptr && P.window == 0 && P.kstart == nullptr && stamps == nullptr) {
-    const int nqb64 = (int)((max_seqlen + fa::kF64Rows - 1) / fa::kF64Rows);
-    const int64_t nitems = (int64_t)nqb64 * nseq * hq;
-    DTG_CHECK(nitems < (1ll << 31), "flash_attn: too many work items");
-    auto queue = at::zeros({1}, q.options().dtype(at::kInt));
-    int ncu = 0;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, q.device().index());
-    ncu = std::max(ncu, 1);
-    const int grid64 = (int)std::min<int64_t>(nitems, ncu);
-    const size_t lds64 = 4 * fa::kFwdBK * D * 2 + fa::kF64Rows * D * 2;
-#define DTG_FWD64(DD, C)                                                                                    \
-  do { set_lds_limit((const void*)&fa::fwd64_kernel<DD, C>, lds64);                                        \
-       hipLaunchKernelGGL((fa::fwd64_kernel<DD, C>), dim3(grid64), dim3(256), lds64, stream(), P,           \
-                          queue.data_ptr<int>(), nqb64, nseq); } while (0)
-#define DTG_FWD64P(DD, C)                                                                                   \
-  do { set_lds_limit((const void*)&fa::fwd64p_kernel<DD, C>, lds64);                                       \
-       hipLaunchKernelGGL((fa::fwd64p_kernel<DD, C>), dim3(grid64), dim3(256), lds64, stream(), P,          \
-                          queue.data_ptr<int>(), nqb64, nseq); } while (0)
-    if (variant[0] == 'p') {
-      if (D == 128) { if (causal) DTG_FWD64P(128, true); else DTG_FWD64P(128, false); }
-      else { if (causal) DTG_FWD64P(64, true); else DTG_FWD64P(64, false); }
-    } else if (D == 128) { if (causal) DTG_FWD64(128, true); else DTG_FWD64(128, false); }
-    else { if (causal) DTG_FWD64(64, true); else DTG_FWD64(64, false); }
-#undef DTG_FWD64P
-#undef DTG_FWD64
-    DTG_LAUNCH_CHECK();
-    return {o, lse};
-  }
   const size_t lds = 4 * fa::kFwdBK * D * 2;
-#define DTG_FWD(DD, C, W, Q)                                                              \
-  do { set_lds_limit((const void*)&fa::fwd_kernel<DD, C, W, Q>, lds);                        \
-       hipLaunchKernelGGL((fa::fwd_kernel<DD, C, W, Q>), grid, dim3(256), lds, stream(), P); } while (0)
-#define DTG_FWD_W(DD, C)                                                                  \
-  do { if (!wide) DTG_FWD(DD, C, false, false); else if (!qlds) DTG_FWD(DD, C, true, false);   \
-       else DTG_FWD(DD, C, true, true); } while (0)
+#define DTG_FWD(DD, C, ...)                                                               \
+  do { set_lds_limit((const void*)&fa::fwd_kernel<DD, C, ##__VA_ARGS__>, lds);               \
+       hipLaunchKernelGGL((fa::fwd_kernel<DD, C, ##__VA_ARGS__>), grid, dim3(256), lds, stream(), P); } while (0)
   if (drop != nullptr) {  // attention dropout: the default variant's DROP instantiation
     DTG_CHECK(P.window == 0 && P.kstart == nullptr, "flash_attn dropout: no sliding window / key ranges");
     P.drop = *drop;
-#define DTG_FWD_DROP(DD, C)                                                                           \
-  do { set_lds_limit((const void*)&fa::fwd_kernel<DD, C, true, true, false, true>, lds);                 \
-       hipLaunchKernelGGL((fa::fwd_kernel<DD, C, true, true, false, true>), grid, dim3(256), lds, stream(), P); } while (0)
-    if (D == 128) { if (causal) DTG_FWD_DROP(128, true); else DTG_FWD_DROP(128, false); }
-    else { if (causal) DTG_FWD_DROP(64, true); else DTG_FWD_DROP(64, false); }
-#undef DTG_FWD_DROP
-  } else if (P.window > 0) {  // sliding window (causal only): the WIN instantiation of the default variant
-    if (D == 128) { set_lds_limit((const void*)&fa::fwd_kernel<128, true, true, true, true>, lds);
-                    hipLaunchKernelGGL((fa::fwd_kernel<128, true, true, true, true>), grid, dim3(256), lds, stream(), P); }
-    else { set_lds_limit((const void*)&fa::fwd_kernel<64, true, true, true, true>, lds);
-           hipLaunchKernelGGL((fa::fwd_kernel<64, true, true, true, true>), grid, dim3(256), lds, stream(), P); }
-  } else if (D == 128) { if (causal) DTG_FWD_W(128, true); else DTG_FWD_W(128, false); }
-  else { if (causal) DTG_FWD_W(64, true); else DTG_FWD_W(64, false); }
-#undef DTG_FWD_W
+    if (D == 128) { if (causal) DTG_FWD(128, true, false, true); else DTG_FWD(128, false, false, true); }
+    else { if (causal) DTG_FWD(64, true, false, true); else DTG_FWD(64, false, false, true); }
+  } else if (P.window > 0) {  // sliding window (causal only): the WIN instantiation
+    if (D == 128) DTG_FWD(128, true, true); else DTG_FWD(64, true, true);
+  } else if (D == 128) { if (causal) DTG_FWD(128, true); else DTG_FWD(128, false); }
+  else { if (causal) DTG_FWD(64, true); else DTG_FWD(64, false); }
 #undef DTG_FWD
   DTG_LAUNCH_CHECK();
   return {o, lse};
@@ -1927,7 +1304,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_fwd_stamped(const at::
 }
 
 static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen, int64_t hq, int nseq,
-                          hipStream_t st, bool pre_delta, bool drop = false);
+                          hipStream_t st, bool drop = false);
 static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max_seqlen_k, int64_t hkv,
                             int nseq, hipStream_t st, const at::Tensor& dk_t, const at::Tensor& dv_t, bool drop = false);
 
@@ -1995,51 +1372,19 @@ static void flash_attn_bwd_impl(const at::Tensor& dout_, const at::Tensor& q, co
   if (drop != nullptr) {
     DTG_CHECK(P.window == 0 && P.kstart == nullptr, "flash_attn dropout: no sliding window / key ranges");
     P.drop = *drop;
-    launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, stream(), false, true);
+    launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, stream(), true);
     launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, stream(), dk, dv, true);
     return;
   }
-  // Concurrent backward (DTG_FA_BWD_CONC=1; off by default): delta comes from its own small
-  // kernel, then the dQ kernel runs on a side stream WHILE the dK/dV kernel runs on the
-  // caller's stream, co-resident on every CU (99 KB of LDS for the pair).  The idea: each alone
-  // keeps one wave per SIMD with its MFMA pipe busy a quarter to a third of the time, so one
-  // kernel's softmax work could issue under the other's MFMAs.  Measured on MI355X
-  // (profiles/r3_s04): SLOWER -- 8B shape 0.737 -> 0.803 ms, rime 0.320 -> 0.342, 2 x 8192
-  // 4.22 -> 4.40 -- the pair contends for LDS bandwidth and L2 more than it gains in issue
-  // overlap; kept as an option, not the default.
-  const char* conc_env = std::getenv("DTG_FA_BWD_CONC");  // per call: tests switch it in-process
-  const bool conc = conc_env != nullptr && conc_env[0] == '1';
-  const bool concurrent = conc && P.window == 0;
-  hipStream_t main_st = stream(), dq_st = main_st;
-  if (concurrent) {
-    dim3 dgrid((T + 256 / (D / 8) - 1) / (256 / (D / 8)), hq);
-    if (D == 128) fa::bwd_delta_kernel<128><<<dgrid, 256, 0, main_st>>>(bf16_ptr(dout), bf16_ptr(o), P.delta, T, (int)hq);
-    else fa::bwd_delta_kernel<64><<<dgrid, 256, 0, main_st>>>(bf16_ptr(dout), bf16_ptr(o), P.delta, T, (int)hq);
-    DTG_LAUNCH_CHECK();
-    static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    if (ev_fork == nullptr) {
-      DTG_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess, "flash_attn: event");
-      DTG_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess, "flash_attn: event");
-    }
-    dq_st = c10::hip::getStreamFromPool(false, q.device().index()).stream();
-    DTG_CHECK(hipEventRecord(ev_fork, main_st) == hipSuccess, "flash_attn: event record");
-    DTG_CHECK(hipStreamWaitEvent(dq_st, ev_fork, 0) == hipSuccess, "flash_attn: stream wait");
-    launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, dq_st, true);
-    launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, main_st, dk, dv);
-    DTG_CHECK(hipEventRecord(ev_join, dq_st) == hipSuccess, "flash_attn: event record");
-    DTG_CHECK(hipStreamWaitEvent(main_st, ev_join, 0) == hipSuccess, "flash_attn: stream wait");
-    return;
-  }
-  launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, main_st, false);
-  launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, main_st, dk, dv);
+  // (A concurrent form -- dQ on a side stream while dK/dV runs -- was slower at every shape:
+  // the pair contends for LDS bandwidth and L2, profiles/r3_s04; removed in round 6.)
+  launch_bwd_dq(P, D, causal, max_seqlen, hq, nseq, stream());
+  launch_bwd_dkdv(P, D, causal, max_seqlen_k, hkv, nseq, stream(), dk, dv);
 }
 
 static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_t max_seqlen, int64_t hq, int nseq,
-                          hipStream_t st, bool pre_delta, bool drop) {
-  static const int occ = [] {  // waves per SIMD of the dq kernel at head_dim 128 (DTG_FA_OCC=1|2)
-    const char* e = std::getenv("DTG_FA_OCC");
-    return (e != nullptr && e[0] == '2') ? 2 : 1;
-  }();
+                          hipStream_t st, bool drop) {
+  const int occ = tuning().dq_occ;
   {
     dim3 grid(hq, nseq, (max_seqlen + fa::kDqBQ - 1) / fa::kDqBQ);
     const size_t lds = 4 * fa::kDqBK * D * 2 + fa::kDqBQ * 4;  // + the per-row delta
@@ -2047,13 +1392,10 @@ static void launch_bwd_dq(const fa::BwdParams& P, int64_t D, bool causal, int64_
   do { set_lds_limit((const void*)&fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>, lds);         \
        hipLaunchKernelGGL((fa::bwd_dq_kernel<DD, C, O, ##__VA_ARGS__>), grid, dim3(256), lds, st, P); } while (0)
     if (drop) {  // attention dropout (no window, delta computed here)
-      if (D == 128) { if (causal) DTG_BWD_DQ(128, true, 1, false, false, true); else DTG_BWD_DQ(128, false, 1, false, false, true); }
-      else { if (causal) DTG_BWD_DQ(64, true, 2, false, false, true); else DTG_BWD_DQ(64, false, 2, false, false, true); }
-    } else if (P.window > 0) {  // sliding window (causal only)
-      if (D == 128) DTG_BWD_DQ(128, true, 1, true); else DTG_BWD_DQ(64, true, 2, true);
-    } else if (pre_delta) {
       if (D == 128) { if (causal) DTG_BWD_DQ(128, true, 1, false, true); else DTG_BWD_DQ(128, false, 1, false, true); }
       else { if (causal) DTG_BWD_DQ(64, true, 2, false, true); else DTG_BWD_DQ(64, false, 2, false, true); }
+    } else if (P.window > 0) {  // sliding window (causal only)
+      if (D == 128) DTG_BWD_DQ(128, true, 1, true); else DTG_BWD_DQ(64, true, 2, true);
     } else if (D == 128) {
       if (occ == 2) { if (causal) DTG_BWD_DQ(128, true, 2); else DTG_BWD_DQ(128, false, 2); }
       else { if (causal) DTG_BWD_DQ(128, true, 1); else DTG_BWD_DQ(128, false, 1); }
@@ -2068,19 +1410,16 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
   // Items the dK/dV kernel stages ahead (DTG_FA_KV_PF=1|2).  Equal on MI355X once the kernel's
   // false vmcnt waits were gone (bwd 0.767 vs 0.768 ms at the 8B shape, profiles/r1_s51_*), so
   // the single-set form with fewer registers is the default.
-  static const int kv_pf = [] {
-    const char* e = std::getenv("DTG_FA_KV_PF");
-    return (e != nullptr && e[0] == '2') ? 2 : 1;
-  }();
+  const Tuning tn = tuning();
+  const int kv_pf = tn.kv_pf;
   // Split the query items of each key block over several workgroups when the grid cannot fill
   // the chip (e.g. TP = 8: one KV head per rank -> 16 x 8 workgroups for 256 CUs): aim for
-  // >= 2 workgroups per CU.  DTG_FA_KV_SPLIT = N forces N (1 = off); read per call (A/B).
+  // >= 2 workgroups per CU.  Tuning::kv_split = N forces N (1 = off).
   const int nkb = (int)((max_seqlen_k + fa::kKvBK - 1) / fa::kKvBK);
   const int64_t wgs = (int64_t)hkv * nseq * nkb;
   const int kv_pf_eff = drop ? 1 : kv_pf;  // dropout: the single-set, 64-row-item instantiation
   int nsplit = 1;
-  const char* se = std::getenv("DTG_FA_KV_SPLIT");
-  if (se != nullptr && std::atoi(se) > 0) nsplit = std::min(8, std::atoi(se));
+  if (tn.kv_split > 0) nsplit = std::min(8, tn.kv_split);
   else if (wgs > 0 && wgs < 512) nsplit = (int)std::min<int64_t>(4, (512 + wgs - 1) / wgs);
   at::Tensor dk_part, dv_part;
   if (nsplit > 1 && P.kstart == nullptr && P.window == 0 && kv_pf_eff == 1) {
@@ -2095,11 +1434,10 @@ static void launch_bwd_dkdv(fa::BwdParams P, int64_t D, bool causal, int64_t max
   }
   {
     dim3 grid(hkv, nseq, nkb * nsplit);
-    // DTG_FA_KV_QB = 32 | 64: query rows per item; per call (A/B).  64 (the two-half software
-    // pipeline) is the default: backward 2-4 % faster on every benchmarked shape, -1.9 ms per 8B
-    // step (profiles/r3_s39).  Sliding windows and the two-item prefetch keep 32.
-    const char* qe = std::getenv("DTG_FA_KV_QB");
-    const int qb = drop || ((qe == nullptr || std::atoi(qe) != 32) && P.window == 0 && kv_pf == 1) ? 64 : 32;
+    // Tuning::kv_qb = 32 | 64: query rows per item.  64 (the two-half software pipeline) is the
+    // default: backward 2-4 % faster on every benchmarked shape, -1.9 ms per 8B step
+    // (profiles/r3_s39).  Sliding windows and the two-item prefetch keep 32.
+    const int qb = drop || (tn.kv_qb != 32 && P.window == 0 && kv_pf == 1) ? 64 : 32;
     const size_t lds = 4 * (size_t)qb * D * 2 + 2 * 2 * qb * 4;
 #define DTG_BWD_KV(DD, C, PF, ...)                                                        \
   do { set_lds_limit((const void*)&fa::bwd_dkdv_kernel<DD, C, PF, ##__VA_ARGS__>, lds);      \
@@ -2304,6 +1642,7 @@ TORCH_LIBRARY_IMPL(dtg, CUDA, m) {
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("flash_attn_bwd_qkv", &flash_attn_bwd_qkv);
   m.impl("flash_attn_bwd_qkv_rope", &flash_attn_bwd_qkv_rope);
+  m.impl("flash_attn_tuning", &flash_attn_tuning);
 }
 
 }  // namespace dtg

@@ -31,7 +31,25 @@ from .functional import (  # noqa: E402
 from .grad_routing import route_param_grad  # noqa: E402
 from .adamw import adamw_step  # noqa: E402
 
+import contextlib as _contextlib  # noqa: E402
+
+import torch as _torch  # noqa: E402
+
+
+@_contextlib.contextmanager
+def fa_tuning(device="cuda", kv_split: int = -1, kv_qb: int = -1):
+    """Set the flash-attention backward's launch tuning (dK/dV query-item split, 0 = auto; dK/dV
+    query rows per item, 32 | 64) for the duration of the block.  The kernels read these from
+    DTG_FA_KV_SPLIT / DTG_FA_KV_QB once, when the extension loads, never per launch."""
+    like = _torch.empty(0, device=device)
+    old = _torch.ops.dtg.flash_attn_tuning(like, kv_split, kv_qb)
+    try:
+        yield
+    finally:
+        _torch.ops.dtg.flash_attn_tuning(like, old[0], old[1])
+
 __all__ = [
     "add_rms_norm", "attention", "rope", "embedding", "fused_linear_cross_entropy", "linear", "rms_norm",
     "rope_tables", "swiglu", "swiglu_mlp", "vocab_parallel_fused_linear_cross_entropy", "route_param_grad", "adamw_step",
+    "fa_tuning",
 ]

@@ -239,15 +239,18 @@ def dropout_threshold(p):
 def dropout_keep(seed, offset, head, s0, nq, nk, p):
     """bool [nq, nk]: the keep decision of (query q, key k) of the sequence starting at token s0
     (sequence-relative q, k) for query head `head` -- byte (k & 3) of word (q & 3) of
-    Philox4x32-10({k & ~3, s0 + (q & ~3), head, offset}, seed)."""
+    Philox4x32-10({k & ~3, s0 + (q & ~3), head, offset lo}, key = {seed lo, seed hi ^ offset hi}).
+    The offset's high word goes into the key, so offsets past 2^32 (long runs draw 4 per call)
+    never repeat an earlier mask."""
     import numpy as np
 
     thr, _ = dropout_threshold(p)
     q = np.arange(nq, dtype=np.uint64)[:, None]
     k = np.arange(nk, dtype=np.uint64)[None, :]
     seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    offset = int(offset) & 0xFFFFFFFFFFFFFFFF
     w = philox4x32_10(k & ~np.uint64(3), np.uint64(s0) + (q & ~np.uint64(3)), np.full_like(q, head),
-                      np.full_like(q, int(offset) & 0xFFFFFFFF), seed & 0xFFFFFFFF, seed >> 32)
+                      np.full_like(q, offset & 0xFFFFFFFF), seed & 0xFFFFFFFF, (seed >> 32) ^ (offset >> 32))
     sel = (q & np.uint64(3)).astype(np.int64)
     word = np.choose(np.broadcast_to(sel, (nq, nk)), [np.broadcast_to(x, (nq, nk)) for x in w])
     byte = (word >> (np.uint64(8) * (k & np.uint64(3)))) & np.uint64(255)
@@ -434,12 +437,25 @@ def embedding_bwd_(out, ids, dy):
     out.copy_((out.float() + acc).to(out.dtype))
 
 
+_TUNING = [0, 64]
+
+
+def flash_attn_tuning(like, kv_split, kv_qb):
+    """CPU: the reference attention has no launch tuning; the knobs are only remembered."""
+    old = list(_TUNING)
+    if kv_split >= 0:
+        _TUNING[0] = int(kv_split)
+    if kv_qb >= 0:
+        _TUNING[1] = int(kv_qb)
+    return old
+
+
 for _name, _fn in list(globals().items()):
     if _name in (
         "rmsnorm_fwd", "add_rmsnorm_fwd", "rmsnorm_bwd", "rope_", "swiglu_fwd", "swiglu_bwd",
         "ce_fwd_bwd_", "ce_stats", "ce_grad_", "adamw_", "adamw_t_", "flash_attn_fwd", "flash_attn_bwd",
         "flash_attn_bwd_qkv", "transpose2d", "transpose_mats_", "swiglu_bwd_t", "embedding_bwd_", "flash_attn_varlen_fwd",
         "flash_attn_varlen_bwd", "flash_attn_fwd_drop", "flash_attn_bwd_drop", "flash_attn_bwd_qkv_drop", "philox_rng",
-        "flash_attn_bwd_qkv_rope",
+        "flash_attn_bwd_qkv_rope", "flash_attn_tuning",
     ):
         LIB.impl(_name, _fn, "CPU")

@@ -64,6 +64,9 @@ _DEFS = [
     "-> (Tensor, Tensor, Tensor)",
     "flash_attn_fwd_stamped(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
     "bool causal) -> (Tensor, Tensor, Tensor)",
+    # backward launch tuning (read once from DTG_FA_* at load): set (kv_split, kv_qb), a negative
+    # value keeps a knob; returns the previous pair.  `like` picks the device's implementation.
+    "flash_attn_tuning(Tensor like, int kv_split, int kv_qb) -> int[]",
 ]
 
 for _d in _DEFS:

@@ -21,23 +21,25 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
-@pytest.mark.parametrize("D,hq,hkv,causal,docs,split,window,conc", [
-    (128, 8, 2, True, [0, 512], "1", 0, "0"),
-    (128, 8, 2, True, [0, 200, 384, 512], "1", 0, "0"),
-    (128, 4, 1, False, [0, 256, 512], "1", 0, "0"),
-    (64, 6, 2, True, [0, 300, 512], "1", 0, "0"),
-    (128, 4, 1, True, [0, 512], "2", 0, "0"),
-    # sliding window (Mistral) and the concurrent dQ / dK-dV backward go through the same epilogues
-    (128, 8, 2, True, [0, 512], "1", 128, "0"),
-    (64, 6, 2, True, [0, 300, 512], "1", 100, "1"),
-    (128, 8, 2, True, [0, 200, 384, 512], "1", 0, "1"),
+@pytest.mark.parametrize("D,hq,hkv,causal,docs,split,window", [
+    (128, 8, 2, True, [0, 512], 1, 0),
+    (128, 8, 2, True, [0, 200, 384, 512], 1, 0),
+    (128, 4, 1, False, [0, 256, 512], 1, 0),
+    (64, 6, 2, True, [0, 300, 512], 1, 0),
+    (128, 4, 1, True, [0, 512], 2, 0),
+    # sliding window (Mistral) goes through the same epilogues
+    (128, 8, 2, True, [0, 512], 1, 128),
+    (64, 6, 2, True, [0, 300, 512], 1, 100),
 ])
-def test_fused_rope_bwd_matches_separate_pass(cuda, monkeypatch, D, hq, hkv, causal, docs, split, window, conc):
-    import dtg.ops  # noqa: F401
+def test_fused_rope_bwd_matches_separate_pass(cuda, D, hq, hkv, causal, docs, split, window):
+    import dtg.ops
 
+    with dtg.ops.fa_tuning(cuda, kv_split=split):
+        _fused_case(cuda, D, hq, hkv, causal, docs, window)
+
+
+def _fused_case(cuda, D, hq, hkv, causal, docs, window):
     ops = torch.ops.dtg
-    monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
-    monkeypatch.setenv("DTG_FA_BWD_CONC", conc)
     torch.manual_seed(0)
     T = docs[-1]
     cu = torch.tensor(docs, dtype=torch.int32, device=cuda)

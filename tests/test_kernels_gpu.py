@@ -390,16 +390,24 @@ def test_flash_attn_dropout_matches_masked_reference(cuda, D, hq, hkv, seqlens, 
     _close(o, o_ref, 3e-2, 2e-2, "attn out (dropout)")
     _close(lse, lse_ref, 2e-3, 1e-3, "lse")
     ref = dops.flash_attn_bwd_drop(do, q, k, v, o_ref, lse_ref, cu, max(seqlens), scale, causal, p, rng)
-    for split in ("1", "3"):
-        monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
-        got = dops.flash_attn_bwd_drop(do.to(cuda), q.to(cuda), k.to(cuda), v.to(cuda), o, lse, cu.to(cuda),
-                                       max(seqlens), scale, causal, p, rng.to(cuda))
+    for split in (1, 3):
+        with ops.fa_tuning(cuda, kv_split=split):
+            got = dops.flash_attn_bwd_drop(do.to(cuda), q.to(cuda), k.to(cuda), v.to(cuda), o, lse, cu.to(cuda),
+                                           max(seqlens), scale, causal, p, rng.to(cuda))
         for a, b, n in zip(got, ref, ("dq", "dk", "dv")):
             assert _rel(a, b) < 2e-2, f"{n} (split {split}) rel err {_rel(a, b)}"
     # another offset is another mask
     o2, _ = dops.flash_attn_fwd_drop(q.to(cuda), k.to(cuda), v.to(cuda), cu.to(cuda), max(seqlens), scale, causal, p,
                                      torch.tensor([seed, off + 1], dtype=torch.int64, device=cuda))
     assert _rel(o2, o_ref) > 5e-2
+    # an offset past 2^32 keys the generator with its high word: the same mask as the CPU
+    # reference, and not the mask of its low word alone
+    big = torch.tensor([seed, off + (1 << 32)], dtype=torch.int64)
+    o3_ref, _ = dops.flash_attn_fwd_drop(q, k, v, cu, max(seqlens), scale, causal, p, big)
+    o3, _ = dops.flash_attn_fwd_drop(q.to(cuda), k.to(cuda), v.to(cuda), cu.to(cuda), max(seqlens), scale, causal, p,
+                                     big.to(cuda))
+    _close(o3, o3_ref, 3e-2, 2e-2, "attn out (dropout, offset >= 2^32)")
+    assert _rel(o3, o_ref) > 5e-2
 
 
 def test_gpt2_trains_through_the_dropout_kernels(cuda):
@@ -437,65 +445,61 @@ def test_flash_attn_d64_mha(cuda, seqlens):
     _attn_case(cuda, seqlens, hq=4, hkv=4, D=64, causal=True)
 
 
-@pytest.mark.parametrize("variant", ["narrow", "wide", "qlds", "f64", "p64"])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_attn_fwd_variants(cuda, variant, causal, monkeypatch):
-    """Every forward variant (DTG_FA_FWD, read per call) against the fp32 reference, including
-    logits with a large dynamic range (qscale 8: the running max keeps growing by more than the
-    lazy-rescale threshold, so the rescale path runs on many tiles)."""
-    monkeypatch.setenv("DTG_FA_FWD", variant)
-    _attn_case(cuda, [100, 257, 667], hq=8, hkv=2, D=128, causal=causal, stride_extra=8)
-    _attn_case(cuda, [512, 300], hq=4, hkv=4, D=64, causal=causal)
+def test_flash_attn_fwd_large_logit_range(cuda, causal):
+    """The forward against the fp32 reference on logits with a large dynamic range (qscale 8:
+    the running max keeps growing by more than the lazy-rescale threshold, so the rescale path
+    runs on many tiles), GQA and MHA, head_dim 128 and 64."""
     _attn_case(cuda, [1024, 77], hq=4, hkv=2, D=128, causal=causal, qscale=8.0)
+    _attn_case(cuda, [512, 300], hq=4, hkv=4, D=64, causal=causal, qscale=8.0)
 
 
-@pytest.mark.parametrize("split", ["1", "2", "4"])
+@pytest.mark.parametrize("split", [1, 2, 4])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_attn_bwd_kv_split(cuda, split, causal, monkeypatch):
+def test_flash_attn_bwd_kv_split(cuda, split, causal):
     """dK/dV with each key block's query items split over workgroups (f32 partials summed in
-    split order, DTG_FA_KV_SPLIT): matches the fp32 reference, is bitwise reproducible, and the
+    split order, kv_split): matches the fp32 reference, is bitwise reproducible, and the
     single-GPU default (no split) is unchanged."""
-    monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
-    qkv, cu = _attn_case(cuda, [1024, 77, 300], hq=8, hkv=2, D=128, causal=causal, stride_extra=8)
-    T, D, hq, hkv = qkv.shape[0], 128, 8, 2
-    g = qkv.to(cuda)
-    q, k, v = (g[:, a * D:b * D].view(T, b - a, D) for a, b in ((0, hq), (hq, hq + hkv), (hq + hkv, hq + 2 * hkv)))
-    o, lse = dops.flash_attn_fwd(q, k, v, cu.to(cuda), 1024, D ** -0.5, causal, 0)
-    torch.manual_seed(3)
-    do = torch.randn(T, hq, D, device=cuda).bfloat16()
-    a = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
-    b = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    with ops.fa_tuning(cuda, kv_split=split):
+        qkv, cu = _attn_case(cuda, [1024, 77, 300], hq=8, hkv=2, D=128, causal=causal, stride_extra=8)
+        T, D, hq, hkv = qkv.shape[0], 128, 8, 2
+        g = qkv.to(cuda)
+        q, k, v = (g[:, a * D:b * D].view(T, b - a, D) for a, b in ((0, hq), (hq, hq + hkv), (hq + hkv, hq + 2 * hkv)))
+        o, lse = dops.flash_attn_fwd(q, k, v, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+        torch.manual_seed(3)
+        do = torch.randn(T, hq, D, device=cuda).bfloat16()
+        a = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+        b = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
-    monkeypatch.setenv("DTG_FA_KV_SPLIT", "1")
-    ref = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+    with ops.fa_tuning(cuda, kv_split=1):
+        ref = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
     assert torch.equal(a[0], ref[0])  # dQ is not affected
     for x, y in zip(a[1:], ref[1:]):
         assert _rel(x, y) < 1e-2
 
 
-@pytest.mark.parametrize("split", ["1", "4"])
+@pytest.mark.parametrize("split", [1, 4])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("D,hq,hkv", [(128, 8, 2), (64, 4, 4)])
-def test_flash_attn_bwd_kv_qb64(cuda, D, hq, hkv, causal, split, monkeypatch):
-    """dK/dV with 64-query items (two-half software pipeline, DTG_FA_KV_QB=64): the fp32
-    reference on varlen sequences whose lengths are not multiples of 64, alone and split; dQ is
-    untouched and dK/dV agree with the 32-row items to summation-order rounding."""
-    monkeypatch.setenv("DTG_FA_KV_SPLIT", split)
-    monkeypatch.setenv("DTG_FA_KV_QB", "64")
-    qkv, cu = _attn_case(cuda, [1024, 77, 300], hq=hq, hkv=hkv, D=D, causal=causal, stride_extra=8)
-    T = qkv.shape[0]
-    g = qkv.to(cuda)
-    q, k, v = (g[:, a * D:b * D].view(T, b - a, D) for a, b in ((0, hq), (hq, hq + hkv), (hq + hkv, hq + 2 * hkv)))
-    o, lse = dops.flash_attn_fwd(q, k, v, cu.to(cuda), 1024, D ** -0.5, causal, 0)
-    torch.manual_seed(3)
-    do = torch.randn(T, hq, D, device=cuda).bfloat16()
-    a = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
-    b = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
-    for x, y in zip(a, b):
-        assert torch.equal(x, y)
-    monkeypatch.setenv("DTG_FA_KV_QB", "32")
-    ref = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+def test_flash_attn_bwd_kv_qb64(cuda, D, hq, hkv, causal, split):
+    """dK/dV with 64-query items (two-half software pipeline, kv_qb 64): the fp32 reference on
+    varlen sequences whose lengths are not multiples of 64, alone and split; dQ is untouched and
+    dK/dV agree with the 32-row items to summation-order rounding."""
+    with ops.fa_tuning(cuda, kv_split=split, kv_qb=64):
+        qkv, cu = _attn_case(cuda, [1024, 77, 300], hq=hq, hkv=hkv, D=D, causal=causal, stride_extra=8)
+        T = qkv.shape[0]
+        g = qkv.to(cuda)
+        q, k, v = (g[:, a * D:b * D].view(T, b - a, D) for a, b in ((0, hq), (hq, hq + hkv), (hq + hkv, hq + 2 * hkv)))
+        o, lse = dops.flash_attn_fwd(q, k, v, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+        torch.manual_seed(3)
+        do = torch.randn(T, hq, D, device=cuda).bfloat16()
+        a = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+        b = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    with ops.fa_tuning(cuda, kv_split=split, kv_qb=32):
+        ref = dops.flash_attn_bwd(do, q, k, v, o, lse, cu.to(cuda), 1024, D ** -0.5, causal, 0)
     assert torch.equal(a[0], ref[0])
     for x, y in zip(a[1:], ref[1:]):
         assert _rel(x, y) < 1e-2

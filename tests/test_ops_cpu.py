@@ -208,3 +208,25 @@ def test_transpose2d_and_tn_weight_grad_routing():
     assert route_weight_grad_mm(p, a, b, a_t=at, b_t=b.t().contiguous()) is None
     assert route_weight_grad_mm(p, a, b) is None  # second contribution accumulates
     torch.testing.assert_close(p.main_grad, 2 * ref)
+
+
+def test_dropout_mask_offset_high_word_is_keyed():
+    """The Philox offset's high word enters the key (ADVICE r5 flash_attn.hip:173): an offset past
+    2^32 gives a new mask instead of repeating the mask of its low word; offsets below 2^32 keep
+    the round-5 masks (key = seed)."""
+    import numpy as np
+
+    from dtg.ops import _cpu
+
+    seed, off = 0x123456789AB, 77
+    a = _cpu.dropout_keep(seed, off, 0, 0, 64, 64, 0.5)
+    b = _cpu.dropout_keep(seed, off + (1 << 32), 0, 0, 64, 64, 0.5)
+    assert not torch.equal(a, b)
+    q = np.arange(64, dtype=np.uint64)[:, None]
+    k = np.arange(64, dtype=np.uint64)[None, :]
+    w = _cpu.philox4x32_10(k & ~np.uint64(3), q & ~np.uint64(3), np.full_like(q, 0), np.full_like(q, off),
+                           seed & 0xFFFFFFFF, seed >> 32)
+    word = np.choose(np.broadcast_to((q & np.uint64(3)).astype(np.int64), (64, 64)),
+                     [np.broadcast_to(x, (64, 64)) for x in w])
+    byte = (word >> (np.uint64(8) * (k & np.uint64(3)))) & np.uint64(255)
+    assert torch.equal(a, torch.from_numpy(byte.astype(np.int64) < _cpu.dropout_threshold(0.5)[0]))

@@ -32,20 +32,16 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--sweep", action="store_true",
                     help="constant 16k tokens, S = 512..8192, causal and non-causal (Hq32/Hkv8/D128)")
-    ap.add_argument("--ab", default=None,
-                    help="comma list of DTG_FA_FWD variants (e.g. v0,v1): forward timed in interleaved "
-                         "rounds in ONE process (same device, same clocks), medians reported")
     ap.add_argument("--ab-bwd", default=None,
-                    help="VAR=v1,v2 (e.g. DTG_FA_OCC=1,2): backward timed under each value of the environment "
-                         "knob in interleaved rounds in ONE process, medians reported, outputs compared bitwise")
+                    help="KNOB=v1,v2 with KNOB kv_split or kv_qb (dtg.ops.fa_tuning): backward timed under "
+                         "each value in interleaved rounds in ONE process (same device, same clocks), medians "
+                         "reported, outputs compared bitwise")
     ap.add_argument("--ab-tolerant", action="store_true",
                     help="--ab-bwd variants that change the summation order: compare within 1e-2 relative")
     a = ap.parse_args()
     if a.ab_bwd:
         var, vals = a.ab_bwd.split("=", 1)
         return ab_bwd(a, var, vals.split(","))
-    if a.ab:
-        return ab(a, a.ab.split(","))
     if a.sweep:
         for S in (512, 1024, 2048, 4096, 8192):
             for causal in (True, False):
@@ -79,42 +75,6 @@ def _inputs(c, causal):
     return q, k, v, cu, maxlen, flops, 1 / math.sqrt(d)
 
 
-def ab(a, variants, rounds=7):
-    import statistics
-
-    cases = [("S1024c", dict(B=16, S=1024, hq=32, hkv=8, d=128, docs=None), True),
-             ("S512nc", dict(B=32, S=512, hq=32, hkv=8, d=128, docs=None), False),
-             ("S8192nc", dict(B=2, S=8192, hq=32, hkv=8, d=128, docs=None), False),
-             ("S4096c", dict(B=4, S=4096, hq=32, hkv=8, d=128, docs=None), True),
-             ("rime", SHAPES["rime"], True), ("gpt2", SHAPES["gpt2"], True)]
-    ops = torch.ops.dtg
-    for name, c, causal in cases:
-        q, k, v, cu, maxlen, flops, scale = _inputs(c, causal)
-        ref = None
-        times = {vv: [] for vv in variants}
-        for r in range(rounds):
-            for vv in variants:
-                os.environ["DTG_FA_FWD"] = vv
-                for _ in range(5):
-                    o, _ = ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal)
-                if ref is None:
-                    ref = o.float()
-                elif r == 0:
-                    assert (o.float() - ref).abs().max().item() < 2e-2, (name, vv)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    ops.flash_attn_fwd(q, k, v, cu, maxlen, scale, causal)
-                e1.record()
-                torch.cuda.synchronize()
-                times[vv].append(e0.elapsed_time(e1) / a.iters)
-        rec = {"case": name}
-        for vv in variants:
-            med = statistics.median(times[vv])
-            rec[vv] = {"ms": round(med, 4), "min_ms": round(min(times[vv]), 4), "TFLOPs": round(flops / med / 1e9, 1)}
-        print(json.dumps(rec), flush=True)
-
-
 def ab_bwd(a, var, variants, rounds=7):
     import statistics
 
@@ -134,23 +94,23 @@ def ab_bwd(a, var, variants, rounds=7):
         times = {vv: [] for vv in variants}
         for r in range(rounds):
             for vv in variants:
-                os.environ[var] = vv
-                for _ in range(3):
-                    g = ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, causal)
-                if ref is None:
-                    ref = g.clone()
-                elif r == 0 and not a.ab_tolerant:
-                    assert torch.equal(g, ref), (name, vv, (g.float() - ref.float()).abs().max().item())
-                elif r == 0:
-                    err = ((g.float() - ref.float()).norm() / ref.float().norm().clamp_min(1e-12)).item()
-                    assert err < 1e-2, (name, vv, err)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, causal)
-                e1.record()
-                torch.cuda.synchronize()
-                times[vv].append(e0.elapsed_time(e1) / a.iters)
+                with dtg.ops.fa_tuning(q.device, **{var: int(vv)}):
+                    for _ in range(3):
+                        g = ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, causal)
+                    if ref is None:
+                        ref = g.clone()
+                    elif r == 0 and not a.ab_tolerant:
+                        assert torch.equal(g, ref), (name, vv, (g.float() - ref.float()).abs().max().item())
+                    elif r == 0:
+                        err = ((g.float() - ref.float()).norm() / ref.float().norm().clamp_min(1e-12)).item()
+                        assert err < 1e-2, (name, vv, err)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(a.iters):
+                        ops.flash_attn_bwd_qkv(do, qkv, hq, hkv, d, o, lse, cu, maxlen, scale, causal)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    times[vv].append(e0.elapsed_time(e1) / a.iters)
         rec = {"case": name, "bitwise_equal": not a.ab_tolerant}
         for vv in variants:
             med = statistics.median(times[vv])
