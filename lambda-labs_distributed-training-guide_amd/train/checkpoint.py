@@ -568,15 +568,21 @@ class CheckpointManager:
                  async_save: bool = False, fmt: str = "dcp"):
         """fmt: the `checkpoint/` format of the "dp" / "sharded" styles -- "dcp" (torch DCP, the
         reference's tree; train/dcp_ckpt.py) or "dtg" (dtg-sharded-v2).  Loading reads either.
-        A DCP save is collective end to end, so --async-ckpt applies to the "dtg" format only."""
+        An async DCP save snapshots the chunks into reused pinned host buffers and runs DCP's
+        planning collectives and file writes on the writer thread over a dedicated gloo group
+        (created here, collectively), so the training thread's process group is never shared."""
         assert fmt in ("dcp", "dtg"), fmt
         self.exp_dir = Path(exp_dir)
         self.engine, self.optimizer, self.lr_scheduler = engine, optimizer, lr_scheduler
         self.style = style
         self.local_rank = local_rank
         self.fmt = fmt
-        self.async_save = async_save and not (fmt == "dcp" and style != "full")
+        self.async_save = async_save
         self._writer = None   # background thread of the pending save
+        self._host_pool = None  # dcp_ckpt.HostPool of the async DCP snapshots (reused)
+        self._ckpt_pg = None    # gloo group of the async DCP writer thread
+        if async_save and fmt == "dcp" and style != "full" and dist.is_initialized() and get_world_size() > 1:
+            self._ckpt_pg = dist.new_group(backend="gloo")
         self._pending = None  # (state, lr_scheduler state, rng state) to publish on finalize
         self._error = None
 
@@ -593,7 +599,14 @@ class CheckpointManager:
                 sd = self.engine.full_state_dict()
                 if get_rank() == 0:
                     jobs.append(("model.pt", sd))
-            if self.fmt == "dcp":
+            if self.fmt == "dcp" and self.async_save:
+                from .dcp_ckpt import HostPool, snapshot_dcp
+
+                if self._host_pool is None:
+                    self._host_pool = HostPool()
+                shard = ("dcp-snap", snapshot_dcp(self.engine, self.optimizer, self.engine.module.config, global_step,
+                                                  host_pool=self._host_pool))
+            elif self.fmt == "dcp":
                 shard = ("dcp", global_step)
             else:
                 shard = snapshot_sharded(self.engine, global_step)
@@ -609,6 +622,10 @@ class CheckpointManager:
                 from .dcp_ckpt import save_dcp
 
                 save_dcp(pend / "checkpoint", self.engine, self.optimizer, self.engine.module.config, shard[1])
+            elif shard is not None and shard[0] == "dcp-snap":
+                from .dcp_ckpt import write_dcp
+
+                write_dcp(pend / "checkpoint", shard[1], process_group=self._ckpt_pg)
             elif shard is not None:
                 write_sharded(pend / "checkpoint", *shard)
         except BaseException as e:  # surfaced by finalize() on the main thread

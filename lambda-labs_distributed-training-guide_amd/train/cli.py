@@ -150,9 +150,10 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
                    help="checkpoint/ of the sharded chapters (02, 04-07): dcp = torch.distributed.checkpoint "
                         "written by every rank (the reference's tree, readable by dcp_to_torch_save; resumes on "
                         "any world size / TP degree); dtg = this framework's dtg-sharded-v2 (index.json + "
-                        "shard_rNNNNN.pt; --async-ckpt needs it).  Resume reads either")
+                        "shard_rNNNNN.pt).  Resume reads either")
     g.add_argument("--async-ckpt", default="off", choices=["on", "off"],
-                   help="snapshot checkpoints to host memory and write them on a background thread; published "
+                   help="snapshot checkpoints to host memory (reused pinned buffers) and write them on a "
+                        "background thread -- DCP over a dedicated gloo group, or dtg-sharded-v2; published "
                         "(state.json written last) at the next save or at the end of training")
     g.add_argument("--hip-graph", default="off", choices=["on", "off"],
                    help="single GPU: capture the whole step (fwd+bwd+AdamW) in a HIP graph and replay it "

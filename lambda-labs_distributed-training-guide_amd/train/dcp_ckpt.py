@@ -247,17 +247,22 @@ def _adamw_group(optimizer):
     return out
 
 
-def save_dcp(ckpt_dir, engine, optimizer, cfg, global_step=None):
-    """Collective (every rank): write `ckpt_dir` as a DCP checkpoint of {"model": ...,
-    "optimizer": ...} in the reference's layout."""
-    import torch.distributed.checkpoint as dcp
-    from torch.distributed.checkpoint import FileSystemWriter
+class DcpSnapshot:
+    """Everything one rank writes for a DCP save: [(flat key, global shape, offsets, tensor)] chunks,
+    rank 0's param_group objects, the key -> nested-path mappings and the dtg.json record."""
 
-    from .checkpoint import _writes_shards, _TPGeom, param_kind, fsync_dir
+    def __init__(self, tensors, objects, mappings, meta, multi):
+        self.tensors, self.objects, self.mappings, self.meta, self.multi = tensors, objects, mappings, meta, multi
 
-    ckpt_dir = Path(ckpt_dir)
-    ckpt_dir.mkdir(parents=True, exist_ok=True)
-    SavePlanner, _ = _planners()
+
+def snapshot_dcp(engine, optimizer, cfg, global_step=None, host_pool=None) -> DcpSnapshot:
+    """Collective (every rank): describe this rank's part of a DCP save of {"model": ...,
+    "optimizer": ...} in the reference's layout.  With `host_pool` (a HostPool) every chunk is
+    COPIED to host memory -- device chunks into reused pinned buffers, host (offloaded) chunks by
+    memcpy -- so the engine may keep training while `write_dcp` runs on another thread; without it
+    the chunks are views of the live buffers (a synchronous save)."""
+    from .checkpoint import _writes_shards, _TPGeom, param_kind
+
     geo = _TPGeom(engine)
     write = _writes_shards(engine)
     skip = getattr(engine.module, "_dtg_ckpt_skip", set())
@@ -285,12 +290,14 @@ def save_dcp(ckpt_dir, engine, optimizer, cfg, global_step=None):
             key = f"optimizer.state.{hf}.step"
             tensors.append((key, [], [], step))
             mappings[key] = ("optimizer", "state", hf, "step")
+    if host_pool is not None:
+        tensors = host_pool.copy([(k, g, o, t) for k, g, o, t in tensors])
     multi = dist.is_initialized() and dist.get_world_size() > 1
     all_fqns = [None] * dist.get_world_size() if multi else [sorted(fqns)]
     if multi:
         dist.all_gather_object(all_fqns, sorted(fqns))
     rank0 = (dist.get_rank() if dist.is_initialized() else 0) == 0
-    objects = {}
+    objects, meta = {}, None
     if rank0:
         names = sorted(set().union(*[set(x) for x in all_fqns]))
         group = dict(_adamw_group(optimizer), params=names)
@@ -301,18 +308,79 @@ def save_dcp(ckpt_dir, engine, optimizer, cfg, global_step=None):
             key = f"optimizer.param_groups.0.{k}"
             objects[key] = v
             mappings[key] = ("optimizer", "param_groups", 0, k)
-    writer = FileSystemWriter(str(ckpt_dir), single_file_per_rank=True, sync_files=True)
-    dcp.save({}, storage_writer=writer, planner=SavePlanner(tensors, objects, mappings), no_dist=not multi)
-    if rank0:
         meta = {"format": FORMAT, "step": int(engine.step_count), "global_step": global_step,
                 "world_size": dist.get_world_size() if multi else 1, "tp_size": geo.size}
+    return DcpSnapshot(tensors, objects, mappings, meta, multi)
+
+
+def write_dcp(ckpt_dir, snap: DcpSnapshot, process_group=None):
+    """Collective over `process_group` (default: the world): write a snapshot as the DCP tree
+    (`.metadata` + one fsynced `__<rank>_0.distcp` per rank) plus dtg.json.  Issues collectives only
+    on `process_group`, so with a dedicated gloo group it runs on a background thread while the
+    training thread keeps the main group busy (--async-ckpt)."""
+    import torch.distributed.checkpoint as dcp
+    from torch.distributed.checkpoint import FileSystemWriter
+
+    from .checkpoint import fsync_dir
+
+    ckpt_dir = Path(ckpt_dir)
+    ckpt_dir.mkdir(parents=True, exist_ok=True)
+    SavePlanner, _ = _planners()
+    writer = FileSystemWriter(str(ckpt_dir), single_file_per_rank=True, sync_files=True)
+    dcp.save({}, storage_writer=writer, planner=SavePlanner(snap.tensors, snap.objects, snap.mappings),
+             process_group=process_group, no_dist=not snap.multi)
+    if snap.meta is not None:
         with open(ckpt_dir / META, "w") as fp:
-            json.dump(meta, fp)
+            json.dump(snap.meta, fp)
             fp.flush()
             os.fsync(fp.fileno())
-    if multi:
-        dist.barrier()
+    if snap.multi:
+        dist.barrier(group=process_group)
     fsync_dir(ckpt_dir)
+
+
+def save_dcp(ckpt_dir, engine, optimizer, cfg, global_step=None):
+    """Collective (every rank): write `ckpt_dir` as a DCP checkpoint of {"model": ...,
+    "optimizer": ...} in the reference's layout (synchronous: chunks are read from the live
+    buffers while DCP writes them)."""
+    write_dcp(ckpt_dir, snapshot_dcp(engine, optimizer, cfg, global_step))
+
+
+class HostPool:
+    """Host copies of a save's chunks for --async-ckpt, in flat per-dtype buffers that are
+    allocated once (page-locked, exact size: utils/pinned.py) and reused by every later save of
+    the same layout.  Device chunks are copied with non_blocking copies and one device sync;
+    host chunks (CPU-offloaded moments / master weights) by memcpy."""
+
+    def __init__(self):
+        self._bufs = {}  # dtype -> flat tensor
+
+    def copy(self, items):
+        from ..utils.pinned import pinned_zeros
+
+        need = {}
+        for _, _, _, t in items:
+            if t.dim() > 0:
+                need[t.dtype] = need.get(t.dtype, 0) + t.numel()
+        for dt, n in need.items():
+            if dt not in self._bufs or self._bufs[dt].numel() < n:
+                self._bufs[dt] = None
+                self._bufs[dt] = pinned_zeros(n, dt)
+        pos = {dt: 0 for dt in need}
+        out, dev = [], False
+        for key, gshape, offs, t in items:
+            if t.dim() == 0:
+                out.append((key, gshape, offs, t.detach().to("cpu", copy=True)))
+                continue
+            n = t.numel()
+            dst = self._bufs[t.dtype][pos[t.dtype]:pos[t.dtype] + n].view(t.shape)
+            pos[t.dtype] += n
+            dst.copy_(t.detach(), non_blocking=t.is_cuda)
+            dev = dev or t.is_cuda
+            out.append((key, gshape, offs, dst))
+        if dev:
+            torch.cuda.synchronize()
+        return out
 
 
 # ------------------------------------------------------------------------------ load

@@ -368,10 +368,6 @@ def run(chapter: str, argv=None):
     state = new_state()
     resumed = False
     fmt = getattr(args, "ckpt_format", "dcp")
-    if fmt == "dcp" and getattr(args, "async_ckpt", "off") == "on" and style != "full":
-        LOGGER.warning("--async-ckpt writes the dtg-sharded-v2 format (a DCP save is collective end to end): "
-                       "using --ckpt-format dtg")
-        fmt = "dtg"
     mgr = CheckpointManager(exp_dir, engine, opt, lr_scheduler, style, local_rank,
                             async_save=getattr(args, "async_ckpt", "off") == "on", fmt=fmt)
     # DTG_FAKE_WORLD rehearsal: the other ranks are a fake process group, so its weights are
@@ -389,7 +385,9 @@ def run(chapter: str, argv=None):
     udist.barrier()
     if not fake and has_checkpoint(exp_dir):
         LOGGER.info(f"Resuming from {exp_dir}")
+        t_load = time.perf_counter()
         state = mgr.load()
+        LOGGER.info(f"checkpoint loaded in {time.perf_counter() - t_load:.2f} s")
         resumed = True
     LOGGER.info(f"Resumed={resumed} | {state}")
     udist.make_exp_dir(exp_dir, per_rank_dirs=chapter in ("04", "deepspeed"))
@@ -554,13 +552,19 @@ def run(chapter: str, argv=None):
             if state["global_step"] % args.ckpt_freq == 0 and not fake:
                 ucomm.check_xgmi()  # never checkpoint state computed from stale peer data
                 LOGGER.info("Saving checkpoint.")
+                t_save = time.perf_counter()
                 mgr.save(state)
+                LOGGER.info(f"checkpoint save: training stalled {time.perf_counter() - t_save:.2f} s"
+                            + (" (async: snapshot only; the files are written in the background)" if mgr.async_save else ""))
             if args.max_steps and state["global_step"] >= args.max_steps:
                 if run_loss is not None:
                     state["running_loss"] += float(run_loss.item())
                 LOGGER.info(f"Reached --max-steps {args.max_steps}")
                 progress.close()
+                t_fin = time.perf_counter()
                 mgr.finalize()
+                if mgr.async_save:
+                    LOGGER.info(f"checkpoint finalize (join the writer, publish): {time.perf_counter() - t_fin:.2f} s")
                 ucomm.check_xgmi()
                 return state
         progress.close()

@@ -7,6 +7,7 @@ previous dtg-sharded-v2 format stays readable through the same manager.
 
 Reference: /root/reference/04-fully-sharded-data-parallel/train_llm.py:121-154,249-263,
 06-tensor-parallel/train_llm.py:177-190,283-295."""
+import json
 import os
 
 import pytest
@@ -167,3 +168,84 @@ def test_dtg_sharded_v2_still_loads_through_the_manager(tmp_path):
     res = run_distributed(_dtg_roundtrip, 2, str(tmp_path))
     assert (tmp_path / "checkpoint" / "index.json").exists()
     assert all(step == 2 and same for step, same in res)
+
+
+def _async_save_overlapped(rank, world, d):
+    """dp 2 x tp 2: two steps, an async DCP save, two more steps while the writer runs (its file
+    writes held back until those steps are done), then finalize.  Returns this rank's chunks at
+    the saved step and after the later steps."""
+    import threading
+    import time
+
+    import dtg.train.dcp_ckpt as dc
+    from dtg.train.checkpoint import CheckpointManager, new_state
+
+    started, steps_done = threading.Event(), threading.Event()
+    real = dc.write_dcp
+
+    def held(*a, **k):  # the writer starts, then waits for the training thread's two steps
+        started.set()
+        steps_done.wait(60)
+        return real(*a, **k)
+
+    dc.write_dcp = held
+    cfg, model, eng, opt, dp_rank, dp = _engine(2)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10)
+    batches = _batches(cfg.vocab_size, n=4)
+
+    def step(ids):
+        per = ids.shape[0] // dp
+        mine = ids[dp_rank * per:(dp_rank + 1) * per]
+        opt.zero_grad()
+        eng.backward(model(input_ids=mine, labels=mine).loss)
+        opt.step()
+        sched.step()
+
+    def dump():
+        return {(hf, tuple(offs)): {k: v.clone() for k, v in views.items()}
+                for hf, hshape, offs, sizes, views in dc._chunks(eng, cfg)}
+
+    for ids in batches[:2]:
+        step(ids)
+    saved = dump()
+    mgr = CheckpointManager(d, eng, opt, sched, "sharded", async_save=True, fmt="dcp")
+    st = new_state()
+    st["global_step"] = 2
+    t0 = time.perf_counter()
+    mgr.save(st)
+    stall = time.perf_counter() - t0
+    assert started.wait(60)
+    for ids in batches[2:]:
+        step(ids)
+    steps_done.set()
+    later = dump()
+    mgr.finalize()
+    return saved, later, stall
+
+
+@pytest.mark.slow
+def test_async_dcp_save_overlaps_training_and_resumes_bit_exact(tmp_path):
+    d = str(tmp_path)
+    res = run_distributed(_async_save_overlapped, 4, d)
+    ck = tmp_path / "checkpoint"
+    assert (ck / ".metadata").exists() and not (tmp_path / ".pending").exists()
+    assert json.loads((tmp_path / "state.json").read_text())["global_step"] == 2
+    # the later steps really changed the state the writer was holding a snapshot of
+    assert any(not torch.equal(res[0][0][k]["p"], res[0][1][k]["p"]) for k in res[0][0])
+    from torch.distributed.checkpoint.format_utils import dcp_to_torch_save
+
+    dcp_to_torch_save(str(ck), str(tmp_path / "full.pt"))
+    sd = torch.load(tmp_path / "full.pt", weights_only=True)
+    model_sd, opt_sd = sd["model"], sd["optimizer"]
+    for saved, _, _ in res:  # the checkpoint holds the step-2 snapshot, not the live buffers
+        for (hf, offs), views in saved.items():
+            idx = tuple(slice(o, o + s) for o, s in zip(offs, views["p"].shape))
+            assert torch.equal(model_sd[hf][idx], views["p"]), hf
+            assert torch.equal(opt_sd["state"][hf]["exp_avg_sq"][idx], views["v"]), hf
+    # and it resumes bit-exactly on another layout (W = 2, TP = 1)
+    shapes = {k: tuple(v.shape) for k, v in model_sd.items()}
+    dumps = run_distributed(_load_and_dump, 2, d, 1, "fsdp")
+    got = _assemble([x[0] for x in dumps], "p", shapes)
+    m = _assemble([x[0] for x in dumps], "m", shapes)
+    for k in opt_sd["state"]:
+        assert torch.equal(got[k], model_sd[k]) and torch.equal(m[k], opt_sd["state"][k]["exp_avg"]), k

@@ -74,7 +74,8 @@ def test_fsdp_async_checkpoint_resume(tmp_path):
     d = tmp_path / "fa"
     assert not (d / ".pending").exists()
     assert json.loads((d / "state.json").read_text())["global_step"] == 4
-    assert (d / "checkpoint" / "index.json").exists() and (d / "rng.pt").exists() and (d / "lr_scheduler.pt").exists()
+    # the reference's DCP tree, written on the writer thread over its own gloo group
+    assert (d / "checkpoint" / ".metadata").exists() and (d / "rng.pt").exists() and (d / "lr_scheduler.pt").exists()
     r = _torchrun("04-fully-sharded-data-parallel", base + ["--max-steps", "6"])
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "Resuming" in out, out[-3000:]
