@@ -121,10 +121,11 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
     g.add_argument("--ac-layers", default="all",
                    help="with --activation-checkpointing on: how many decoder layers recompute their forward "
                         "(the first N of this rank's stack; the others keep their activations).  all = every "
-                        "layer (the reference); N; auto = after step 1, as few as the measured peak, the "
-                        "per-layer activation size and --ac-budget-gb allow (agreed over all ranks)")
-    g.add_argument("--ac-budget-gb", default=270.0, type=float,
-                   help="HBM budget (GB per GPU) --ac-layers auto plans against (MI355X: 288 GB)")
+                        "layer (the reference); N; auto = as few as --ac-budget-gb allows, planned from the measured "
+                        "peaks of steps 1 and 2 (agreed over all ranks)")
+    g.add_argument("--ac-budget-gb", default=280.0, type=float,
+                   help="HBM budget (GB = 1e9 bytes per GPU, reserved by the caching allocator) --ac-layers auto "
+                        "plans against; an MI355X holds 309 GB (288 GiB), the rest is left to RCCL / fragmentation")
     g.add_argument("--reshard-after-forward", default="on", choices=["on", "off"])
     g.add_argument("--num-workers", default=1, type=int)
     g.add_argument("--prefetch-factor", default=2, type=int)

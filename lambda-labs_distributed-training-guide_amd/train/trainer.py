@@ -504,8 +504,8 @@ def run(chapter: str, argv=None):
                 torch.distributed.all_reduce(loss_sum, group=model._dtg_seq[1])
             state["global_step"] += 1
             state["epoch_step"] += 1
-            if model._dtg_ac_auto is not None:
-                _plan_ac_layers(args, model, cfg, device, model._dtg_ac_auto["tp"], seq_length)
+            if model._dtg_ac_auto is not None and _plan_ac_layers(args, model, cfg, device, model._dtg_ac_auto,
+                                                                  seq_length):
                 model._dtg_ac_auto = None
             # host read of the xGMI communicators' pinned error words (no device sync): a peer
             # lost in this step's barriers stops the job here, not at the next log step
@@ -576,34 +576,58 @@ def run(chapter: str, argv=None):
     return state
 
 
-def _plan_ac_layers(args, model, cfg, device, tp: int, seq_length: int, peak_bytes=None) -> int:
-    """--ac-layers auto, after the first step: keep checkpointed only as many layers as the HBM
-    budget requires.  The step's peak (every layer checkpointed) is measured; each layer released
-    adds its activations (layer_activation_bytes, x1.25) minus its checkpointed input.  Every rank
-    takes the largest count any rank needs (a recompute re-issues the layer's TP collectives).
-    Returns the number of checkpointed layers."""
+def _agree_max(value: int, device) -> int:
+    """The largest value any rank holds (every rank calls it)."""
     import torch.distributed as dist
 
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([int(value)], dtype=torch.int64, device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
+    return int(value)
+
+
+def _plan_ac_layers(args, model, cfg, device, plan: dict, seq_length: int, peak_bytes=None) -> bool:
+    """--ac-layers auto: keep checkpointed only as many layers as the HBM budget requires.
+    Measured, in two steps:
+      1. after step 1 (every layer checkpointed) the step's peak P1 is read, and layers are
+         released by the analytical per-layer size (layer_activation_bytes, x1.5: on the 405B
+         tp 4 rank a released layer measured 2.74 GB against 2.13 estimated, so step 2 must not
+         trust the estimate to the last layer);
+      2. after step 2 the peak P2 with those layers released gives the MEASURED cost of a released
+         layer, (P2 - P1) / released, and the count is re-planned from P1 with it (x1.05).
+    Peaks are the caching allocator's reserved bytes (what the HBM really holds).  Every rank
+    takes the largest count any rank needs (a recompute re-issues the layer's TP collectives).
+    `plan` carries the state between the two calls; returns True when planning is done."""
     from ..parallel.checkpointing import ac_layers_for_budget, layer_activation_bytes, set_checkpointed_layers
 
-    n_ckpt = checkpointed_count(model)
+    n = len(model.layers)
     if peak_bytes is None:
         if device.type != "cuda":
             LOGGER.info("--ac-layers auto: no HBM to plan against off the GPU; every layer stays checkpointed")
-            return n_ckpt
+            return True
         peak_bytes = torch.cuda.max_memory_reserved(device)
-    per_layer = layer_activation_bytes(cfg, args.batch_size, seq_length, tp)
-    inp = 2 * cfg.hidden_size * args.batch_size * seq_length // max(1, tp)
-    keep = ac_layers_for_budget(len(model.layers), n_ckpt, int(peak_bytes), int(args.ac_budget_gb * 1e9), per_layer, inp)
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        t = torch.tensor([keep], dtype=torch.int64,
-                         device=device if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        keep = int(t.item())
+    budget = int(args.ac_budget_gb * 1e9)
+    if plan.get("p1") is None:
+        n_ckpt = checkpointed_count(model)
+        per_layer = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"])
+        inp = 2 * cfg.hidden_size * args.batch_size * seq_length // max(1, plan["tp"])
+        keep = _agree_max(ac_layers_for_budget(n, n_ckpt, int(peak_bytes), budget, per_layer, inp, safety=1.5),
+                          device)
+        set_checkpointed_layers(model, keep)
+        plan.update(p1=int(peak_bytes), released=n_ckpt - keep)
+        LOGGER.info(f"--ac-layers auto (1/2): step-1 peak {peak_bytes / 1e9:.1f} GB, budget {args.ac_budget_gb:g} GB, "
+                    f"~{per_layer / 1e9:.2f} GB per released layer (estimate) -> {keep} of {n} layers checkpointed")
+        return plan["released"] == 0
+    p1, released = plan["p1"], plan["released"]
+    slope = max(1, (int(peak_bytes) - p1) // released)
+    keep = _agree_max(ac_layers_for_budget(n, n, p1, budget, slope, 0, safety=1.05), device)
     set_checkpointed_layers(model, keep)
-    LOGGER.info(f"--ac-layers auto: step-1 peak {peak_bytes / 1e9:.1f} GB, budget {args.ac_budget_gb:g} GB, "
-                f"{per_layer / 1e9:.2f} GB per released layer -> {keep} of {len(model.layers)} layers checkpointed")
-    return keep
+    if device.type == "cuda":  # hand back the blocks step 2's larger release cached
+        torch.cuda.empty_cache()
+    LOGGER.info(f"--ac-layers auto (2/2): step-2 peak {peak_bytes / 1e9:.1f} GB with {released} layers released -> "
+                f"measured {slope / 1e9:.2f} GB per released layer -> {keep} of {n} layers checkpointed")
+    return True
 
 
 def _offload_info(engine) -> dict:

@@ -67,7 +67,7 @@ def test_budget_releases_what_the_headroom_holds():
     from dtg.parallel.checkpointing import ac_layers_for_budget, layer_activation_bytes
 
     GB = 10 ** 9
-    # 100 checkpointed layers, 128 GB peak, 270 GB budget, 1.7 GB per layer, 0.13 GB input
+    # 100 checkpointed layers, 128 GB peak, 270 GB budget, 1.7 GB per layer, 0.13 GB input, x1.25
     keep = ac_layers_for_budget(100, 100, 128 * GB, 270 * GB, int(1.7 * GB), int(0.13 * GB))
     assert keep == 100 - int((142 * GB) // int((1.7 - 0.13) * GB * 1.25))
     assert ac_layers_for_budget(100, 100, 280 * GB, 270 * GB, GB, 0) == 100  # over budget: all stay
@@ -77,7 +77,9 @@ def test_budget_releases_what_the_headroom_holds():
     assert 1.8e9 < b < 2.4e9
 
 
-def test_plan_ac_layers_with_a_measured_peak():
+def test_plan_ac_layers_from_measured_peaks():
+    """Step 1 (all checkpointed, peak P1) releases layers by the analytical estimate; step 2's peak
+    gives the measured cost per released layer, and the count is re-planned from P1 with it."""
     import argparse
 
     from dtg.models import build_model, resolve_config
@@ -89,9 +91,18 @@ def test_plan_ac_layers_with_a_measured_peak():
     apply_activation_checkpointing(m)
     per = layer_activation_bytes(cfg, 2, 128)
     inp = 2 * cfg.hidden_size * 2 * 128
-    args = argparse.Namespace(batch_size=2, ac_budget_gb=(1e9 + 3.5 * (per - inp) * 1.25) / 1e9)
-    keep = _plan_ac_layers(args, m, cfg, torch.device("cpu"), 1, 128, peak_bytes=int(1e9))
-    assert keep == 5 and [layer._dtg_checkpointed for layer in m.layers] == [True] * 5 + [False] * 3
+    GB = 10 ** 9
+    args = argparse.Namespace(batch_size=2, ac_budget_gb=(GB + 3.5 * (per - inp) * 1.5) / GB)
+    plan = {"tp": 1}
+    done = _plan_ac_layers(args, m, cfg, torch.device("cpu"), plan, 128, peak_bytes=GB)
+    assert not done and plan["released"] == 3
+    assert [layer._dtg_checkpointed for layer in m.layers] == [True] * 5 + [False] * 3
+    # the released layers really cost twice the estimate: step 2 peaks at P1 + 3 x 2 x estimate
+    real = int(2 * (per - inp) * 1.5)
+    done = _plan_ac_layers(args, m, cfg, torch.device("cpu"), plan, 128, peak_bytes=GB + 3 * real)
+    assert done
+    free = int(args.ac_budget_gb * GB) - GB
+    assert [layer._dtg_checkpointed for layer in m.layers].count(False) == free // int(real * 1.05) == 1
 
 
 def _torchrun(chapter_dir, args, nproc=2, timeout=400):
