@@ -73,6 +73,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False, o
         "-DTORCH_EXTENSION_NAME=_C", "-Wno-unused-result", "-Wno-deprecated-declarations",
     ] + [f"-I{i}" for i in incs] + [f"-I{CSRC}", f"-I{sysconfig.get_paths()['include']}"]
     hip_flags = common + [f"--offload-arch={ARCH}", "-fno-gpu-rdc", "-munsafe-fp-atomics"]
+    hip_flags += os.environ.get("DTG_EXTRA_HIPFLAGS", "").split()  # A/B variant builds (with --out)
     cpu_flags = common + ["-march=x86-64-v3", "-fopenmp", "-x", "c++"]
     # Per-file codegen options.  flash_attn.hip: MFMA results in ArchVGPRs.  Its backward kernels
     # keep 128 f32 dK/dV (or dQ) accumulators live across the loop; in the default AGPR form the

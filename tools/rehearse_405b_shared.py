@@ -68,8 +68,20 @@ def prep(a):
             shard, size, k = {}, 0, k + 1
     if shard:
         save_file(shard, os.path.join(a.dir, f"model-{k:05d}.safetensors"))
+    _drop_page_cache(a.dir)
     print(json.dumps({"prep_s": round(time.perf_counter() - t0, 1), "files": k + 1,
                       "params_B": round(sum(v.numel() for v in hf.values()) / 1e9, 3)}), flush=True)
+
+
+def _drop_page_cache(d):
+    """The written files' pages leave the page cache (it counts against the box's memory cap)."""
+    for f in sorted(os.listdir(d)):
+        fd = os.open(os.path.join(d, f), os.O_RDONLY)
+        try:
+            os.fsync(fd)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+        finally:
+            os.close(fd)
 
 
 def _owned_chunks(engine, cfg):
@@ -85,17 +97,20 @@ def _owned_chunks(engine, cfg):
     return [(hf, tuple(offs), views["p"]) for hf, hshape, offs, sizes, views in _chunks(engine, cfg, keep)]
 
 
-def _fingerprint(chunks, initial):
-    """{hf name: [sum w, sum w^2, sum d, sum d^2]} of the weights w and of the update d = w - w0."""
+def _fingerprint(chunks, initial, block=1 << 26):
+    """{hf name: [sum w, sum w^2, sum d, sum d^2]} of the weights w and of the update d = w - w0,
+    in float64, streamed in blocks where the weights live (the GPU: no host copies)."""
     out = {}
     for (hf, offs, view), w0 in zip(chunks, initial):
-        w = view.detach().double().cpu()
-        d = w - w0.double()
         s = out.setdefault(hf, [0.0, 0.0, 0.0, 0.0])
-        s[0] += float(w.sum())
-        s[1] += float((w * w).sum())
-        s[2] += float(d.sum())
-        s[3] += float((d * d).sum())
+        wf, w0f = view.detach().reshape(-1), w0.reshape(-1)
+        for i in range(0, wf.numel(), block):
+            w = wf[i:i + block].double()
+            d = w - w0f[i:i + block].to(w.device).double()
+            s[0] += float(w.sum())
+            s[1] += float((w * w).sum())
+            s[2] += float(d.sum())
+            s[3] += float((d * d).sum())
     return out
 
 
@@ -126,7 +141,7 @@ def run(a):
     opt = FlatAdamW(eng, lr=a.lr)
     build_s = time.perf_counter() - t0
     chunks = _owned_chunks(eng, cfg)
-    initial = [v.detach().to("cpu", copy=True) for _, _, v in chunks]
+    initial = [v.detach().clone() for _, _, v in chunks]  # on the parameters' device (HBM, not host RAM)
     g = torch.Generator().manual_seed(1)
     rows = a.batch * dp
     batches = [torch.randint(0, cfg.vocab_size, (rows, a.seq), generator=g) for _ in range(a.steps)]
