@@ -136,6 +136,13 @@ __device__ __forceinline__ void pipeline_reads() {
   __builtin_amdgcn_sched_group_barrier(kSchedMfma, AHEAD, 0);
 }
 
+// Forward: wave priority around the MFMA phases -- the wave issuing a GEMM block outranks its
+// SIMD partner, which meanwhile runs its softmax on the VALU.  Round 6's bounded attention
+// attempt (profiles/r6/attention/): forward +1.5 % at the 8B shape, +2.7 % at S 8192, rime
+// neutral; the same around the dQ kernel's MFMA phases was neutral and is not used.
+__device__ __forceinline__ void prio_hi() { __builtin_amdgcn_s_setprio(1); }
+__device__ __forceinline__ void prio_lo() { __builtin_amdgcn_s_setprio(0); }
+
 // Row of accumulator register `reg` for lane half h (32x32 C/D map).
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 // The lane-independent part: acc_row(reg, h) == acc_row0(reg) + 4h, a compile-time constant, so
@@ -419,6 +426,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
     if ((!CAUSAL || kt0 <= wave_qmax + koff_c) && (win == 0 || kt0 + kFwdBK - 1 >= wave_q0 + koff_c - win + 1)) {
       f32x16 s[2];
       __builtin_amdgcn_sched_barrier(0);
+      prio_hi();
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         bf16x8 kf[NC];
@@ -430,6 +438,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       }
       pipeline_reads<2 * NC, 1, 4>();
       __builtin_amdgcn_sched_barrier(0);
+      prio_lo();
       if ((CAUSAL && kt0 + kFwdBK - 1 > wave_q0 + koff_c) || kt0 + kFwdBK > klen ||
           (win > 0 && kt0 < wave_qmax + koff_c - win + 1)) {
 #pragma unroll
@@ -481,6 +490,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) pf[j] = pack8(s[j >> 1], j & 1);
       __builtin_amdgcn_sched_barrier(0);
+      prio_hi();
 #pragma unroll
       for (int j = 0; j < 4; ++j) {  // 16-key steps
         const char* vb = V + 16 * j * RB;
@@ -492,6 +502,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdParams P) {
       }
       pipeline_reads<4 * ND, 2, 3>();
       __builtin_amdgcn_sched_barrier(0);
+      prio_lo();
     }
     if (more) {
       char* nb = smem + (1 - B) * 2 * TILE;

@@ -52,6 +52,9 @@ class TPInfo:
         # chunks of the overlapped sequence-parallel regions (parallel/async_tp.py; 1 = the
         # synchronous gather -> block -> scatter path)
         self.overlap_chunks = async_tp.DEFAULT_CHUNKS
+        # re-gather the sequence-parallel inputs in the backward instead of keeping them
+        # (`--sp-regather`, parallel/async_tp.py `regathered`; layers that recompute skip it)
+        self.sp_regather = False
 
     @property
     def enabled(self):
@@ -142,26 +145,40 @@ class LlamaDecoderLayer(nn.Module):
         else:
             n, res = ops.add_rms_norm(x, res, self.input_layernorm.weight, self.eps)
         ka, km = self._overlap_chunks(n.shape[0], rc) if g is not None else (1, 1)
+        regather = g is not None and self._regather()
         if ka > 1:
             a = async_tp.sp_region(n, lambda xg, j, out=None: self.self_attn(xg, _chunk_ctx(rc, xg.shape[0]), out=out), g, ka,
-                                   tuple(p for p in self.self_attn.parameters()))
+                                   tuple(p for p in self.self_attn.parameters()), regather=regather)
+        elif g is not None:
+            a = self._sp_block(n, lambda xg: self.self_attn(xg, rc), g, regather)
         else:
-            if g is not None:
-                n = tp_comm.gather_seq(n, g)
             a = self.self_attn(n, rc)
-            if g is not None:
-                a = tp_comm.scatter_seq(a, g)
         n2, res = ops.add_rms_norm(a, res, self.post_attention_layernorm.weight, self.eps)
         if km > 1:
             m = async_tp.sp_region(n2, lambda xg, j, out=None: self.mlp(xg, out=out), g, km,
-                                   (self.mlp.gate_up_proj.weight, self.mlp.down_proj.weight))
+                                   (self.mlp.gate_up_proj.weight, self.mlp.down_proj.weight), regather=regather)
+        elif g is not None:
+            m = self._sp_block(n2, self.mlp, g, regather)
         else:
-            if g is not None:
-                n2 = tp_comm.gather_seq(n2, g)
             m = self.mlp(n2)
-            if g is not None:
-                m = tp_comm.scatter_seq(m, g)
         return m, res
+
+    def _regather(self):
+        return self.tp.sp_regather and torch.is_grad_enabled() and not getattr(self, "_dtg_checkpointed", False)
+
+    @staticmethod
+    def _sp_block(n, fn, g, regather):
+        """Synchronous sequence-parallel sub-block: gather -> fn -> reduce-scatter.  With regather
+        the gathered input is not kept for fn's backward (async_tp.regathered): it is re-gathered,
+        the all-gather issued as soon as the sub-block's output gradient arrives."""
+        full = tp_comm.gather_seq(n, g)
+        if not regather:
+            return tp_comm.scatter_seq(fn(full), g)
+        with async_tp.regathered(full, n, g) as h:
+            y = fn(full)
+        if y.requires_grad:
+            y.register_hook(lambda grad, h=h: h.prefetch())
+        return tp_comm.scatter_seq(y, g)
 
     def _overlap_chunks(self, rows_local, rc: RunCtx):
         """(attention, MLP) chunk counts of the overlapped SP regions for this forward."""

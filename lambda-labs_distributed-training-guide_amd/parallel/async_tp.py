@@ -36,12 +36,20 @@ Attention chunks must hold whole sequences (dense rows, T/n a multiple of k x S)
 region accepts any chunking.  Layers under activation checkpointing keep the synchronous
 path (a recompute must not stop half-way through a pipelined region).
 
+With `regather` (`--sp-regather on`), autograd does not keep the GATHERED chunk for the
+column-parallel GEMM's weight gradient: a saved-tensor hook swaps it for a handle on this rank's
+local rows, and the backward re-gathers them (prefetched with the chunk's dY gather).  The
+activations a layer keeps shrink by (1 - 1/n) of one [T, H] tensor per region -- at the 405B
+tp 4 recipe 0.4 GB per region -- for one more all-gather per region in the backward, which is
+what lets `--ac-layers auto` release more layers from recomputation (`regathered`).
+
 Reference behaviour: the reference's TP chapter runs DTensor's synchronous redistributes
 (/root/reference/06-tensor-parallel/train_llm.py:84-128); this is the MI355X design that hides
 them, not a translation.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -52,9 +60,51 @@ from ..utils import comm
 DEFAULT_CHUNKS = int(os.environ.get("DTG_TP_OVERLAP_CHUNKS", "2"))
 
 
+class RegatherHandle:
+    """A sequence-parallel all-gather result [n * c, ...] that autograd does not keep: `get()`
+    re-gathers this rank's `local` rows (waiting for a `prefetch()` issued earlier, if any)."""
+
+    def __init__(self, local, shape, dtype, group):
+        self.local, self.shape, self.dtype, self.group = local, tuple(shape), dtype, group
+        self._buf = self._work = None
+
+    def prefetch(self):
+        if self._buf is None:
+            self._buf = torch.empty(self.shape, dtype=self.dtype, device=self.local.device)
+            self._work = comm.all_gather_dim0_into_async(self._buf, self.local, self.group)
+
+    def get(self):
+        self.prefetch()
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        return self._buf
+
+
+@contextlib.contextmanager
+def regathered(full, local, group):
+    """Inside the block, every tensor autograd saves that IS `full` (same storage, shape, strides and
+    dtype: the gathered activation the column-parallel GEMM keeps for its weight gradient) is
+    replaced by a RegatherHandle on `local`; the backward's unpack re-gathers it.  Yields the
+    handle (callers prefetch it ahead of the backward that needs it)."""
+    h = RegatherHandle(local, full.shape, full.dtype, group)
+    key = (full.data_ptr(), tuple(full.shape), tuple(full.stride()), full.dtype)
+
+    def pack(t):
+        if (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype) == key:
+            return h
+        return t
+
+    def unpack(v):
+        return v.get() if isinstance(v, RegatherHandle) else v
+
+    with torch.autograd.graph.saved_tensors_hooks(pack, unpack):
+        yield h
+
+
 class _Region(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, fn, group, k, *params):
+    def forward(ctx, x, fn, group, k, regather, *params):
         n = comm.world(group)
         Tl, H = x.shape
         Tc = Tl // k
@@ -62,7 +112,7 @@ class _Region(torch.autograd.Function):
         out = torch.empty_like(xs)
         g = torch.empty((n * Tc, H), dtype=x.dtype, device=x.device)
         work = comm.all_gather_dim0_into_async(g, xs[0], group)
-        leaves, ys, rs = [], [], []
+        leaves, ys, rs, handles = [], [], [], []
         for j in range(k):
             work.wait()
             cur = g
@@ -73,13 +123,20 @@ class _Region(torch.autograd.Function):
             buf = comm.rs_input_buffer(group, (n * Tc, H), x.dtype, stage_bytes=Tc * H * x.element_size())
             with torch.enable_grad():
                 leaf = cur.detach().requires_grad_(True)
-                y = fn(leaf, j) if buf is None else fn(leaf, j, out=buf)
+                with (regathered(leaf, xs[j], group) if regather else contextlib.nullcontext()) as h:
+                    y = fn(leaf, j) if buf is None else fn(leaf, j, out=buf)
             rs.append(comm.reduce_scatter_dim0_into_async(out[j], y.detach(), group))
             leaves.append(leaf)
             ys.append(y)
+            handles.append(h)
         for w in rs:
             w.wait()
+        if regather:  # the gathered chunks are dropped: the leaves keep only their metadata (for .grad)
+            for leaf in leaves:
+                leaf.untyped_storage().resize_(0)
+            ctx.xs = xs
         ctx.leaves, ctx.ys, ctx.group, ctx.k, ctx.n_params = leaves, ys, group, k, len(params)
+        ctx.handles = handles
         return out.view(Tl, H)
 
     @staticmethod
@@ -92,6 +149,9 @@ class _Region(torch.autograd.Function):
         dx = torch.empty_like(ds)
         g = torch.empty((n * Tc, H), dtype=dout.dtype, device=dout.device)
         work = comm.all_gather_dim0_into_async(g, ds[0], group)
+        hs = ctx.handles
+        if hs[0] is not None:
+            hs[0].prefetch()
         rs = []
         with deferred_notifications():
             for j in range(k):
@@ -100,24 +160,27 @@ class _Region(torch.autograd.Function):
                 if j + 1 < k:
                     g = torch.empty((n * Tc, H), dtype=dout.dtype, device=dout.device)
                     work = comm.all_gather_dim0_into_async(g, ds[j + 1], group)
+                    if hs[j + 1] is not None:
+                        hs[j + 1].prefetch()
                 y, leaf = ctx.ys[j], ctx.leaves[j]
                 torch.autograd.backward(y, cur)
                 gx = leaf.grad
-                ctx.ys[j] = ctx.leaves[j] = None  # release chunk j's graph and saved activations
+                ctx.ys[j] = ctx.leaves[j] = hs[j] = None  # release chunk j's graph and saved activations
                 rs.append(comm.reduce_scatter_dim0_into_async(dx[j], gx, group))
                 del y, leaf, gx
             for w in rs:
                 w.wait()
-        return (dx.view(Tl, H), None, None, None) + (None,) * ctx.n_params
+        return (dx.view(Tl, H), None, None, None, None) + (None,) * ctx.n_params
 
 
-def sp_region(x, fn, group, k, params):
+def sp_region(x, fn, group, k, params, regather: bool = False):
     """reduce_scatter(fn(all_gather(x))) with k-chunk compute/communication overlap.
 
     fn(x_chunk_gathered, j[, out=buffer]) -> partial output of the same row count (written into
     `out` when one is passed); `params` are the weights
-    fn uses (passed so the region is part of the autograd graph even when x needs no grad)."""
-    return _Region.apply(x, fn, group, int(k), *params)
+    fn uses (passed so the region is part of the autograd graph even when x needs no grad).
+    regather: re-gather the chunks in the backward instead of keeping them (see the module doc)."""
+    return _Region.apply(x, fn, group, int(k), bool(regather), *params)
 
 
 def region_chunks(rows_local: int, k: int, row_len: int = 1) -> int:

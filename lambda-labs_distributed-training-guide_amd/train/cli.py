@@ -74,6 +74,11 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
         p.add_argument("--tp-overlap-chunks", default=2, type=int,
                        help="row chunks of the overlapped sequence-parallel regions (parallel/async_tp.py): the "
                             "all-gather / reduce-scatter of one chunk runs under the GEMMs of the next; 1 = off")
+        p.add_argument("--sp-regather", default="off", choices=["on", "off"],
+                       help="layers that do not recompute keep only their sequence-parallel shard of each "
+                            "column-parallel GEMM's input and re-gather it in the backward (one more all-gather "
+                            "per sub-block, prefetched; (1 - 1/tp) of a [tokens, hidden] tensor less per sub-block "
+                            "and layer) -- with --ac-layers auto, more layers skip their recompute")
     if chapter == "deepspeed":
         p.add_argument("--local_rank", type=int, default=None)
         p.add_argument("--deepspeed", action="store_true", help="accepted for launcher compatibility")

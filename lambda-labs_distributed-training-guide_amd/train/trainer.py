@@ -238,6 +238,9 @@ def _build(args, chapter, device, world):
     if tp_group is not None and hasattr(model, "tp"):
         model.tp.overlap_chunks = max(1, getattr(args, "tp_overlap_chunks", 2))
         LOGGER.info(f"tp overlap: {model.tp.overlap_chunks} chunks per sequence-parallel region")
+        model.tp.sp_regather = getattr(args, "sp_regather", "off") == "on"
+        if model.tp.sp_regather:
+            LOGGER.info("sp regather: column-parallel inputs re-gathered in the backward (not kept)")
     model._dtg_seq = seq
     model._dtg_pp = None
     if pp > 1:

@@ -10,7 +10,7 @@ from test_engines_cpu import _batches, _train
 TOL = dict(atol=3e-4, rtol=1e-3)
 
 
-def _tp_worker(rank, world, tp, model_name, batches, engine_mode, chunks=None):
+def _tp_worker(rank, world, tp, model_name, batches, engine_mode, chunks=None, regather=False):
     import torch.distributed as dist
 
     from dtg.models import build_model, resolve_config
@@ -24,12 +24,13 @@ def _tp_worker(rank, world, tp, model_name, batches, engine_mode, chunks=None):
     model = build_model(cfg, device="cpu", dtype=torch.float32, tp_group=tp_group, init=False)
     model.load_state_dict(shard_full_state_dict(full.state_dict(), cfg, tp_rank, tp))
     calls = []
+    model.tp.sp_regather = regather
     if chunks is not None:
         model.tp.overlap_chunks = chunks
         import dtg.parallel.async_tp as atp
 
         orig = atp.sp_region
-        atp.sp_region = lambda x, fn, g, k, params: calls.append(k) or orig(x, fn, g, k, params)
+        atp.sp_region = lambda x, fn, g, k, params, **kw: calls.append(k) or orig(x, fn, g, k, params, **kw)
     if engine_mode == "fsdp":
         from dtg.parallel.fsdp import FullyShard
 
@@ -100,6 +101,43 @@ def test_tp_overlap_chunks_match_single(chunks, mode):
     full = unshard_state_dicts(shards, cfg)
     for n in ref:
         torch.testing.assert_close(full[n], ref[n], **TOL, msg=n)
+
+
+@pytest.mark.parametrize("chunks,mode", [(1, "ddp"), (4, "fsdp")])
+def test_sp_regather_is_bitwise_the_kept_activations(chunks, mode):
+    """--sp-regather: the column-parallel inputs re-gathered in the backward (synchronous
+    sub-blocks at k = 1, overlapped regions at k = 4) train bit for bit like keeping them."""
+    from dtg.models import resolve_config
+
+    model_name = "llama-tiny-d128"
+    cfg = resolve_config(model_name)
+    batches = _batches(cfg.vocab_size, 8, 16)
+    kept = run_distributed(_tp_worker, 2, 2, model_name, batches, mode, chunks, False)
+    regathered = run_distributed(_tp_worker, 2, 2, model_name, batches, mode, chunks, True)
+    for a, b in zip(kept, regathered):
+        assert a[1] == b[1], (a[1], b[1])
+        for n, v in a[0].items():
+            assert torch.equal(v, b[0][n]), n
+
+
+def test_regathered_swaps_only_the_gathered_tensor():
+    """The saved-tensor hook replaces exactly the gathered activation (not the weight) and the
+    backward's unpack re-gathers it (world 1: a copy of the local rows) -- once."""
+    from dtg.parallel.async_tp import RegatherHandle, regathered
+
+    local = torch.randn(8, 4)
+    full = local.clone().requires_grad_(True)
+    w = torch.randn(3, 4, requires_grad=True)
+    with regathered(full, local, None) as h:
+        y = torch.nn.functional.linear(full, w)
+    assert isinstance(h, RegatherHandle) and h._buf is None  # nothing gathered yet
+    gets = []
+    real_get = h.get
+    h.get = lambda: gets.append(1) or real_get()
+    y.sum().backward()
+    assert len(gets) == 1 and torch.equal(h._buf, local)
+    assert torch.allclose(w.grad, torch.ones(3, 8) @ local)
+    assert torch.allclose(full.grad, torch.ones(8, 3) @ w)
 
 
 def _init_worker(rank, world, engine):
