@@ -17,6 +17,7 @@ converts to/from HF's split q/k/v and gate/up tensors.
 from __future__ import annotations
 
 import dataclasses
+import weakref
 from typing import Optional
 
 import torch
@@ -177,7 +178,10 @@ class LlamaDecoderLayer(nn.Module):
         with async_tp.regathered(full, n, g) as h:
             y = fn(full)
         if y.requires_grad:
-            y.register_hook(lambda grad, h=h: h.prefetch())
+            # weak: the hook lives on in the graph until the step's output is released; the
+            # handle (and the rows it holds) must not
+            ref = weakref.ref(h)
+            y.register_hook(lambda grad: None if ref() is None else ref().prefetch())
         return tp_comm.scatter_seq(y, g)
 
     def _overlap_chunks(self, rows_local, rc: RunCtx):

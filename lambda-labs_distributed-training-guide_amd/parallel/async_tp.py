@@ -74,11 +74,15 @@ class RegatherHandle:
             self._work = comm.all_gather_dim0_into_async(self._buf, self.local, self.group)
 
     def get(self):
+        """The re-gathered tensor.  The handle drops its own reference: the tensor lives only as
+        long as the backward node that unpacked it (autograd keeps the graph's nodes -- and the
+        handles they reference -- until the step's output is released)."""
         self.prefetch()
         if self._work is not None:
             self._work.wait()
             self._work = None
-        return self._buf
+        buf, self._buf = self._buf, None
+        return buf
 
 
 @contextlib.contextmanager
@@ -112,7 +116,7 @@ class _Region(torch.autograd.Function):
         out = torch.empty_like(xs)
         g = torch.empty((n * Tc, H), dtype=x.dtype, device=x.device)
         work = comm.all_gather_dim0_into_async(g, xs[0], group)
-        leaves, ys, rs, handles = [], [], [], []
+        leaves, ys, rs, handles, in_slot = [], [], [], [], []
         for j in range(k):
             work.wait()
             cur = g
@@ -129,8 +133,15 @@ class _Region(torch.autograd.Function):
             leaves.append(leaf)
             ys.append(y)
             handles.append(h)
+            in_slot.append(buf is not None)
         for w in rs:
             w.wait()
+        # The chunks' partial outputs have been reduce-scattered: their backward needs only their
+        # graphs, not their values, so the [n * Tc, H] buffers go now instead of at the backward
+        # (xGMI workspace slots are the communicator's and stay).
+        for y, slot in zip(ys, in_slot):
+            if not slot:
+                y.untyped_storage().resize_(0)
         if regather:  # the gathered chunks are dropped: the leaves keep only their metadata (for .grad)
             for leaf in leaves:
                 leaf.untyped_storage().resize_(0)
@@ -170,6 +181,7 @@ class _Region(torch.autograd.Function):
                 del y, leaf, gx
             for w in rs:
                 w.wait()
+        ctx.xs = ctx.handles = None
         return (dx.view(Tl, H), None, None, None, None) + (None,) * ctx.n_params
 
 

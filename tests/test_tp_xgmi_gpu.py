@@ -30,7 +30,7 @@ def _run(model, eng, ids):
     return out.loss.item()
 
 
-def _worker(rank, world, rows=2, chunks=1, engine="kernel"):
+def _worker(rank, world, rows=2, chunks=1, engine="kernel", regather=False):
     import torch.distributed as dist
 
     from dtg.models import build_model, resolve_config
@@ -50,6 +50,7 @@ def _worker(rank, world, rows=2, chunks=1, engine="kernel"):
     model = build_model(cfg, device=dev, tp_group=tp_group, init=False)
     model.load_state_dict(shard_full_state_dict(full.state_dict(), cfg, tp_rank, 2))
     model.tp.overlap_chunks = chunks  # > 1: overlapped SP regions, xGMI collectives on a side stream
+    model.tp.sp_regather = regather
     eng = DataParallel(model, mode="single", tp_group=tp_group, broadcast_from_rank0=False)
     loss = _run(model, eng, _ids(cfg.vocab_size, rows).to(dev))
     torch.cuda.synchronize()
@@ -80,3 +81,15 @@ def test_tp2_xgmi_matches_single_device(cuda, rows, chunks, engine):
     for n, g in ref_g.items():
         rel = ((full[n] - g).norm() / g.norm().clamp_min(1e-12)).item()
         assert rel < 3e-2, (n, rel)
+
+
+@pytest.mark.parametrize("rows,chunks,engine", [(2, 1, "kernel"), (4, 2, "dma")])
+def test_tp2_xgmi_sp_regather_is_bitwise(cuda, rows, chunks, engine):
+    """--sp-regather on the xGMI transports: the backward re-gathers the column-parallel inputs
+    (prefetched on the xGMI side stream) and every gradient is bitwise the kept-activation run's."""
+    kept = run_distributed(_worker, 2, rows, chunks, engine, False)
+    regathered = run_distributed(_worker, 2, rows, chunks, engine, True)
+    for a, b in zip(kept, regathered):
+        assert a[0] == b[0]
+        for n, g in a[1].items():
+            assert torch.equal(g, b[1][n]), n
