@@ -581,7 +581,8 @@ class CheckpointManager:
         self._writer = None   # background thread of the pending save
         self._host_pool = None  # dcp_ckpt.HostPool of the async DCP snapshots (reused)
         self._ckpt_pg = None    # gloo group of the async DCP writer thread
-        if async_save and fmt == "dcp" and style != "full" and dist.is_initialized() and get_world_size() > 1:
+        if (async_save and fmt == "dcp" and style != "full" and dist.is_initialized() and get_world_size() > 1
+                and dist.get_backend() != "fake"):  # a DTG_FAKE_WORLD rehearsal never saves
             self._ckpt_pg = dist.new_group(backend="gloo")
         self._pending = None  # (state, lr_scheduler state, rng state) to publish on finalize
         self._error = None
