@@ -56,14 +56,17 @@ def parse(argv=None):
     # auto (default) = the faster of the two on this job's group at one bucket, timed at startup in a
     # child job (parallel/transport.py; a first contact with cross-device IPC cannot take the measured
     # run down); recorded as dp_comm_calibration
-    ap.add_argument("--dp-comm", default="auto", choices=["auto", "rccl", "xgmi-dma"])
+    # RCCL by default (auto = the child-job calibration of parallel/transport.py, opt-in until a
+    # multi-GPU run has validated the direct-peer paths; their evidence comes from the xGMI child
+    # diagnostic after the timed region)
+    ap.add_argument("--dp-comm", default="rccl", choices=["auto", "rccl", "xgmi-dma"])
     # BASELINE config 06 (Llama-3-8B TP=8 over xGMI): --tp 8 --gpus 8.  Tensor + sequence parallel
     # inside groups of --tp ranks, data parallel (--parallel) across them; a step is dp x B x S
     # tokens (the reference's TP tok/s formula, 06-tensor-parallel/train_llm.py:256).
     ap.add_argument("--tp", type=int, default=1)
     # auto = the fastest of RCCL / xGMI pull kernels / xGMI copy engines at this job's TP message size,
-    # timed at startup like --dp-comm auto (the chapter-06/07 trainer's default too); the PG backend on CPU
-    ap.add_argument("--tp-comm", default="auto", choices=["auto", "rccl", "xgmi", "xgmi-dma"])
+    # timed at startup in a child job like --dp-comm auto (opt-in, as in the trainer); the PG backend on CPU
+    ap.add_argument("--tp-comm", default="rccl", choices=["auto", "rccl", "xgmi", "xgmi-dma"])
     ap.add_argument("--tp-overlap-chunks", type=int, default=2)
     ap.add_argument("--overlap-optimizer", type=int, default=0,
                     help="1: per-bucket AdamW (and ZeRO all-gather) on a side stream during backward (measured +0.2%% on 1 GPU, off)")

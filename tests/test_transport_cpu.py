@@ -63,9 +63,9 @@ def test_resolve_on_cpu_is_the_process_group():
     assert explicit == ("xgmi", None)
 
 
-def test_trainer_defaults_to_rccl_and_bench_to_auto():
-    """The trainer's chapters default to RCCL (auto is opt-in and runs in a child job); the bench
-    keeps auto, which it has always calibrated in a child job."""
+def test_trainer_and_bench_default_to_rccl():
+    """The trainer's chapters and the bench default to RCCL; auto (the child-job calibration) is
+    opt-in until a multi-GPU run has validated the direct-peer paths."""
     import bench
     from dtg.train.cli import get_parser
 
@@ -76,7 +76,7 @@ def test_trainer_defaults_to_rccl_and_bench_to_auto():
         a = get_parser(ch).parse_args(["-e", "x", "-d", "synthetic", "-m", "llama-tiny"])
         assert a.dp_comm == "rccl"
     b = bench.parse([])
-    assert b.tp_comm == "auto" and b.dp_comm == "auto"
+    assert b.tp_comm == "rccl" and b.dp_comm == "rccl"
     assert math.isfinite(b.deadline_s) and b.diag_budget_s < b.deadline_s
 
 
