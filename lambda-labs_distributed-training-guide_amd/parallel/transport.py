@@ -413,6 +413,8 @@ def resolve_isolated(flag: str, kind: str, device, msg_bytes: int, mesh=(1, 0), 
         note = None
         if dev.type != "cuda":
             note = "CPU: the process group's backend is the only transport"
+        elif dist.get_backend() == "fake":
+            note = "DTG_FAKE_WORLD rehearsal: no peers to calibrate against"
         elif dist.get_backend() != "nccl" and os.environ.get("DTG_TRANSPORT_CALIBRATE") != "1":
             note = "non-RCCL process group: not calibrated (DTG_TRANSPORT_CALIBRATE=1 forces it)"
         elif int(os.environ.get("LOCAL_WORLD_SIZE", world)) != world:
