@@ -623,7 +623,10 @@ def _plan_ac_layers(args, model, cfg, device, plan: dict, seq_length: int, peak_
                     f"~{per_layer / 1e9:.2f} GB per released layer (estimate) -> {keep} of {n} layers checkpointed")
         return plan["released"] == 0
     p1, released = plan["p1"], plan["released"]
-    slope = max(1, (int(peak_bytes) - p1) // released)
+    # never below a quarter of the estimate: a step-2 peak that did not grow (a reset peak
+    # counter, an allocator that freed a cache) must not release every layer
+    floor = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"]) // 4
+    slope = max(1, floor, (int(peak_bytes) - p1) // released)
     keep = _agree_max(ac_layers_for_budget(n, n, p1, budget, slope, 0, safety=1.05), device)
     set_checkpointed_layers(model, keep)
     if device.type == "cuda":  # hand back the blocks step 2's larger release cached

@@ -103,6 +103,14 @@ def test_plan_ac_layers_from_measured_peaks():
     assert done
     free = int(args.ac_budget_gb * GB) - GB
     assert [layer._dtg_checkpointed for layer in m.layers].count(False) == free // int(real * 1.05) == 1
+    # a step-2 peak that did not grow cannot release every layer: the slope has a floor
+    m2 = build_model(cfg, device="cpu", dtype=torch.float32)
+    apply_activation_checkpointing(m2)
+    plan = {"tp": 1}
+    _plan_ac_layers(args, m2, cfg, torch.device("cpu"), plan, 128, peak_bytes=GB)
+    _plan_ac_layers(args, m2, cfg, torch.device("cpu"), plan, 128, peak_bytes=GB)
+    released = [layer._dtg_checkpointed for layer in m2.layers].count(False)
+    assert released == min(8, free // int((per // 4) * 1.05))
 
 
 def _torchrun(chapter_dir, args, nproc=2, timeout=400):
