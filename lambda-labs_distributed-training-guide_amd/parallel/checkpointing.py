@@ -7,12 +7,13 @@ hooks (FSDP gather/reshard) still fire on the layer's __call__, while the recomp
 original forward directly (no hooks, parameters already gathered by the pre-backward node).
 
 The reference checkpoints every decoder layer (/root/reference/05-training-llama-405b/
-train_llm.py:122-126).  On a 288 GB MI355X that leaves most of the HBM idle at 405B width (the
-tp 4 x dp 2 one-node recipe peaks at ~150 GB projected to 126 layers), so the number of
+train_llm.py:122-126).  On a 309 GB (288 GiB) MI355X that leaves most of the HBM idle at 405B
+width (the tp 4 x dp 2 one-node recipe peaks at ~157 GB projected to 126 layers), so the number of
 checkpointed layers is a knob: `--ac-layers N` checkpoints the first N layers of the rank's stack
-and keeps the rest's activations, and `--ac-layers auto` picks N after the first step from the
-measured peak, the HBM budget and the per-layer activation size (`ac_layers_for_budget`).  Which
-layers recompute changes no value: the recompute is bitwise the forward (tests/test_ac_layers_cpu.py).
+and keeps the rest's activations, and `--ac-layers auto` plans N from the measured peaks of the
+first two steps against the HBM budget (train/trainer.py `_plan_ac_layers`, with
+`layer_activation_bytes` as the first estimate and `ac_layers_for_budget`).  Which layers recompute
+changes no value: the recompute is bitwise the forward (tests/test_ac_layers_cpu.py).
 """
 import torch
 from torch.utils.checkpoint import checkpoint
@@ -55,21 +56,25 @@ def checkpointed_count(model, layers=None) -> int:
     return sum(1 for layer in layers if getattr(layer, "_dtg_checkpointed", False))
 
 
-def layer_activation_bytes(cfg, batch: int, seq: int, tp: int = 1) -> int:
-    """Bytes one Llama decoder layer keeps for its backward WITHOUT checkpointing, per rank: the
-    norm inputs / outputs on the sequence-parallel shard, and the fused QKV, attention output (+
-    LSE), gate|up and SwiGLU outputs on the gathered tokens, column-sharded over TP (the layer's
-    saved tensors in models/llama.py).  With checkpointing it keeps only its input (2 H bytes per
-    local token), which the caller subtracts."""
+def layer_activation_bytes(cfg, batch: int, seq: int, tp: int = 1, regather: bool = False) -> int:
+    """Bytes one Llama decoder layer keeps for its backward WITHOUT checkpointing, per rank (the
+    saved tensors of models/llama.py's fused ops): the two add+RMSNorm residual sums on the
+    sequence-parallel shard; the fused QKV, the attention output and LSE and the gate|up output on
+    the gathered tokens, column-sharded over TP (SwiGLU's product is recomputed); and the two
+    column-parallel GEMM inputs -- gathered, or only this rank's rows with `regather`
+    (--sp-regather).  With checkpointing a layer keeps only its input (2 H bytes per local token),
+    which the caller subtracts.  Measured at the 405B tp 4 rank, b4 x 4096: 2.23 GB kept /
+    1.45 GB re-gathered against 2.50 / 1.70 here (profiles/r6/405b_ac/)."""
     H, I = cfg.hidden_size, cfg.intermediate_size
     nq, nkv, d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
     tp = max(1, int(tp))
     t_full = batch * seq
     t_local = t_full // tp
-    norms = 2 * 4 * H * t_local
-    cols = 2 * t_full * ((nq + 2 * nkv) * d + nq * d + 3 * I) // tp
+    norms = 2 * 2 * H * t_local
+    cols = 2 * t_full * ((nq + 2 * nkv) * d + nq * d + 2 * I) // tp
     lse = 4 * t_full * nq // tp
-    return int(norms + cols + lse)
+    inputs = 2 * 2 * H * (t_local if (regather and tp > 1) else t_full)
+    return int(norms + cols + lse + inputs)
 
 
 def ac_layers_for_budget(n_layers: int, n_ckpt: int, peak_bytes: int, budget_bytes: int, per_layer_bytes: int,

@@ -255,7 +255,8 @@ def _build(args, chapter, device, world):
         spec = str(getattr(args, "ac_layers", "all"))
         apply_activation_checkpointing(model, count=None if spec in ("all", "auto") else int(spec))
         if spec == "auto":
-            model._dtg_ac_auto = {"tp": tp_group.size() if tp_group is not None else 1}
+            model._dtg_ac_auto = {"tp": tp_group.size() if tp_group is not None else 1,
+                                  "regather": getattr(args, "sp_regather", "off") == "on"}
         LOGGER.info(f"activation checkpointing: {checkpointed_count(model)} of {len(model.layers)} layers"
                     + (" (auto: re-planned after step 1 against --ac-budget-gb)" if spec == "auto" else ""))
     LOGGER.info(f"{sum(p.numel() for p in model.parameters()) / 1e9:.3f}B parameters (this rank's shard of TP)")
@@ -613,7 +614,7 @@ def _plan_ac_layers(args, model, cfg, device, plan: dict, seq_length: int, peak_
     budget = int(args.ac_budget_gb * 1e9)
     if plan.get("p1") is None:
         n_ckpt = checkpointed_count(model)
-        per_layer = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"])
+        per_layer = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"], plan.get("regather", False))
         inp = 2 * cfg.hidden_size * args.batch_size * seq_length // max(1, plan["tp"])
         keep = _agree_max(ac_layers_for_budget(n, n_ckpt, int(peak_bytes), budget, per_layer, inp, safety=1.5),
                           device)
@@ -625,7 +626,7 @@ def _plan_ac_layers(args, model, cfg, device, plan: dict, seq_length: int, peak_
     p1, released = plan["p1"], plan["released"]
     # never below a quarter of the estimate: a step-2 peak that did not grow (a reset peak
     # counter, an allocator that freed a cache) must not release every layer
-    floor = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"]) // 4
+    floor = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"], plan.get("regather", False)) // 4
     slope = max(1, floor, (int(peak_bytes) - p1) // released)
     keep = _agree_max(ac_layers_for_budget(n, n, p1, budget, slope, 0, safety=1.05), device)
     set_checkpointed_layers(model, keep)

@@ -74,7 +74,7 @@ def test_budget_releases_what_the_headroom_holds():
     assert ac_layers_for_budget(10, 10, 1 * GB, 270 * GB, GB, 0) == 0       # everything fits
     cfg = resolve_config("meta-llama/Llama-3.1-405B")
     b = layer_activation_bytes(cfg, 4, 4096, tp=4)  # the tp 4 x dp 2 one-node recipe
-    assert 1.8e9 < b < 2.4e9
+    assert 2.3e9 < b < 2.7e9 and 1.5e9 < layer_activation_bytes(cfg, 4, 4096, tp=4, regather=True) < 1.9e9
 
 
 def test_plan_ac_layers_from_measured_peaks():
