@@ -19,9 +19,12 @@ from dtg.models import resolve_config  # noqa: E402
 HBM_GB = 288.0
 
 
-def plan(model, world=8, tp=1, strategy="fsdp", batch=1, seq=4096, ac=False, offload=False, resident_params=False):
+def plan(model, world=8, tp=1, strategy="fsdp", batch=1, seq=4096, ac=False, offload=False, resident_params=False,
+         ac_layers=None, regather=False):
     """offload: gradients + AdamW state (+ parameters unless resident_params) in host memory;
-    resident_params keeps the bf16 parameter shard in HBM and a master copy on the host."""
+    resident_params keeps the bf16 parameter shard in HBM and a master copy on the host.
+    ac_layers: with `ac`, only that many layers recompute (--ac-layers N); the others keep their
+    activations (dtg.parallel.checkpointing.layer_activation_bytes, with --sp-regather)."""
     c = resolve_config(model)
     P = c.num_params()
     H, I, L = c.hidden_size, c.intermediate_size, c.num_hidden_layers
@@ -41,6 +44,12 @@ def plan(model, world=8, tp=1, strategy="fsdp", batch=1, seq=4096, ac=False, off
     Tfull = batch * seq
     per_tok_layer = 2 * (4 * H / (tp if tp > 1 else 1)) + 2 * Tfull / T * ((nq + 2 * nkv) * d + nq * d + 3 * I) / tp
     acts = L * T * per_tok_layer if not ac else L * T * 2 * H + T * per_tok_layer
+    if ac and ac_layers is not None:  # the planner the trainer uses: kept layers' saved tensors
+        from dtg.parallel.checkpointing import layer_activation_bytes
+
+        n_ckpt = max(0, min(L, int(ac_layers)))
+        kept = layer_activation_bytes(c, batch, seq, tp, regather)
+        acts = n_ckpt * T * 2 * H + (L - n_ckpt) * kept + T * per_tok_layer
     logits = 2 * min(Tfull, (1 << 29) // max(c.vocab_size, 1)) * c.vocab_size / tp * 2
     host = 0.0
     if offload:
@@ -69,10 +78,13 @@ def main():
     ap.add_argument("--offload", action="store_true")
     ap.add_argument("--resident-params", action="store_true",
                     help="with --offload: parameter shard stays in HBM (--offload-params off / auto)")
+    ap.add_argument("--ac-layers", type=int, default=None, help="with --ac: layers that recompute (the rest keep)")
+    ap.add_argument("--regather", action="store_true", help="--sp-regather: kept layers hold local GEMM inputs")
     ap.add_argument("--exact", action="store_true",
                     help="also print the exact FSDP unit layout (dtg.parallel.plan on a meta-device model)")
     a = ap.parse_args()
-    r = plan(a.model, a.world, a.tp, a.strategy, a.batch, a.seq, a.ac, a.offload, a.resident_params)
+    r = plan(a.model, a.world, a.tp, a.strategy, a.batch, a.seq, a.ac, a.offload, a.resident_params, a.ac_layers,
+             a.regather)
     for k, v in r.items():
         print(f"{k:20s} {v:.2f}" if isinstance(v, float) else f"{k:20s} {v}")
     if a.exact and a.tp == 1:
