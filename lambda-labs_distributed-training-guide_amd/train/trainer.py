@@ -593,16 +593,18 @@ def _agree_max(value: int, device) -> int:
 
 def _plan_ac_layers(args, model, cfg, device, plan: dict, seq_length: int, peak_bytes=None) -> bool:
     """--ac-layers auto: keep checkpointed only as many layers as the HBM budget requires.
-    Measured, in two steps:
+    Measured, over the first steps:
       1. after step 1 (every layer checkpointed) the step's peak P1 is read, and layers are
-         released by the analytical per-layer size (layer_activation_bytes, x1.5: on the 405B
-         tp 4 rank a released layer measured 2.74 GB against 2.13 estimated, so step 2 must not
-         trust the estimate to the last layer);
-      2. after step 2 the peak P2 with those layers released gives the MEASURED cost of a released
-         layer, (P2 - P1) / released, and the count is re-planned from P1 with it (x1.05).
-    Peaks are the caching allocator's reserved bytes (what the HBM really holds).  Every rank
-    takes the largest count any rank needs (a recompute re-issues the layer's TP collectives).
-    `plan` carries the state between the two calls; returns True when planning is done."""
+         released by the analytical per-layer size (layer_activation_bytes, x1.5);
+      2. after step 2 the peak with those layers released gives the MEASURED cost of a released
+         layer, (P2 - P1) / released, and the count is re-planned from P1 with it (x1.05);
+      3. after steps 3 and 4, while the peak is still over the budget, the same re-plan from the
+         larger release (a peak dominated by a transient at small releases -- the loss head, a
+         gathered FSDP unit -- hides part of the per-layer cost at step 2: the 405B FSDP rank
+         measured 1.04 GB per layer there and overshot at 73 released).
+    Peaks are the caching allocator's reserved bytes (what the HBM really holds), reset at each
+    planning step.  Every rank takes the largest count any rank needs (a recompute re-issues the
+    layer's TP collectives).  `plan` carries the state between calls; returns True when done."""
     from ..parallel.checkpointing import ac_layers_for_budget, layer_activation_bytes, set_checkpointed_layers
 
     n = len(model.layers)
@@ -612,29 +614,37 @@ def _plan_ac_layers(args, model, cfg, device, plan: dict, seq_length: int, peak_
             return True
         peak_bytes = torch.cuda.max_memory_reserved(device)
     budget = int(args.ac_budget_gb * 1e9)
-    if plan.get("p1") is None:
+    est = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"], plan.get("regather", False))
+    phase = plan.get("phase", 1)
+    if phase == 1:
         n_ckpt = checkpointed_count(model)
-        per_layer = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"], plan.get("regather", False))
         inp = 2 * cfg.hidden_size * args.batch_size * seq_length // max(1, plan["tp"])
-        keep = _agree_max(ac_layers_for_budget(n, n_ckpt, int(peak_bytes), budget, per_layer, inp, safety=1.5),
-                          device)
-        set_checkpointed_layers(model, keep)
-        plan.update(p1=int(peak_bytes), released=n_ckpt - keep)
-        LOGGER.info(f"--ac-layers auto (1/2): step-1 peak {peak_bytes / 1e9:.1f} GB, budget {args.ac_budget_gb:g} GB, "
-                    f"~{per_layer / 1e9:.2f} GB per released layer (estimate) -> {keep} of {n} layers checkpointed")
-        return plan["released"] == 0
-    p1, released = plan["p1"], plan["released"]
-    # never below a quarter of the estimate: a step-2 peak that did not grow (a reset peak
-    # counter, an allocator that freed a cache) must not release every layer
-    floor = layer_activation_bytes(cfg, args.batch_size, seq_length, plan["tp"], plan.get("regather", False)) // 4
-    slope = max(1, floor, (int(peak_bytes) - p1) // released)
-    keep = _agree_max(ac_layers_for_budget(n, n, p1, budget, slope, 0, safety=1.05), device)
+        keep = _agree_max(ac_layers_for_budget(n, n_ckpt, int(peak_bytes), budget, est, inp, safety=1.5), device)
+        plan.update(p1=int(peak_bytes), released=n_ckpt - keep, phase=2)
+        msg = f"step-1 peak {peak_bytes / 1e9:.1f} GB, ~{est / 1e9:.2f} GB per released layer (estimate)"
+        done = plan["released"] == 0
+    else:
+        p1, released = plan["p1"], plan["released"]
+        # never below a quarter of the estimate: a peak that did not grow (a reset peak counter,
+        # an allocator that freed a cache) must not release every layer
+        slope = max(1, est // 4, (int(peak_bytes) - p1) // max(1, released))
+        over = int(peak_bytes) > budget
+        if phase == 2 or over:
+            keep = _agree_max(ac_layers_for_budget(n, n, p1, budget, slope, 0, safety=1.05), device)
+            keep = max(keep, n - released) if phase > 2 else keep  # later steps only re-checkpoint
+        else:
+            keep = n - released
+        plan.update(released=n - keep, phase=phase + 1)
+        msg = (f"step-{phase} peak {peak_bytes / 1e9:.1f} GB with {released} layers released -> measured "
+               f"{slope / 1e9:.2f} GB per released layer")
+        done = (phase >= 2 and not over and phase > 2) or phase >= 4 or (phase == 2 and keep == n)
     set_checkpointed_layers(model, keep)
-    if device.type == "cuda":  # hand back the blocks step 2's larger release cached
+    if device.type == "cuda":  # hand back the blocks of the trial, measure the next step afresh
         torch.cuda.empty_cache()
-    LOGGER.info(f"--ac-layers auto (2/2): step-2 peak {peak_bytes / 1e9:.1f} GB with {released} layers released -> "
-                f"measured {slope / 1e9:.2f} GB per released layer -> {keep} of {n} layers checkpointed")
-    return True
+        torch.cuda.reset_peak_memory_stats(device)
+    LOGGER.info(f"--ac-layers auto ({phase}): {msg}, budget {args.ac_budget_gb:g} GB -> {keep} of {n} layers "
+                f"checkpointed" + ("" if done else "; checked again after the next step"))
+    return done
 
 
 def _offload_info(engine) -> dict:

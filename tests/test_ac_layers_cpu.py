@@ -79,7 +79,9 @@ def test_budget_releases_what_the_headroom_holds():
 
 def test_plan_ac_layers_from_measured_peaks():
     """Step 1 (all checkpointed, peak P1) releases layers by the analytical estimate; step 2's peak
-    gives the measured cost per released layer, and the count is re-planned from P1 with it."""
+    gives the measured cost per released layer and the count is re-planned from P1 with it; step
+    3 confirms (within budget: done) or re-checkpoints (over budget: a transient hid part of the
+    cost at step 2); a peak that did not grow cannot release every layer (slope floor)."""
     import argparse
 
     from dtg.models import build_model, resolve_config
@@ -87,30 +89,44 @@ def test_plan_ac_layers_from_measured_peaks():
     from dtg.train.trainer import _plan_ac_layers
 
     cfg = resolve_config("llama-tiny", num_hidden_layers=8)
-    m = build_model(cfg, device="cpu", dtype=torch.float32)
-    apply_activation_checkpointing(m)
     per = layer_activation_bytes(cfg, 2, 128)
     inp = 2 * cfg.hidden_size * 2 * 128
     GB = 10 ** 9
     args = argparse.Namespace(batch_size=2, ac_budget_gb=(GB + 3.5 * (per - inp) * 1.5) / GB)
-    plan = {"tp": 1}
-    done = _plan_ac_layers(args, m, cfg, torch.device("cpu"), plan, 128, peak_bytes=GB)
-    assert not done and plan["released"] == 3
-    assert [layer._dtg_checkpointed for layer in m.layers] == [True] * 5 + [False] * 3
-    # the released layers really cost twice the estimate: step 2 peaks at P1 + 3 x 2 x estimate
-    real = int(2 * (per - inp) * 1.5)
-    done = _plan_ac_layers(args, m, cfg, torch.device("cpu"), plan, 128, peak_bytes=GB + 3 * real)
-    assert done
-    free = int(args.ac_budget_gb * GB) - GB
-    assert [layer._dtg_checkpointed for layer in m.layers].count(False) == free // int(real * 1.05) == 1
-    # a step-2 peak that did not grow cannot release every layer: the slope has a floor
-    m2 = build_model(cfg, device="cpu", dtype=torch.float32)
-    apply_activation_checkpointing(m2)
-    plan = {"tp": 1}
-    _plan_ac_layers(args, m2, cfg, torch.device("cpu"), plan, 128, peak_bytes=GB)
-    _plan_ac_layers(args, m2, cfg, torch.device("cpu"), plan, 128, peak_bytes=GB)
-    released = [layer._dtg_checkpointed for layer in m2.layers].count(False)
-    assert released == min(8, free // int((per // 4) * 1.05))
+    budget = int(args.ac_budget_gb * GB)
+    cpu = torch.device("cpu")
+
+    def fresh():
+        m = build_model(cfg, device="cpu", dtype=torch.float32)
+        apply_activation_checkpointing(m)
+        return m, {"tp": 1}
+
+    def released(m):
+        return [layer._dtg_checkpointed for layer in m.layers].count(False)
+
+    m, plan = fresh()
+    assert not _plan_ac_layers(args, m, cfg, cpu, plan, 128, peak_bytes=GB)
+    assert released(m) == 3 and [layer._dtg_checkpointed for layer in m.layers] == [True] * 5 + [False] * 3
+    real = int(2 * (per - inp) * 1.5)  # a released layer really costs twice the estimate
+    assert not _plan_ac_layers(args, m, cfg, cpu, plan, 128, peak_bytes=GB + 3 * real)
+    assert released(m) == (budget - GB) // int(real * 1.05) == 1
+    assert _plan_ac_layers(args, m, cfg, cpu, plan, 128, peak_bytes=GB + real)  # within budget: done
+    assert released(m) == 1
+
+    # step 3 over the budget (the step-2 slope was hidden by a transient): re-checkpoint
+    m, plan = fresh()
+    _plan_ac_layers(args, m, cfg, cpu, plan, 128, peak_bytes=GB)
+    _plan_ac_layers(args, m, cfg, cpu, plan, 128, peak_bytes=GB + 3 * (per - inp))  # looks cheap
+    n2 = released(m)
+    assert n2 > 3
+    assert not _plan_ac_layers(args, m, cfg, cpu, plan, 128, peak_bytes=budget + GB // 10)
+    assert released(m) < n2
+
+    # a step-2 peak that did not grow: the slope floor (a quarter of the estimate)
+    m, plan = fresh()
+    _plan_ac_layers(args, m, cfg, cpu, plan, 128, peak_bytes=GB)
+    _plan_ac_layers(args, m, cfg, cpu, plan, 128, peak_bytes=GB)
+    assert released(m) == min(8, (budget - GB) // int((per // 4) * 1.05))
 
 
 def _torchrun(chapter_dir, args, nproc=2, timeout=400):

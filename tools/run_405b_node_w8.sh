@@ -24,10 +24,10 @@ for d in $depths; do
   rm -rf /tmp/dtg405w8
   (cd 05-training-llama-405b && DTG_FAKE_WORLD=8 OMP_NUM_THREADS=$SHARE timeout -k 10 540 python -u train_llm.py \
      -e r405w8 -m meta-llama/Llama-3.1-405B --num-layers $d -b 1 -s 4096 -d synthetic --num-workers 1 \
-     --save-dir /tmp/dtg405w8 --ckpt-freq 100000 --max-steps 5 --log-freq 1 --cpu-offload on --offload-params off \
+     --save-dir /tmp/dtg405w8 --ckpt-freq 100000 --max-steps ${STEPS:-5} --log-freq 1 --cpu-offload on --offload-params off \
      --pin-numa on --cpu-share $SHARE --offload-grad-ring ${RING:-auto} ${EXTRA:-} > $O/ch05_405b_w8_rank0_depth$d.log 2>&1)
   rc=$?
   echo "depth=$d rc=$rc"
-  grep -E "global_step': [45]," $O/ch05_405b_w8_rank0_depth$d.log | grep -oE "'(time/forward|time/backward|time/update|time/total|peak_alloc_in_gb|offload/[a-z0-9_]+|host/[a-z_]+)': [0-9.]+" | tr '\n' ' '; echo
+  grep -E "global_step': ($(seq -s'|' $(( ${STEPS:-5} - 1 )) ${STEPS:-5}))," $O/ch05_405b_w8_rank0_depth$d.log | grep -oE "'(time/forward|time/backward|time/update|time/total|peak_alloc_in_gb|peak_resv_in_gb|ac/layers|offload/[a-z0-9_]+|host/[a-z_]+)': [0-9.]+" | tr '\n' ' '; echo
   [ $rc -eq 0 ] || { tail -30 $O/ch05_405b_w8_rank0_depth$d.log; exit $rc; }
 done
