@@ -638,10 +638,12 @@ def _plan_ac_layers(args, model, cfg, device, plan: dict, seq_length: int, peak_
         msg = (f"step-{phase} peak {peak_bytes / 1e9:.1f} GB with {released} layers released -> measured "
                f"{slope / 1e9:.2f} GB per released layer")
         done = (phase >= 2 and not over and phase > 2) or phase >= 4 or (phase == 2 and keep == n)
+    changed = keep != checkpointed_count(model)
     set_checkpointed_layers(model, keep)
-    if device.type == "cuda":  # hand back the blocks of the trial, measure the next step afresh
-        torch.cuda.empty_cache()
-        torch.cuda.reset_peak_memory_stats(device)
+    if device.type == "cuda":
+        if changed:  # hand back the blocks of the trial (re-reserving costs a step's worth of seconds)
+            torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(device)  # the next step's peak, not the trial's
     LOGGER.info(f"--ac-layers auto ({phase}): {msg}, budget {args.ac_budget_gb:g} GB -> {keep} of {n} layers "
                 f"checkpointed" + ("" if done else "; checked again after the next step"))
     return done
