@@ -20,10 +20,10 @@ for spec in $runs; do
   IFS=+ read ac rg <<< "$spec"   # e.g. "auto+rg": --ac-layers auto --sp-regather on
   extra=""; [ "$rg" = rg ] && extra="--sp-regather on"
   rm -rf /tmp/dtg405_ac
-  log=$O/ch07_405b_tp4_b4_d100_ac_${spec}.log
+  log=$O/ch07_405b_tp${TP:-4}_b${TP:-4}_d100_ac_${spec}.log
   (cd 07-2d-parallel && DTG_FAKE_WORLD=8 OMP_NUM_THREADS=$SHARE timeout -k 10 480 python -u train_llm.py \
-     -e r405_ac -m meta-llama/Llama-3.1-405B --num-layers 100 -b 4 -s 4096 -d synthetic --num-workers 1 \
-     --tp 4 --save-dir /tmp/dtg405_ac --ckpt-freq 100000 --max-steps ${STEPS:-6} --log-freq 1 --cpu-offload on \
+     -e r405_ac -m meta-llama/Llama-3.1-405B --num-layers 100 -b ${TP:-4} -s 4096 -d synthetic --num-workers 1 \
+     --tp ${TP:-4} --save-dir /tmp/dtg405_ac --ckpt-freq 100000 --max-steps ${STEPS:-6} --log-freq 1 --cpu-offload on \
      --offload-params off --activation-checkpointing on --ac-layers $ac --ac-budget-gb ${BUDGET:-256} \
      --pin-numa on --cpu-share $SHARE $extra > $log 2>&1)
   rc=$?
