@@ -15,8 +15,6 @@
 
 #include "common.h"
 
-#include <cstring>
-
 namespace dtg {
 
 template <typename T>
@@ -171,12 +169,10 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   h.grad_scale = grad_scale;
   const int threads = 256;
   const int64_t want = (n + threads * 8 - 1) / (threads * 8);
-  // DTG_ADAM_UNROLL = 2 | 4 (vectors per lane per iteration), DTG_ADAM_WG_PER_CU: grid size
-  // (A/B knobs, tools/bench_kernels.py); read per call so a benchmark can switch in-process.
-  const char* ue = std::getenv("DTG_ADAM_UNROLL");
-  const char* we = std::getenv("DTG_ADAM_WG_PER_CU");
-  const int unroll = (ue && std::atoi(ue) == 4) ? 4 : 2;
-  const int wg_per_cu = we ? std::max(1, std::atoi(we)) : 16;
+  // 2 vectors per lane per iteration, up to 16 workgroups per CU: unroll 2 / 4 x 4-32 workgroups
+  // per CU span 5.04-5.41 TB/s, 16 and 32 within 2 % (profiles/r3/s08/kernels.log); the knobs
+  // were removed in round 6
+  constexpr int unroll = 2, wg_per_cu = 16;
   const int blocks = (int)std::min<int64_t>(want, 256 * wg_per_cu);
   float* mp = has_master ? master->data_ptr<float>() : nullptr;
   const bool gb = g.scalar_type() == at::kBFloat16;
@@ -187,10 +183,7 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   const bool vec = (n % 8 == 0) && aligned(p) && aligned(g) && aligned(m) && aligned(v) &&
                    (!has_master || aligned(*master));
 #define DTG_ADAM_LAUNCH(GT, ST, MASTER)                                                      \
-  do { if (vec && unroll == 4) adamw_kernel<GT, ST, MASTER, true, 4><<<blocks, threads, 0, stream()>>>( \
-      bf16_mut(p), mp, reinterpret_cast<const GT*>(g.data_ptr()), reinterpret_cast<ST*>(m.data_ptr()), \
-      reinterpret_cast<ST*>(v.data_ptr()), n, h, hp);                                       \
-  else if (vec) adamw_kernel<GT, ST, MASTER, true, 2><<<blocks, threads, 0, stream()>>>(            \
+  do { if (vec) adamw_kernel<GT, ST, MASTER, true, unroll><<<blocks, threads, 0, stream()>>>(       \
       bf16_mut(p), mp, reinterpret_cast<const GT*>(g.data_ptr()), reinterpret_cast<ST*>(m.data_ptr()), \
       reinterpret_cast<ST*>(v.data_ptr()), n, h, hp);                                       \
   else adamw_kernel<GT, ST, MASTER, false><<<blocks, threads, 0, stream()>>>(               \
@@ -219,13 +212,9 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
 // of W per step), this kernel writes W^T while the updated W is still in registers: the read is
 // saved, the write moves here.  The flat buffer is described as a list of matrices (2-D params;
 // 1-D params as [1, n] rows with no transposed copy); the grid walks 64 x TC tiles of all of
-// them: phase 1 updates the tile row-wise with 16-byte vectors and parks the new bf16 values in
-// LDS, phase 2 writes the tile's columns as rows of W^T (16-byte vectors again).
-//
-// TC (tile columns) sets the access pattern: every phase-1 row segment is TC x 2 bytes of each
-// of the six streams (p, g, m, v in; p, m, v out), every W^T segment 128 bytes.  64-column tiles
-// read 128-byte segments of 64 different rows per array; 128 / 256 columns read 256 / 512-byte
-// segments (NT = 256 / 512 threads keep four vectors per lane).
+// them, one tile per workgroup (TC = 64 | 128 | 256 columns; the engines use 256).  An LDS-staged
+// form (update row-wise, park the tile in LDS, write its columns as W^T rows) ran 5.54 TB/s at
+// its best tile against this kernel's 5.98 (profiles/r5/transpose/) and was removed in round 6.
 // ------------------------------------------------------------------------------------------
 struct MatDesc {
   int64_t off, rows, cols, toff, tile0;  // toff < 0: no transposed copy
@@ -234,7 +223,7 @@ struct MatDesc {
 constexpr int kAtRows = 64;
 
 // Eight raw elements of a buffer, converted to f32 only when the update runs (bf16 vectors stay
-// packed in 4 VGPRs while their loads are in flight under the previous tile's store phase).
+// packed in 4 VGPRs while their loads are in flight).
 template <typename T>
 struct Raw8;
 template <>
@@ -253,124 +242,8 @@ struct Raw8<float> {
   __device__ __forceinline__ float operator[](int j) const { return j < 4 ? a[j] : b[j - 4]; }
 };
 
-template <typename ST, bool MASTER, int TC, int NT>
-__global__ __launch_bounds__(NT) void adamw_t_kernel(uint16_t* __restrict__ p, float* __restrict__ master,
-                                                     const uint16_t* __restrict__ g, ST* __restrict__ m,
-                                                     ST* __restrict__ v, uint16_t* __restrict__ pt,
-                                                     const MatDesc* __restrict__ mats, int nmats, int64_t ntiles,
-                                                     AdamHyper h, const float* __restrict__ dev_hyper) {
-  constexpr int kPitch = TC + 2;          // halfwords; odd dword pitch spreads the column gathers
-  constexpr int kVR = TC / 8;             // 16-byte vectors per tile row
-  constexpr int kNP = kAtRows * kVR / NT; // phase-1 vectors per lane
-  constexpr int kOutPerPass = NT / 8;     // W^T rows written per phase-2 pass (8 vectors each)
-  static_assert(kAtRows * kVR % NT == 0 && TC % kOutPerPass == 0, "tile shape");
-  using PT = typename std::conditional<MASTER, float, uint16_t>::type;
-  __shared__ uint16_t tile[kAtRows * kPitch];
-  if (dev_hyper != nullptr) {
-    h.lr = dev_hyper[0];
-    h.bc1 = dev_hyper[1];
-    h.bc2_sqrt = dev_hyper[2];
-  }
-  const float step_size = h.lr / h.bc1;
-  const float decay = 1.f - h.lr * h.wd;
-  const int tid = threadIdx.x;
-  int lo = 0;  // the matrix of tile t: tiles are walked in increasing order, so it only advances
-  {
-    int hi = nmats - 1;  // binary search for this block's first tile
-    const int64_t t0 = blockIdx.x;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (mats[mid].tile0 <= t0) lo = mid; else hi = mid - 1;
-    }
-  }
-  // Software pipeline: tile t+G's operand vectors are loaded before tile t's transposed store
-  // phase (and its two barriers), so their HBM latency overlaps it.
-  Raw8<PT> pr[kNP];
-  Raw8<uint16_t> gr[kNP];
-  Raw8<ST> mr[kNP], vr[kNP];
-  int64_t kk[kNP];
-  MatDesc md;
-  int64_t r0 = 0, c0 = 0;
-  auto locate = [&](int64_t t) {
-    while (lo + 1 < nmats && mats[lo + 1].tile0 <= t) ++lo;
-    md = mats[lo];
-    const int64_t lt = t - md.tile0;
-    const int64_t ntc = (md.cols + TC - 1) / TC;
-    r0 = (lt / ntc) * kAtRows;
-    c0 = (lt % ntc) * TC;
-  };
-  auto fetch = [&]() {
-#pragma unroll
-    for (int i = 0; i < kNP; ++i) {
-      const int id = tid + NT * i;
-      const int64_t r = r0 + id / kVR, c = c0 + (id % kVR) * 8;
-      kk[i] = (r < md.rows && c < md.cols) ? md.off + r * md.cols + c : -1;
-      if (kk[i] >= 0) {
-        if constexpr (MASTER) pr[i].load(master + kk[i]); else pr[i].load(p + kk[i]);
-        gr[i].load(g + kk[i]);
-        mr[i].load(m + kk[i]);
-        vr[i].load(v + kk[i]);
-      }
-    }
-  };
-  int64_t t = blockIdx.x;
-  if (t < ntiles) {
-    locate(t);
-    fetch();
-  }
-  for (; t < ntiles; t += gridDim.x) {
-    const MatDesc cur = md;
-    const int64_t cr0 = r0, cc0 = c0;
-#pragma unroll
-    for (int i = 0; i < kNP; ++i) {
-      const int id = tid + NT * i;
-      uint32_t* dst = reinterpret_cast<uint32_t*>(tile + (id / kVR) * kPitch + (id % kVR) * 8);
-      if (kk[i] >= 0) {
-        float pv[8], mv[8], vv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pv[j] = pr[i][j];
-          mv[j] = mr[i][j];
-          vv[j] = vr[i][j];
-          adam_elem(pv[j], gr[i][j] * h.grad_scale, mv[j], vv[j], h, step_size, decay);
-        }
-        st8<ST>(m + kk[i], mv);
-        st8<ST>(v + kk[i], vv);
-        if (MASTER) st8<float>(master + kk[i], pv);
-        u16x8 pb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = f2bf(pv[j]);
-        *reinterpret_cast<u16x8*>(p + kk[i]) = pb;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dst[j] = (uint32_t)pb[2 * j] | ((uint32_t)pb[2 * j + 1] << 16);
-      }
-    }
-    const int64_t tn = t + gridDim.x;
-    if (tn < ntiles) {  // next tile's loads in flight under this tile's transposed store
-      locate(tn);
-      fetch();
-    }
-    if (cur.toff >= 0) {
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < TC / kOutPerPass; ++i) {
-        const int oc = tid / 8 + kOutPerPass * i, orr = (tid % 8) * 8;  // input column -> W^T row
-        const int64_t c = cc0 + oc, r = cr0 + orr;
-        if (c < cur.cols && r < cur.rows) {
-          u16x8 o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = tile[(orr + j) * kPitch + oc];
-          *reinterpret_cast<u16x8*>(pt + cur.toff + c * cur.rows + r) = o;
-        }
-      }
-    }
-    __syncthreads();  // the tile buffer is reused by this block's next tile
-  }
-}
-
-// Register-blocked form (the default; DTG_ADAMT_KERNEL=lds selects the kernel above): no LDS, no barriers.  The same
-// 64 x TC tile walk (one tile per workgroup of TC threads, i.e. TC / 64 waves); every lane owns an
-// 8 x 8 block: eight 16-B row vectors of p, g, m, v in, the update in f32, p / m / v rows out,
+// Register-blocked: no LDS, no barriers.  One 64 x TC tile per workgroup of TC threads (TC / 64
+// waves); every lane owns an 8 x 8 block: eight 16-B row vectors of p, g, m, v in, the update in f32, p / m / v rows out,
 // and -- for a matrix with a transposed copy -- the updated block through an in-register 8 x 8
 // transpose (transpose8x8) to eight 16-B rows of W^T.  Eight lanes cover 128 contiguous bytes of
 // every row they load or store.  Matrices with a W^T have rows and columns that are multiples of
@@ -491,11 +364,7 @@ void adamw_t_(const at::Tensor& p, const c10::optional<at::Tensor>& master, cons
   uint16_t* ptp = bf16_mut(pt);
   const bool sb = m.scalar_type() == at::kBFloat16;
   DTG_CHECK(sb || m.scalar_type() == at::kFloat, "adamw_t_: states must be bf16 or f32");
-  // default: the register-blocked kernel (5.98 vs 5.54 TB/s over 8 Llama-3-8B layers against the
-  // LDS kernel at its best tile, profiles/r5/transpose/); DTG_ADAMT_KERNEL=lds selects the LDS one
-  const char* ke = std::getenv("DTG_ADAMT_KERNEL");  // per call: A/B runs switch it in-process
-  if (ke == nullptr || std::strcmp(ke, "lds") != 0) {
-    DTG_CHECK(ntiles < (int64_t(1) << 31), "adamw_t_: too many tiles");
+  DTG_CHECK(ntiles < (int64_t(1) << 31), "adamw_t_: too many tiles");
 #define DTG_ADAMT_REG(ST, MASTER, TC)                                                                       \
   adamw_t_reg_kernel<ST, MASTER, TC><<<(unsigned)ntiles, TC, 0, stream()>>>(                                \
       bf16_mut(p), mp, gp, reinterpret_cast<ST*>(m.data_ptr()), reinterpret_cast<ST*>(v.data_ptr()), ptp, md, nm, \
@@ -506,33 +375,13 @@ void adamw_t_(const at::Tensor& p, const c10::optional<at::Tensor>& master, cons
     else if (tile_cols == 128) DTG_ADAMT_REG(ST, MASTER, 128);        \
     else DTG_ADAMT_REG(ST, MASTER, 256);                              \
   } while (0)
-    if (has_master) {
-      if (sb) DTG_ADAMT_REG_TC(uint16_t, true); else DTG_ADAMT_REG_TC(float, true);
-    } else {
-      if (sb) DTG_ADAMT_REG_TC(uint16_t, false); else DTG_ADAMT_REG_TC(float, false);
-    }
+  if (has_master) {
+    if (sb) DTG_ADAMT_REG_TC(uint16_t, true); else DTG_ADAMT_REG_TC(float, true);
+  } else {
+    if (sb) DTG_ADAMT_REG_TC(uint16_t, false); else DTG_ADAMT_REG_TC(float, false);
+  }
 #undef DTG_ADAMT_REG_TC
 #undef DTG_ADAMT_REG
-    DTG_LAUNCH_CHECK();
-    return;
-  }
-#define DTG_ADAMT_LAUNCH(ST, MASTER, TC, NT)                                                              \
-  adamw_t_kernel<ST, MASTER, TC, NT><<<(int)std::min<int64_t>(ntiles, 256 * 32 * 256 / NT), NT, 0, stream()>>>( \
-      bf16_mut(p), mp, gp, reinterpret_cast<ST*>(m.data_ptr()), reinterpret_cast<ST*>(v.data_ptr()), ptp, md, nm, \
-      ntiles, h, hp)
-#define DTG_ADAMT_TILES(ST, MASTER)                                    \
-  do {                                                                 \
-    if (tile_cols == 64) DTG_ADAMT_LAUNCH(ST, MASTER, 64, 256);        \
-    else if (tile_cols == 128) DTG_ADAMT_LAUNCH(ST, MASTER, 128, 256); \
-    else DTG_ADAMT_LAUNCH(ST, MASTER, 256, 512);                       \
-  } while (0)
-  if (has_master) {
-    if (sb) DTG_ADAMT_TILES(uint16_t, true); else DTG_ADAMT_TILES(float, true);
-  } else {
-    if (sb) DTG_ADAMT_TILES(uint16_t, false); else DTG_ADAMT_TILES(float, false);
-  }
-#undef DTG_ADAMT_TILES
-#undef DTG_ADAMT_LAUNCH
   DTG_LAUNCH_CHECK();
 }
 

@@ -100,29 +100,6 @@ inline uint16_t* bf16_mut(const at::Tensor& t) { return reinterpret_cast<uint16_
   DTG_CHECK((t).is_cuda() && (t).scalar_type() == at::kBFloat16, #t " must be a bf16 GPU tensor")
 #define DTG_LAUNCH_CHECK() C10_HIP_KERNEL_LAUNCH_CHECK()
 
-// Workgroup -> (row tile, column tile) for the tile-transposing streaming kernels.  gc == 0:
-// the 2-D grid's own (blockIdx.y, blockIdx.x).  gc > 0: a 1-D grid walked in bands of gc
-// column tiles, row tiles fastest inside a band, so the workgroups resident at one time read
-// gc * TC-wide row segments and write long contiguous runs of each transposed output row
-// (a wide [T, 28672] source otherwise has every resident workgroup writing 128 B into a
-// different output row).
-__device__ __forceinline__ void tile_coords(int gc, int64_t n_row_tiles, int64_t n_col_tiles, int64_t& rt,
-                                            int64_t& ct) {
-  if (gc <= 0) {
-    rt = blockIdx.y;
-    ct = blockIdx.x;
-    return;
-  }
-  const int64_t pid = blockIdx.x;
-  const int64_t per_band = (int64_t)gc * n_row_tiles;
-  const int64_t band = pid / per_band;
-  const int64_t first = band * gc;
-  const int64_t width = n_col_tiles - first < gc ? n_col_tiles - first : gc;
-  const int64_t in = pid - band * per_band;
-  rt = in / width;
-  ct = first + in % width;
-}
-
 // 8 x 8 transpose of 16-bit values held in registers: v[i] = row i on entry, column i on exit.
 // Three butterfly stages (elements, pairs, quads); only the first needs byte permutes, the other
 // two move whole dwords.
@@ -146,21 +123,15 @@ __device__ __forceinline__ void transpose8x8(u16x8 (&v)[8]) {
   }
 }
 
-constexpr int kDefaultTileGroup = 0;
-
-// Column-band width for tile_coords (DTG_TILE_GROUP, read per call; 0 = 2-D grid).
-inline int tile_group_env(int dflt) {
-  const char* e = std::getenv("DTG_TILE_GROUP");
-  return e ? std::atoi(e) : dflt;
-}
-
-inline dim3 tile_grid(int gc, int64_t n_row_tiles, int64_t n_col_tiles) {
-  if (gc <= 0) {
-    DTG_CHECK(n_row_tiles <= 65535, "tile grid: too many row tiles");
-    return dim3((unsigned)n_col_tiles, (unsigned)n_row_tiles);
-  }
-  DTG_CHECK(n_row_tiles * n_col_tiles < (int64_t(1) << 31), "tile grid: too many tiles");
-  return dim3((unsigned)(n_row_tiles * n_col_tiles));
+// Grid of the tile-transposing streaming kernels: blockIdx.x = column tile (fastest, so the
+// workgroups resident at one time read neighbouring segments of the same source rows),
+// blockIdx.y = row tile.  A banded 1-D tile walk (column tiles grouped so that the transposed
+// output rows are written in long runs) gained 4-8 % on a lone [T, 28672] transpose, was mixed
+// on the SwiGLU backward and moved the 8B step < 0.5 % (profiles/r1/s62_tile_order_ab.md); it
+// was removed in round 6 with the other opt-in tilings.
+inline dim3 tile_grid(int64_t n_row_tiles, int64_t n_col_tiles) {
+  DTG_CHECK(n_row_tiles <= 65535 && n_col_tiles < (int64_t(1) << 31), "tile grid: too many tiles");
+  return dim3((unsigned)n_col_tiles, (unsigned)n_row_tiles);
 }
 
 }  // namespace dtg

@@ -5,9 +5,6 @@
 //
 // One fused GEMM replaces the two HF Linear calls; this kernel reads gu once and writes h
 // once (forward) and reads dh + gu once to write dgu (backward).  f32 math, one rounding.
-#include <cstdlib>
-#include <cstring>
-
 #include "common.h"
 
 namespace dtg {
@@ -58,14 +55,17 @@ __global__ void swiglu_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_
 //   hT   [I, T]    (h = silu(g) * u recomputed from gu, for dW_down = dY^T @ h)
 // One workgroup owns a TT-token x TF-feature tile: 16-byte row loads of g, u, dh (TF x 2-byte
 // segments of TT token rows); the three transposed tiles are staged through LDS (pitch TF + 2
-// halfwords) and stored as 16-byte columns (TT x 2-byte segments of TF feature rows).  Segment
-// length is what the tile shape buys: 128-byte segments (64 x 64) leave HBM well short of its
-// streaming rate, 256-byte ones recover most of it (the adamw_t_ tile measurements, r3_s07).
+// halfwords) and stored as 16-byte columns (TT x 2-byte segments of TF feature rows).
+// 64 x 128 is the measured best of the 64/128 x 64/128 tiles and of a register-blocked 8 x 8
+// form (-2.1 ms per 8B step against 64 x 64, profiles/r3_s32; 4.64 vs 4.52 TB/s against the
+// register-blocked one, profiles/r5/transpose/); the others were removed in round 6.
+constexpr int kSgTT = 64, kSgTF = 128;
+
 template <int TT, int TF>
 __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
     const uint16_t* __restrict__ dh, const uint16_t* __restrict__ gu, int64_t gu_stride,
-    uint16_t* __restrict__ dgu, uint16_t* __restrict__ dguT, uint16_t* __restrict__ hT, int64_t T, int I, int gc) {
-  static_assert((TT == 64 || TT == 128) && (TF == 64 || TF == 128), "tile");
+    uint16_t* __restrict__ dgu, uint16_t* __restrict__ dguT, uint16_t* __restrict__ hT, int64_t T, int I) {
+  static_assert(TT == 64 && TF == 128, "tile");
   constexpr int kPitch = TF + 2;
   constexpr int kVF = TF / 8;                 // 16-byte vectors per token row of the tile
   constexpr int kRowsPerPass = 256 / kVF;     // token rows per phase-1 pass
@@ -75,10 +75,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
   uint16_t* s_dg = smem;
   uint16_t* s_du = smem + TT * kPitch;
   uint16_t* s_h = smem + 2 * TT * kPitch;
-  int64_t rt, ct;
-  tile_coords(gc, (T + TT - 1) / TT, (I + TF - 1) / TF, rt, ct);
-  const int64_t t0 = rt * TT;
-  const int c0 = (int)ct * TF;
+  const int64_t t0 = (int64_t)blockIdx.y * TT;
+  const int c0 = (int)blockIdx.x * TF;
   const int tid = threadIdx.x;
   // all loads of the tile first (3 x TT*TF/2048 vectors per lane in flight), then the math
   constexpr int kNP = TT / kRowsPerPass;
@@ -146,58 +144,6 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
   }
 }
 
-// Register-blocked form (DTG_SWIGLU_TILE=reg): no LDS.  Every lane owns an 8-token x 8-feature
-// block -- 16-B row loads of g, u and dh, f32 math, 16-B row stores of dg and du, then the three
-// transposed outputs through an in-register 8 x 8 transpose (transpose8x8) as 16-B column stores.
-// A wave's 64 lanes cover 64 tokens x 64 features (8 lanes per 128 contiguous bytes of every row
-// they load or store); 4 waves per workgroup cover 128 x 128.
-__global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(
-    const uint16_t* __restrict__ dh, const uint16_t* __restrict__ gu, int64_t gu_stride,
-    uint16_t* __restrict__ dgu, uint16_t* __restrict__ dguT, uint16_t* __restrict__ hT, int64_t T, int I, int gc) {
-  int64_t rt, ct;
-  tile_coords(gc, (T + 127) / 128, (I + 127) / 128, rt, ct);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t t0 = rt * 128 + (w >> 1) * 64 + (lane >> 3) * 8;  // first token of this lane's block
-  const int c0 = (int)ct * 128 + (w & 1) * 64 + (lane & 7) * 8;    // and first feature
-  if (t0 >= T || c0 >= I) return;  // T and I are multiples of 8: a block is wholly in or out
-  u16x8 vg[8], vu[8], vd[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint16_t* row = gu + (t0 + i) * gu_stride + c0;
-    vg[i] = *reinterpret_cast<const u16x8*>(row);
-    vu[i] = *reinterpret_cast<const u16x8*>(row + I);
-    vd[i] = *reinterpret_cast<const u16x8*>(dh + (t0 + i) * I + c0);
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    u16x8 dg, du, h;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float g = bf2f(vg[i][j]), u = bf2f(vu[i][j]), d = bf2f(vd[i][j]);
-      const float sg = sigmoidf_(g);
-      const float silu = g * sg;
-      du[j] = f2bf(d * silu);
-      dg[j] = f2bf(d * u * sg * (1.f + g * (1.f - sg)));
-      h[j] = f2bf(silu * u);
-    }
-    uint16_t* o = dgu + (t0 + i) * 2 * I + c0;
-    *reinterpret_cast<u16x8*>(o) = dg;
-    *reinterpret_cast<u16x8*>(o + I) = du;
-    vg[i] = dg;  // the inputs of row i are dead: reuse their registers for the outputs
-    vu[i] = du;
-    vd[i] = h;
-  }
-  transpose8x8(vg);
-  transpose8x8(vu);
-  transpose8x8(vd);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    *reinterpret_cast<u16x8*>(dguT + (int64_t)(c0 + j) * T + t0) = vg[j];
-    *reinterpret_cast<u16x8*>(dguT + (int64_t)(I + c0 + j) * T + t0) = vu[j];
-    *reinterpret_cast<u16x8*>(hT + (int64_t)(c0 + j) * T + t0) = vd[j];
-  }
-}
-
 std::tuple<at::Tensor, at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& dh_, const at::Tensor& gu) {
   auto dh = dh_.contiguous();
   DTG_CHECK_CUDA_BF16(gu);
@@ -212,39 +158,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& dh
   auto dguT = at::empty({2 * I, T}, gu.options());
   auto hT = at::empty({I, T}, gu.options());
   if (T == 0 || I == 0) return {dgu, dguT, hT};
-  // DTG_SWIGLU_TILE = TTxTF (64x64 | 64x128 | 128x64 | 128x128): token x feature tile (A/B knob;
-  // read per call so tests and benchmarks switch it in-process)
-  // Default 64 x 128: -2.1 ms per 8B step against 64 x 64, three alternating same-box pairs
-  // (profiles/r3_s32; the parser had dropped "64x128" before, so round 3's first A/B never ran it).
-  const char* te = std::getenv("DTG_SWIGLU_TILE");
-  int tt = 64, tf = 128;
-  if (te) {
-    if (!std::strcmp(te, "64x64")) tt = 64, tf = 64;
-    else if (!std::strcmp(te, "64x128")) tt = 64, tf = 128;
-    else if (!std::strcmp(te, "128x64")) tt = 128, tf = 64;
-    else if (!std::strcmp(te, "128x128")) tt = 128, tf = 128;
-  }
-  const int gc = tile_group_env(kDefaultTileGroup);
-  if (te && !std::strcmp(te, "reg")) {
-    swiglu_bwd_t_reg_kernel<<<tile_grid(gc, (T + 127) / 128, (I + 127) / 128), 256, 0, stream()>>>(
-        bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu), bf16_mut(dguT), bf16_mut(hT), T, I, gc);
-    DTG_LAUNCH_CHECK();
-    return {dgu, dguT, hT};
-  }
-  const dim3 grid = tile_grid(gc, (T + tt - 1) / tt, (I + tf - 1) / tf);
-  const size_t lds = 3 * (size_t)tt * (tf + 2) * sizeof(uint16_t);
-#define DTG_SG_LAUNCH(TT_, TF_)                                                                            \
-  do {                                                                                                     \
-    auto fn = swiglu_bwd_t_kernel<TT_, TF_>;                                                               \
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-    fn<<<grid, 256, lds, stream()>>>(bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu), bf16_mut(dguT),  \
-                                     bf16_mut(hT), T, I, gc);                                              \
-  } while (0)
-  if (tt == 64 && tf == 64) DTG_SG_LAUNCH(64, 64);
-  else if (tt == 64) DTG_SG_LAUNCH(64, 128);
-  else if (tf == 64) DTG_SG_LAUNCH(128, 64);
-  else DTG_SG_LAUNCH(128, 128);
-#undef DTG_SG_LAUNCH
+  const size_t lds = 3 * (size_t)kSgTT * (kSgTF + 2) * sizeof(uint16_t);
+  swiglu_bwd_t_kernel<kSgTT, kSgTF><<<tile_grid((T + kSgTT - 1) / kSgTT, (I + kSgTF - 1) / kSgTF), 256, lds, stream()>>>(
+      bf16_ptr(dh), bf16_ptr(gu), gu.stride(0), bf16_mut(dgu), bf16_mut(dguT), bf16_mut(hT), T, I);
   DTG_LAUNCH_CHECK();
   return {dgu, dguT, hT};
 }

@@ -1,4 +1,4 @@
-// bf16 2-D transpose through LDS: out[c, r] = x[r, c]  (x: [R, C] with row stride ldx).
+// bf16 2-D transpose: out[c, r] = x[r, c]  (x: [R, C] with row stride ldx).
 //
 // Why it exists: hipBLASLt's MFMA kernels run 25-40 % faster when both GEMM operands are
 // K-contiguous ("TN").  A Linear layer's weight gradient dW = dY^T X reduces over the token
@@ -6,71 +6,22 @@
 // gradient dX = dY W reads W along its strided dimension.  Transposing dY / X / W into
 // K-contiguous copies costs one streaming read + write each, far less than the GEMM time it
 // buys back on the big layers (tools/bench_gemm_layouts.py, profiles/).
-//
-// Loads and stores are 16 B per lane (8 bf16) along the contiguous dimension of each side; the
-// LDS tile is padded by one dword per row so the column-wise LDS gathers of the store phase
-// spread over the banks.
 #include "common.h"
-
-#include <cstdlib>
 
 namespace dtg {
 
-// Tiles are TR (input rows = tokens) x TC (input columns) with 256 threads; each side moves
-// 16-byte vectors along its contiguous dimension.  64 x 64 (DTG_TRANSPOSE_TILE=64) and 128 x 128 tiles
-// (DTG_TRANSPOSE_TILE=128: 256-B output row segments) measured equal on the full 8B step
-// (same-box A/B, profiles/r1_s36_*); the wide [T, 2I] case alone favours 128 by ~3 %.
-template <int TR, int TC>
-__global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ x, int64_t ldx,
-                                                             uint16_t* __restrict__ out, int64_t R, int64_t C,
-                                                             int gc) {
-  constexpr int P = TC + 2;             // LDS pitch in halfwords (odd dword count)
-  constexpr int LV = TR * TC / 8 / 256; // 16-byte vectors per thread, each phase
-  __shared__ uint16_t tile[TR * P];
-  int64_t rt, ct;
-  tile_coords(gc, (R + TR - 1) / TR, (C + TC - 1) / TC, rt, ct);
-  const int64_t r0 = rt * TR;
-  const int64_t c0 = ct * TC;
-  const int tid = threadIdx.x;
-  constexpr int VPR = TC / 8;  // vectors per input row
-  constexpr int VPC = TR / 8;  // vectors per output row
-#pragma unroll
-  for (int i = 0; i < LV; ++i) {
-    const int id = tid + 256 * i;
-    const int lr = id / VPR, lc = (id % VPR) * 8;
-    const int64_t r = r0 + lr, c = c0 + lc;
-    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (r < R && c < C) v = *reinterpret_cast<const u16x8*>(x + r * ldx + c);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(tile + lr * P + lc);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dst[j] = (uint32_t)v[2 * j] | ((uint32_t)v[2 * j + 1] << 16);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < LV; ++i) {
-    const int id = tid + 256 * i;
-    const int oc = id / VPC, orr = (id % VPC) * 8;  // input column -> output row; first input row
-    const int64_t c = c0 + oc, r = r0 + orr;
-    u16x8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = tile[(orr + j) * P + oc];
-    if (c < C && r < R) *reinterpret_cast<u16x8*>(out + c * R + r) = v;
-  }
-}
-
-// Register-blocked transpose (DTG_TRANSPOSE_TILE=reg): no LDS.  Every lane moves one 8 x 8 block
-// -- eight 16-B row loads, an in-register transpose, eight 16-B column stores -- and a wave's 64
+// Register-blocked: no LDS, no barrier.  Every lane moves one 8 x 8 block -- eight 16-B row
+// loads, an in-register transpose (transpose8x8), eight 16-B column stores -- and a wave's 64
 // lanes cover a 64 x 64 tile (4 waves: 128 x 128 per workgroup).  Eight lanes read 128
 // contiguous bytes of one input row per load instruction, and eight lanes write 128 contiguous
-// bytes of one output row per store instruction.
+// bytes of one output row per store instruction.  Against the LDS-tiled kernels it replaced
+// (64 x 64 and 128 x 128 tiles, removed in round 6): +2 % on [T, 4096], +12 % on [T, 28672]
+// (profiles/r5/transpose/).
 __global__ __launch_bounds__(256) void transpose_bf16_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx,
-                                                                 uint16_t* __restrict__ out, int64_t R, int64_t C,
-                                                                 int gc) {
-  int64_t rt, ct;
-  tile_coords(gc, (R + 127) / 128, (C + 127) / 128, rt, ct);
+                                                                 uint16_t* __restrict__ out, int64_t R, int64_t C) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t r = rt * 128 + (w >> 1) * 64 + (lane >> 3) * 8;  // this lane's first input row
-  const int64_t c = ct * 128 + (w & 1) * 64 + (lane & 7) * 8;    // and first input column
+  const int64_t r = (int64_t)blockIdx.y * 128 + (w >> 1) * 64 + (lane >> 3) * 8;  // this lane's first input row
+  const int64_t c = (int64_t)blockIdx.x * 128 + (w & 1) * 64 + (lane & 7) * 8;    // and first input column
   if (r >= R || c >= C) return;  // R and C are multiples of 8: a block is wholly in or out
   u16x8 v[8];
 #pragma unroll
@@ -90,22 +41,8 @@ at::Tensor transpose2d(const at::Tensor& x) {
   const c10::DeviceGuard g(x.device());
   auto out = at::empty({C, R}, x.options());
   if (R == 0 || C == 0) return out;
-  const char* te = std::getenv("DTG_TRANSPOSE_TILE");  // per call: tests and A/B runs switch it in-process
-  // default: the register-blocked kernel (+2 % on [T, 4096], +12 % on [T, 28672] against the
-  // 64 x 64 LDS tile, same-process A/B in profiles/r5/transpose/)
-  const bool reg = te == nullptr || te[0] == 'r';
-  const int tile = reg ? 0 : std::atoi(te);
-  const int gc = tile_group_env(kDefaultTileGroup);
-  if (reg) {
-    const dim3 grid = tile_grid(gc, (R + 127) / 128, (C + 127) / 128);
-    transpose_bf16_reg_kernel<<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C, gc);
-  } else if (tile == 64) {
-    const dim3 grid = tile_grid(gc, (R + 63) / 64, (C + 63) / 64);
-    transpose_bf16_kernel<64, 64><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C, gc);
-  } else {
-    const dim3 grid = tile_grid(gc, (R + 127) / 128, (C + 127) / 128);
-    transpose_bf16_kernel<128, 128><<<grid, 256, 0, stream()>>>(bf16_ptr(x), x.stride(0), bf16_mut(out), R, C, gc);
-  }
+  transpose_bf16_reg_kernel<<<tile_grid((R + 127) / 128, (C + 127) / 128), 256, 0, stream()>>>(
+      bf16_ptr(x), x.stride(0), bf16_mut(out), R, C);
   DTG_LAUNCH_CHECK();
   return out;
 }

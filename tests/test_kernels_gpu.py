@@ -82,12 +82,8 @@ def test_swiglu(cuda):
     _close(dops.swiglu_bwd(dh.to(cuda), gu.to(cuda)), dops.swiglu_bwd(dh, gu), 3e-2, 2e-2, "swiglu bwd")
 
 
-@pytest.mark.parametrize("tile", ["64", "128", "reg"])
-@pytest.mark.parametrize("group", ["0", "3", "16"])
 @pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (4096, 6144, 6144), (1000, 520, 528), (8, 8, 8), (136, 7000, 7000)])
-def test_transpose2d(cuda, R, C, ld, group, tile, monkeypatch):
-    monkeypatch.setenv("DTG_TILE_GROUP", group)  # 2-D grid, and banded 1-D grids (ragged last band)
-    monkeypatch.setenv("DTG_TRANSPOSE_TILE", tile)
+def test_transpose2d(cuda, R, C, ld):
     x = torch.randn(R, ld).bfloat16()[:, :C]
     y = dops.transpose2d(x.to(cuda))
     assert y.shape == (C, R) and y.is_contiguous()
@@ -120,12 +116,8 @@ def test_transpose_mats_batched(cuda):
         torch.ops.dtg.transpose_mats_(x.to(cuda), out, bad.to(cuda), bad, t0)
 
 
-@pytest.mark.parametrize("group", ["0", "3", "16"])
-@pytest.mark.parametrize("tile", ["64x64", "64x128", "128x64", "128x128", "reg"])
-@pytest.mark.parametrize("T,I", [(64, 64), (4096, 1792), (520, 136)])
-def test_swiglu_bwd_t(cuda, T, I, tile, group, monkeypatch):
-    monkeypatch.setenv("DTG_SWIGLU_TILE", tile)
-    monkeypatch.setenv("DTG_TILE_GROUP", group)
+@pytest.mark.parametrize("T,I", [(64, 64), (4096, 1792), (520, 136), (8, 8)])
+def test_swiglu_bwd_t(cuda, T, I):
     torch.manual_seed(0)
     gu = (2 * torch.randn(T, 2 * I)).bfloat16()
     dh = torch.randn(T, I).bfloat16()
@@ -244,14 +236,12 @@ def test_adamw(cuda, state_dtype, master, n):
         assert (tp.detach().float() - pm.float()).abs().max().item() <= 2 * 2**-7 * tp.detach().float().abs().max().item()
 
 
-@pytest.mark.parametrize("kernel", ["lds", "reg"])
 @pytest.mark.parametrize("tile_cols", [64, 128, 256])
 @pytest.mark.parametrize("state_dtype,master", [(torch.bfloat16, False), (torch.float32, True)])
-def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master, tile_cols, kernel, monkeypatch):
-    """adamw_t_ (update + W^T of every listed matrix; LDS tiles or register-blocked 8 x 8 blocks;
-    edge tiles, [1, n] rows and a 13-row matrix without a copy) == adamw_ on the same elements,
+def test_adamw_t_matches_adamw_and_transposes(cuda, state_dtype, master, tile_cols):
+    """adamw_t_ (update + W^T of every listed matrix in register-blocked 8 x 8 blocks; edge
+    tiles, [1, n] rows and a 13-row matrix without a copy) == adamw_ on the same elements,
     bitwise; copies == W^T exactly; elements outside the listed matrices untouched."""
-    monkeypatch.setenv("DTG_ADAMT_KERNEL", kernel)
     torch.manual_seed(0)
     shapes = [(192, 320), (1, 136), (72, 200), (1024, 64), (13, 128)]  # 72 x 200: partial edge tiles
     offs, o = [], 0

@@ -57,18 +57,9 @@ def main():
         "rmsnorm_bwd(+dres)": (lambda: ops.rmsnorm_bwd(dy, hh, w, rstd, dy), 4 * T * H * E),
         "swiglu_fwd": (lambda: ops.swiglu_fwd(gu), 3 * T * I * E),
     }
-    # A/B pairs run twice in alternating order (A B A B) against clock drift
-    for rep in (1, 2):
-        for tl in ("64x64", "64x128", "128x64", "128x128", "reg"):
-            cases[f"swiglu_bwd_t (dgu, dgu^T, h^T) tile {tl} #{rep}"] = (
-                lambda tl=tl: (os.environ.__setitem__("DTG_SWIGLU_TILE", tl), ops.swiglu_bwd_t(dh, gu)),
-                (3 + 5) * T * I * E)
-        for tt in ("64", "128", "reg"):
-            def tr(src, tt=tt):
-                os.environ["DTG_TRANSPOSE_TILE"] = tt
-                return ops.transpose2d(src)
-            cases[f"transpose [T,H] tile {tt} #{rep}"] = (lambda tr=tr: tr(x), 2 * T * H * E)
-            cases[f"transpose [T,2I] tile {tt} #{rep}"] = (lambda tr=tr: tr(gu), 2 * T * 2 * I * E)
+    cases["swiglu_bwd_t (dgu, dgu^T, h^T)"] = (lambda: ops.swiglu_bwd_t(dh, gu), (3 + 5) * T * I * E)
+    cases["transpose [T,H]"] = (lambda: ops.transpose2d(x), 2 * T * H * E)
+    cases["transpose [T,2I]"] = (lambda: ops.transpose2d(gu), 2 * T * 2 * I * E)
     n = int(a.params) // 16 * 16
     n = min(n, 2_000_000_000)  # keep the AdamW buffers at <= 14 GB
     p = torch.randn(n, **bf)
@@ -89,24 +80,15 @@ def main():
         pw, gw = torch.randn(nt, **bf), torch.randn(nt, **bf)
         mw, vw, ptw = torch.zeros(nt, **bf), torch.zeros(nt, **bf), torch.empty(nt, **bf)
         mats = torch.tensor(desc, dtype=torch.long, device=dev)
-        def at_(kern, tc=tc, mats=mats, tile0=tile0):
-            os.environ["DTG_ADAMT_KERNEL"] = kern
-            ops.adamw_t_(pw, None, gw, mw, vw, ptw, mats, tile0, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0, None, tc)
-        runs = {}
-        for rep in (1, 2):  # A B A B against clock drift
-            runs[f"adamw_t_ 64x{tc} (+W^T) lds #{rep}"] = (lambda: at_("lds"), 16 * nt)
-            runs[f"adamw_t_ 64x{tc} (+W^T) reg #{rep}"] = (lambda: at_("reg"), 16 * nt)
-        if tc == 64:
-            for un, wg in ((2, 16), (4, 16), (2, 8), (4, 8), (2, 32), (4, 4)):
-                def lin(un=un, wg=wg):
-                    os.environ["DTG_ADAM_UNROLL"], os.environ["DTG_ADAM_WG_PER_CU"] = str(un), str(wg)
-                    ops.adamw_(pw, None, gw, mw, vw, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0)
-                runs[f"adamw_ (same buffers) unroll {un} wg/cu {wg}"] = (lin, 14 * nt)
+        runs = {f"adamw_t_ 64x{tc} (+W^T)": (lambda tc=tc, mats=mats, tile0=tile0: ops.adamw_t_(
+            pw, None, gw, mw, vw, ptw, mats, tile0, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0, None, tc), 16 * nt)}
         if tc == 128:  # the tile walk with no transposed copies (toff = -1): layout effect alone
             mats_nt = mats.clone()
             mats_nt[:, 3] = -1
-            runs["adamw_t_ 64x128 tile walk, no W^T"] = (lambda: os.environ.__setitem__("DTG_ADAMT_KERNEL", "lds") or ops.adamw_t_(
+            runs["adamw_t_ 64x128 tile walk, no W^T"] = (lambda: ops.adamw_t_(
                 pw, None, gw, mw, vw, ptw, mats_nt, tile0, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0, None, tc), 14 * nt)
+            runs["adamw_ (same buffers)"] = (lambda: ops.adamw_(pw, None, gw, mw, vw, 1e-4, 0.9, 0.999, 1e-8, 0.01, 3, 1.0),
+                                             14 * nt)
         for name, (fn, nbytes) in runs.items():
             if a.only and not any(o in name for o in a.only.split(',')):
                 continue
