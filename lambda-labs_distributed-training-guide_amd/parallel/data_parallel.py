@@ -156,8 +156,8 @@ class DataParallel:
         import math
 
         sp = self.space
-        # adamw_t_ tile width (64 x TC tiles; DTG_ADAMT_TC = 64 | 128 | 256).  256: the register-
-        # blocked kernel's fastest walk (profiles/r5/transpose/; the LDS kernel's was 128, r3/s07)
+        # adamw_t_ tile width (64 x TC tiles; DTG_ADAMT_TC = 64 | 128 | 256, read once here).
+        # 256: the register-blocked kernel's fastest walk (profiles/r5/transpose/, r6/knobs/)
         self._wt_tc = int(os.environ.get("DTG_ADAMT_TC", "256"))
         rows_desc, slots, toff, tile0 = [], {}, 0, 0
         for i in range(len(sp.names)):
