@@ -1,0 +1,217 @@
+"""Property-based tests (hypothesis) of the host-side logic every run depends on -- SURVEY §4.2
+tier T0: packed-sequence collation against a naive token walk, flat-buffer bucketing and shard
+ranges, DCP name/row mapping of the fused projections, the activation-checkpointing budget,
+the skip-ahead sampler, the LR schedule and LR scaling rules.
+
+References: /root/reference/00-rime/packed_dataset.py:14-49 (collate), 02-distributed-data-
+parallel/train_llm.py:96-103 (sampler), 04-fully-sharded-data-parallel/train_llm.py:249-263 (DCP
+keys), 01-single-gpu/train_llm.py:111-113 (cosine schedule)."""
+import argparse
+import math
+import os
+
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+# DTG_HYP_EXAMPLES raises the example count for a longer hunt (default: a few seconds in total)
+SETTINGS = dict(max_examples=int(os.environ.get("DTG_HYP_EXAMPLES", "60")), deadline=None, database=None,
+                suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+EOS = 0
+
+
+# ------------------------------------------------------------------------------ packing
+def _naive_positions(row):
+    """Walk the tokens: positions restart after every EOS; the last token ends a document."""
+    pos, lens, p = [], [], 0
+    for i, tok in enumerate(row):
+        pos.append(p)
+        p += 1
+        if tok == EOS or i == len(row) - 1:
+            lens.append(p)
+            p = 0
+    return pos, lens
+
+
+@settings(**SETTINGS)
+@given(st.integers(1, 4).flatmap(lambda b: st.integers(1, 48).flatmap(
+    lambda t: st.lists(st.lists(st.sampled_from([EOS, 1, 2, 3, 4, 5]), min_size=t, max_size=t),
+                       min_size=b, max_size=b))))
+def test_packed_collate_matches_naive_walk(rows):
+    from dtg.data.packed import PackedCollator
+
+    samples = [{"input_ids": torch.tensor(r)} for r in rows]
+    before = [s["input_ids"].clone() for s in samples]
+    out = PackedCollator(EOS)(samples)
+    T = len(rows[0])
+    forced = [r[:-1] + [EOS] for r in rows]  # the reference forces x[-1] = eos
+    assert out["input_ids"].tolist() == forced and out["labels"].tolist() == forced
+    assert all(torch.equal(a, s["input_ids"]) for a, s in zip(before, samples))  # no in-place EOS write
+    pos, lens = zip(*(_naive_positions(r) for r in forced))
+    assert out["position_ids"].tolist() == list(pos)
+    flat_lens = [n for ls in lens for n in ls]
+    assert out["cu_seqlens"].dtype == torch.int32
+    assert out["cu_seqlens"].tolist() == [0] + list(torch.cumsum(torch.tensor(flat_lens), 0).tolist())
+    assert out["cu_seqlens"][-1] == len(rows) * T and out["max_seqlen"] == max(flat_lens)
+    assert out["num_valid"] == len(rows) * (T - 1)
+    # the documents cu_seqlens delimits are exactly the blocks where position ids restart
+    doc = torch.repeat_interleave(torch.arange(len(flat_lens)), torch.tensor(flat_lens))
+    starts = (out["position_ids"].reshape(-1) == 0).cumsum(0) - 1
+    assert torch.equal(doc, starts)
+
+
+# ------------------------------------------------------------------------------ flat buckets
+@settings(**SETTINGS)
+@given(st.lists(st.lists(st.integers(1, 40), min_size=1, max_size=2), min_size=1, max_size=12),
+       st.integers(1, 8), st.integers(64, 4096), st.booleans())
+def test_flat_space_buckets_partition_and_shard(shapes, world, bucket_bytes, with_trailing):
+    from dtg.parallel.flat import ALIGN, FlatSpace
+
+    params = [(f"p{i}", torch.nn.Parameter(torch.zeros(*s))) for i, s in enumerate(shapes)]
+    trailing = (lambda p: p.dim() == 1) if with_trailing else None
+    sp = FlatSpace(params, "cpu", world=world, bucket_bytes=bucket_bytes, trailing=trailing)
+    # buckets tile [0, numel) contiguously, each a whole number of world x ALIGN elements
+    assert sp.buckets[0].start == 0 and sp.buckets[-1].end == sp.numel
+    for a, b in zip(sp.buckets, sp.buckets[1:]):
+        assert a.end == b.start
+    for b in sp.buckets:
+        assert b.numel > 0 and b.numel % (world * ALIGN) == 0
+        ranges = [sp.shard_range(b, r) for r in range(world)]
+        assert ranges[0][0] == b.start and ranges[-1][1] == b.end
+        assert all(x[1] == y[0] for x, y in zip(ranges, ranges[1:]))
+    # every parameter is 16-element aligned, inside its own bucket, and no two overlap
+    spans = []
+    for i, (o, shape) in enumerate(zip(sp.offsets, sp.shapes)):
+        n = math.prod(shape)
+        b = sp.param_bucket[i]
+        assert o % ALIGN == 0 and b.start <= o and o + n <= b.end
+        spans.append((o, o + n))
+        assert sp.param_view(i).shape == torch.Size(shape)
+    spans.sort()
+    assert all(x[1] <= y[0] for x, y in zip(spans, spans[1:]))
+    # backward order: the flat order is the reverse of registration, trailing params last
+    names = [n for n, _ in params][::-1]
+    if with_trailing:
+        tail = [n for n, p in params[::-1] if p.dim() == 1]
+        names = [n for n in names if n not in tail] + tail
+        if tail and len(tail) < len(params):
+            assert sp.buckets[-1].trailing and all(p.dim() == 1 for p in sp.buckets[-1].params)
+    assert sp.names == names
+
+
+# ------------------------------------------------------------------------------ DCP names
+@settings(**SETTINGS)
+@given(st.sampled_from([(4, 2, 8), (8, 8, 16), (6, 2, 4), (32, 8, 16), (4, 1, 8)]), st.data())
+def test_dcp_fused_projection_chunks_tile_the_rectangle(heads, data):
+    """Any row range of the fused qkv / gate_up weight (a TP shard, an FSDP piece) maps onto HF
+    q/k/v (gate/up) chunks that cover exactly those rows, at the right HF offsets."""
+    from dtg.models.config import LlamaConfig
+    from dtg.train.dcp_ckpt import _Names
+
+    nq, nkv, d = heads
+    inter = data.draw(st.integers(1, 40))
+    H = 16
+    cfg = LlamaConfig(vocab_size=32, hidden_size=H, intermediate_size=inter, num_hidden_layers=1,
+                      num_attention_heads=nq, num_key_value_heads=nkv, head_dim=d)
+    names = _Names(cfg)
+    for name, rows, parts in (
+            ("layers.0.self_attn.qkv_proj.weight", (nq + 2 * nkv) * d,
+             [("q_proj", 0, nq * d), ("k_proj", nq * d, nkv * d), ("v_proj", (nq + nkv) * d, nkv * d)]),
+            ("layers.0.mlp.gate_up_proj.weight", 2 * inter, [("gate_proj", 0, inter), ("up_proj", inter, inter)])):
+        r0 = data.draw(st.integers(0, rows - 1))
+        nr = data.draw(st.integers(1, rows - r0))
+        c0 = data.draw(st.integers(0, H - 1))
+        nc = data.draw(st.integers(1, H - c0))
+        got = names.split(name, [rows, H], [r0, nr, c0, nc, 0])
+        covered = []
+        for hf, hshape, offs, sizes, (lo, hi) in got:
+            short, g0, n = next(p for p in parts if hf.endswith(p[0] + ".weight"))
+            assert hf.startswith("model.layers.0.") and hshape == [n, H]
+            assert offs == [lo - g0, c0] and sizes == [hi - lo, nc]
+            assert g0 <= lo < hi <= g0 + n
+            covered.append((lo, hi))
+        covered.sort()
+        assert covered[0][0] == r0 and covered[-1][1] == r0 + nr
+        assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+
+
+# ------------------------------------------------------------------------------ AC budget
+@settings(**SETTINGS)
+@given(st.integers(1, 130), st.data(), st.integers(1, 10 ** 9), st.integers(0, 10 ** 8),
+       st.integers(0, 400 * 10 ** 9), st.integers(0, 400 * 10 ** 9), st.floats(1.0, 2.0))
+def test_ac_budget_keeps_the_fewest_layers_that_fit(n, data, per, inp, peak, budget, safety):
+    from dtg.parallel.checkpointing import ac_layers_for_budget
+
+    n_ckpt = data.draw(st.integers(0, n))
+    keep = ac_layers_for_budget(n, n_ckpt, peak, budget, per, inp, safety)
+    assert 0 <= keep <= n_ckpt
+    extra = max(1, int((per - inp) * safety))
+    released = n_ckpt - keep
+    if peak >= budget:
+        assert keep == n_ckpt  # over budget already: nothing is released
+    else:
+        assert peak + released * extra <= budget  # what is released fits
+        assert keep == 0 or peak + (released + 1) * extra > budget  # and one more would not
+    # a larger budget never checkpoints more layers
+    assert ac_layers_for_budget(n, n_ckpt, peak, budget + 10 ** 9, per, inp, safety) <= keep
+
+
+# ------------------------------------------------------------------------------ sampler
+@settings(**SETTINGS)
+@given(st.integers(1, 200), st.integers(1, 8), st.integers(0, 5), st.integers(0, 3), st.data())
+def test_sampler_resume_and_rank_partition(n, world, seed, epoch, data):
+    from dtg.data import ResumableSampler
+
+    ds = list(range(n))
+    full = []
+    for r in range(world):
+        s = ResumableSampler(ds, num_replicas=world, rank=r, seed=seed)
+        s.set_epoch(epoch)
+        order = list(s)
+        assert len(order) == len(s) == n // world  # drop_last
+        full.append(order)
+        skip = data.draw(st.integers(0, len(order)))
+        s.set_epoch(epoch, skip=skip)  # resume part-way: the same order, minus what was consumed
+        assert list(s) == order[skip:] and len(s) == len(order) - skip
+    flat = [i for o in full for i in o]
+    assert len(set(flat)) == len(flat)  # ranks never share a sample
+
+
+# ------------------------------------------------------------------------------ LR
+@settings(**SETTINGS)
+@given(st.floats(1e-6, 1e-2), st.integers(0, 50), st.integers(51, 300), st.floats(0.0, 0.5))
+def test_warmup_cosine_schedule(lr, warm, total, floor):
+    from dtg.train.trainer import _scheduler
+
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=lr)
+    args = argparse.Namespace(lr=lr, ds_scheduler={"type": "WarmupCosineLR", "params": {
+        "total_num_steps": total, "warmup_num_steps": warm, "cos_min_ratio": floor}})
+    sched = _scheduler(args, opt)
+    lrs = []
+    for _ in range(total + 5):
+        lrs.append(opt.param_groups[0]["lr"])
+        opt.step()
+        sched.step()
+    for i in range(1, warm):  # linear warm-up
+        assert lrs[i] == pytest.approx(lr * (i + 1) / warm, rel=1e-6)
+    assert all(0 <= x <= lr * (1 + 1e-6) for x in lrs)
+    assert all(x >= floor * lr * (1 - 1e-6) for x in lrs[warm:])  # the cosine floor after warm-up
+    tail = lrs[warm:total + 1]
+    assert all(a >= b - 1e-12 for a, b in zip(tail, tail[1:]))  # non-increasing after warm-up
+    assert lrs[-1] == pytest.approx(floor * lr, rel=1e-6, abs=1e-12)
+
+
+@settings(**SETTINGS)
+@given(st.floats(1e-6, 1.0), st.integers(1, 4096), st.integers(1, 4096), st.integers(1, 64), st.integers(1, 16))
+def test_lr_scaling_rules(lr, b0, b1, dp, accum):
+    from dtg.utils.lr_scaling import effective_batch, scale_lr
+
+    assert effective_batch(b1, dp, accum) == b1 * dp * accum
+    assert scale_lr(lr, b0, b0) == pytest.approx(lr)
+    lin, sq = scale_lr(lr, b0, b1, "linear"), scale_lr(lr, b0, b1, "sqrt")
+    assert lin == pytest.approx(lr * b1 / b0) and sq == pytest.approx(lr * math.sqrt(b1 / b0))
+    assert (lin >= sq) == (b1 >= b0) or lin == pytest.approx(sq)
+    with pytest.raises(ValueError):
+        scale_lr(lr, b0, b1, "cubic")
