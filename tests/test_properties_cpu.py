@@ -215,3 +215,64 @@ def test_lr_scaling_rules(lr, b0, b1, dp, accum):
     assert (lin >= sq) == (b1 >= b0) or lin == pytest.approx(sq)
     with pytest.raises(ValueError):
         scale_lr(lr, b0, b1, "cubic")
+
+
+# ------------------------------------------------------------------------------ TP geometry
+def _tp_local(G, kind, r, n, nq, nkv, d):
+    """The TP plan's shard of global tensor G (2-D) for rank r of n, written independently of
+    train/checkpoint.py: q/k/v and gate/up row blocks per rank, o/down column blocks, embedding /
+    head row blocks, everything else replicated."""
+    if n == 1 or kind == "rep":
+        return G
+    if kind == "qkv":
+        q, k, v = G[:nq * d], G[nq * d:(nq + nkv) * d], G[(nq + nkv) * d:]
+        bq, bk = nq // n * d, nkv // n * d
+        return torch.cat([q[r * bq:(r + 1) * bq], k[r * bk:(r + 1) * bk], v[r * bk:(r + 1) * bk]])
+    if kind == "gate_up":
+        i = G.shape[0] // 2
+        b = i // n
+        return torch.cat([G[r * b:(r + 1) * b], G[i + r * b:i + (r + 1) * b]])
+    if kind == "col":
+        b = G.shape[1] // n
+        return G[:, r * b:(r + 1) * b]
+    b = G.shape[0] // n  # row
+    return G[r * b:(r + 1) * b]
+
+
+@settings(**SETTINGS)
+@given(st.sampled_from([1, 2, 4, 8]), st.sampled_from(["layers.0.self_attn.qkv_proj.weight", "layers.0.mlp.gate_up_proj.weight",
+                                                       "layers.0.self_attn.o_proj.weight", "embed_tokens.weight",
+                                                       "layers.0.input_layernorm.weight", "layers.0.self_attn.qkv_proj.bias"]),
+       st.data())
+def test_checkpoint_rectangles_tile_the_global_tensor(n, name, data):
+    """Every rank's TP-local flat range, cut into arbitrary data-parallel pieces, maps to global
+    rectangles (train/checkpoint.py _TPGeom.rects) that hold exactly the right elements and,
+    over all ranks and pieces, cover the global tensor once -- what lets a checkpoint load on
+    any (dp, tp) layout."""
+    from dtg.models.config import LlamaConfig
+    from dtg.train.checkpoint import _TPGeom, param_kind
+
+    nkv = n * data.draw(st.integers(1, 2))
+    nq = nkv * data.draw(st.integers(1, 3))
+    d, H = 4, 8 * n
+    inter = n * data.draw(st.integers(1, 3))
+    cfg = LlamaConfig(vocab_size=16 * n, hidden_size=H, intermediate_size=inter, num_hidden_layers=1,
+                      num_attention_heads=nq, num_key_value_heads=nkv, head_dim=d)
+    kind = param_kind(name) if n > 1 else "rep"
+    gshape = {"qkv": [(nq + 2 * nkv) * d, 1 if name.endswith("bias") else H], "gate_up": [2 * inter, H],
+              "col": [H, nq * d], "row": [cfg.vocab_size, H], "rep": [1, H]}[param_kind(name)]
+    G = torch.arange(math.prod(gshape), dtype=torch.float64).view(gshape)
+    seen = torch.zeros(gshape, dtype=torch.int64)
+    for r in range(n):
+        geo = object.__new__(_TPGeom)
+        geo.rank, geo.size, geo.cfg = r, n, cfg
+        L = _tp_local(G, kind, r, n, nq, nkv, d).contiguous()
+        local_shape = [H] if name.endswith("layernorm.weight") else list(L.shape)
+        flat = L.reshape(-1)
+        cuts = sorted(set(data.draw(st.lists(st.integers(1, flat.numel() - 1), max_size=4)))) if flat.numel() > 1 else []
+        for start, end in zip([0] + cuts, cuts + [flat.numel()]):
+            for r0, nr, c0, nc, off in geo.rects(name, local_shape, start, end - start):
+                got = flat[start + off:start + off + nr * nc].view(nr, nc)
+                assert torch.equal(got, G[r0:r0 + nr, c0:c0 + nc]), (r, start, (r0, nr, c0, nc, off))
+                seen[r0:r0 + nr, c0:c0 + nc] += 1
+    assert bool((seen == (n if kind == "rep" else 1)).all())
