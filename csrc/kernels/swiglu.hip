@@ -57,7 +57,7 @@ __global__ void swiglu_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_
 // segments of TT token rows); the three transposed tiles are staged through LDS (pitch TF + 2
 // halfwords) and stored as 16-byte columns (TT x 2-byte segments of TF feature rows).
 // 64 x 128 is the measured best of the 64/128 x 64/128 tiles and of a register-blocked 8 x 8
-// form (-2.1 ms per 8B step against 64 x 64, profiles/r3_s32; 4.64 vs 4.52 TB/s against the
+// form (-2.1 ms per 8B step against 64 x 64, profiles/r3/s32; 4.64 vs 4.52 TB/s against the
 // register-blocked one, profiles/r5/transpose/); the others were removed in round 6.
 constexpr int kSgTT = 64, kSgTF = 128;
 
