@@ -552,6 +552,17 @@ def write_single_shard(ckpt_dir, params: dict, moments: dict = None, step: int =
 
 
 # ------------------------------------------------------------------------------ high level
+def _any_failed(err) -> bool:
+    """Collective: did the checkpoint write fail on ANY rank?  Every rank then raises together,
+    instead of the healthy ranks waiting at the next barrier for a rank that already left."""
+    if not (dist.is_initialized() and get_world_size() > 1) or dist.get_backend() == "fake":
+        return err is not None
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([int(err is not None)], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item())
+
+
 class CheckpointManager:
     """Save/resume in the reference's layout. `style` in {"full", "dp", "sharded"}.
 
@@ -651,8 +662,9 @@ class CheckpointManager:
         self._writer.join()
         self._writer = None
         err, self._error = self._error, None
-        if err is not None:
-            raise RuntimeError("async checkpoint write failed") from err
+        if _any_failed(err):
+            self._pending = None  # the half-written .pending is discarded by the next save / start
+            raise RuntimeError("async checkpoint write failed" + ("" if err else " on another rank")) from err
         barrier()
         if get_rank() == 0:
             self._publish(*self._pending)
@@ -689,8 +701,8 @@ class CheckpointManager:
         jobs, shard = self._snapshot_host(state.get("global_step"))
         self._write_pending(jobs, shard)
         err, self._error = self._error, None
-        if err is not None:
-            raise RuntimeError("checkpoint write failed") from err
+        if _any_failed(err):
+            raise RuntimeError("checkpoint write failed" + ("" if err else " on another rank")) from err
         barrier()
         if get_rank() == 0:
             box = _RngBox()

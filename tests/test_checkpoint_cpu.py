@@ -324,3 +324,41 @@ def test_every_payload_is_fsynced_before_commit(tmp_path, monkeypatch, style):
     assert pend in before  # the directory entries of the payload
     assert str(tmp_path) in events[marker + 1:]  # the renames into exp_dir
     assert (tmp_path / "state.json").exists() and not (tmp_path / ".pending").exists()
+
+
+def _failing_write_worker(rank, world, d, async_save):
+    """Rank 1's checkpoint write fails; every rank must raise (none may wait at a barrier for a
+    rank that already left), and the previous checkpoint stays published."""
+    import dtg.train.checkpoint as ck
+    from dtg.train.checkpoint import CheckpointManager, new_state
+
+    m, eng, opt = _make("zero")
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10)
+    mgr = CheckpointManager(d, eng, opt, sched, "sharded", async_save=async_save, fmt="dtg")
+    st = new_state()
+    st["global_step"] = 1
+    mgr.save(st)
+    mgr.finalize()
+    if rank == 1:
+        def boom(*a, **k):
+            raise OSError("disk full (injected)")
+
+        ck.write_sharded = boom
+    st["global_step"] = 2
+    out = []
+    try:
+        mgr.save(st)
+        mgr.finalize()
+    except RuntimeError as e:
+        out.append(str(e))
+    return out
+
+
+@pytest.mark.parametrize("async_save", [False, True])
+def test_checkpoint_write_failure_raises_on_every_rank(tmp_path, async_save):
+    import json
+
+    res = run_distributed(_failing_write_worker, 2, str(tmp_path), async_save)
+    assert res[1] == ["async checkpoint write failed" if async_save else "checkpoint write failed"]
+    assert res[0] == [("async checkpoint write failed" if async_save else "checkpoint write failed") + " on another rank"]
+    assert json.loads((tmp_path / "state.json").read_text())["global_step"] == 1
