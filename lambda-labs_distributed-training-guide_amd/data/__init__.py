@@ -7,12 +7,13 @@ import torch
 from torch.utils.data import DataLoader, DistributedSampler
 
 from .packed import PackedCollator, dense_collate, packed_position_ids
-from .synthetic import SyntheticPacked, SyntheticTokens
+from .synthetic import SyntheticPacked, SyntheticPattern, SyntheticTokens
 
 
 def build_dataset(name: str, *, tokenizer_name: str = None, seq_length: int = 1024, vocab_size: int = 50257,
                   max_position_embeddings: int = 1024, num_samples: int = 100_000, eos_id: int = None, seed: int = 0):
-    """`synthetic` / `synthetic:packed` / `synthetic:packed:<mean_doc_len>` or an HF dataset name/path.
+    """`synthetic` / `synthetic:packed` / `synthetic:packed:<mean_doc_len>` / `synthetic:pattern`
+    (learnable progressions, for convergence checks) or an HF dataset name/path.
 
     Returns (dataset, seq_length, collate_fn)."""
     if name.startswith("synthetic"):
@@ -21,6 +22,8 @@ def build_dataset(name: str, *, tokenizer_name: str = None, seq_length: int = 10
             mean = int(parts[2]) if len(parts) > 2 else 512
             eos = eos_id if eos_id is not None else vocab_size - 1
             return SyntheticPacked(num_samples, seq_length, vocab_size, eos, mean, seed), seq_length, PackedCollator(eos)
+        if len(parts) > 1 and parts[1] == "pattern":
+            return SyntheticPattern(num_samples, seq_length, vocab_size, seed=seed), seq_length, dense_collate
         return SyntheticTokens(num_samples, seq_length, vocab_size, seed), seq_length, dense_collate
     if name.startswith("disk:"):
         import datasets

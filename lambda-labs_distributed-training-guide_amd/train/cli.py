@@ -19,7 +19,7 @@ def get_parser(chapter: str) -> argparse.ArgumentParser:
         p.add_argument("-m", "--model-name", default="llama-3.2-3b-rime")
     else:
         p.add_argument("-d", "--dataset-name", default=None, required=True,
-                       help="HF dataset name/path, or `synthetic` / `synthetic:packed[:mean_doc_len]` (offline)")
+                       help="HF dataset name/path, or `synthetic` / `synthetic:packed[:mean_doc_len]` / `synthetic:pattern` (learnable; offline)")
         p.add_argument("-m", "--model-name", default=None, required=True,
                        help="HF hub name (bundled configs: see dtg.models.available_configs) or config.json path")
     p.add_argument("--save-dir", default="../outputs")
