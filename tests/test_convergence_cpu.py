@@ -12,12 +12,21 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run_pattern(tmp_path, extra=(), steps=160, timeout=600):
-    cmd = [sys.executable, "train_llm.py", "-e", "cv", "-m", "llama-tiny", "-d", "synthetic:pattern", "-b", "16",
+def run_pattern(tmp_path, extra=(), steps=160, timeout=600, chapter="01-single-gpu", nproc=0):
+    """Train on synthetic:pattern; nproc > 0 launches `nproc` gloo ranks through torchrun."""
+    launch = [sys.executable]
+    if nproc:
+        from _dist import free_port
+
+        launch += ["-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
+                   "--master-addr", "127.0.0.1", "--master-port", str(free_port())]
+    cmd = launch + ["train_llm.py", "-e", "cv", "-m", "llama-tiny", "-d", "synthetic:pattern", "-b", "16",
            "-s", "64", "--lr", "3e-3", "--num-workers", "0", "--log-freq", "20", "--ckpt-freq", "100000",
            "--max-steps", str(steps), "--save-dir", str(tmp_path), *extra]
-    r = subprocess.run(cmd, cwd=os.path.join(ROOT, "01-single-gpu"), capture_output=True, text=True, timeout=timeout,
-                       env=dict(os.environ, DTG_NO_WANDB="1"))
+    env = dict(os.environ, DTG_NO_WANDB="1")
+    if nproc:
+        env["OMP_NUM_THREADS"] = "1"  # the ranks share the 8 CPUs
+    r = subprocess.run(cmd, cwd=os.path.join(ROOT, chapter), capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     recs = [json.loads(x) for x in (tmp_path / "cv" / "metrics-rank0.jsonl").read_text().splitlines()]
     return [x["running_loss"] for x in recs if x["global_step"] > 0]
@@ -26,4 +35,11 @@ def run_pattern(tmp_path, extra=(), steps=160, timeout=600):
 def test_pattern_data_is_learned(tmp_path):
     losses = run_pattern(tmp_path)
     assert math.log(512) * 0.6 < losses[0]  # starts near ln V (llama-tiny: V = 512; window mean of steps 1-20)
+    assert losses[-1] < 1.5 and losses[-1] < losses[0] / 3, losses
+
+
+def test_pattern_data_is_learned_2d_tp2_dp2(tmp_path):
+    """Chapter 07's FSDP x TP (tp 2 x dp 2, four gloo ranks, real collectives) learns too."""
+    losses = run_pattern(tmp_path, ("-b", "8", "--tp", "2"), chapter="07-2d-parallel", nproc=4)
+    assert math.log(512) * 0.6 < losses[0]
     assert losses[-1] < 1.5 and losses[-1] < losses[0] / 3, losses
