@@ -43,3 +43,10 @@ def test_pattern_data_is_learned_2d_tp2_dp2(tmp_path):
     losses = run_pattern(tmp_path, ("-b", "8", "--tp", "2"), chapter="07-2d-parallel", nproc=4)
     assert math.log(512) * 0.6 < losses[0]
     assert losses[-1] < 1.5 and losses[-1] < losses[0] / 3, losses
+
+
+def test_pattern_data_is_learned_fsdp_offload(tmp_path):
+    """Chapter 05's FSDP with CPU offload (host AdamW) on two gloo ranks learns too."""
+    losses = run_pattern(tmp_path, ("-b", "8", "--cpu-offload", "on"), chapter="05-training-llama-405b", nproc=2)
+    assert math.log(512) * 0.6 < losses[0]
+    assert losses[-1] < 1.5 and losses[-1] < losses[0] / 3, losses
