@@ -276,3 +276,73 @@ def test_checkpoint_rectangles_tile_the_global_tensor(n, name, data):
                 assert torch.equal(got, G[r0:r0 + nr, c0:c0 + nc]), (r, start, (r0, nr, c0, nc, off))
                 seen[r0:r0 + nr, c0:c0 + nc] += 1
     assert bool((seen == (n if kind == "rep" else 1)).all())
+
+
+# ------------------------------------------------------------------------------ HF weights x TP
+class _FakeHF:
+    """models/loading.py's _LazyHF interface over an in-memory HF state dict."""
+
+    def __init__(self, sd):
+        self.sd = sd
+
+    def shape(self, k):
+        return list(self.sd[k].shape)
+
+    def get(self, k):
+        return self.sd[k]
+
+    def rows(self, k, r0, r1, c0=None, c1=None):
+        t = self.sd[k]
+        return t[r0:r1] if (t.dim() == 1 or c0 is None) else t[r0:r1, c0:c1]
+
+
+@settings(**SETTINGS)
+@given(st.sampled_from([1, 2, 4]), st.booleans(), st.booleans(), st.data())
+def test_hf_conversion_and_tp_loading_agree(tp, tie, bias, data):
+    """HF -> fused layout -> HF is exact; the TP sharder, an independent shard rule and the
+    per-rank safetensors row reader (--init-from) give the same rank-local rows for any row range."""
+    from dtg.models.config import LlamaConfig
+    from dtg.models.hf_compat import llama_from_hf, llama_to_hf
+    from dtg.models.loading import _read_rows
+    from dtg.parallel.tensor_parallel import shard_full_state_dict
+    from dtg.train.checkpoint import param_kind
+
+    nkv = tp * data.draw(st.integers(1, 2))
+    nq = nkv * data.draw(st.integers(1, 2))
+    d, H, inter, V = 4, 8 * tp, 4 * tp * data.draw(st.integers(1, 3)), 8 * tp
+    cfg = LlamaConfig(vocab_size=V, hidden_size=H, intermediate_size=inter, num_hidden_layers=1,
+                      num_attention_heads=nq, num_key_value_heads=nkv, head_dim=d, tie_word_embeddings=tie)
+    g = torch.Generator().manual_seed(data.draw(st.integers(0, 10 ** 6)))
+    p = "model.layers.0."
+    shapes = {p + "self_attn.q_proj.weight": (nq * d, H), p + "self_attn.k_proj.weight": (nkv * d, H),
+              p + "self_attn.v_proj.weight": (nkv * d, H), p + "self_attn.o_proj.weight": (H, nq * d),
+              p + "mlp.gate_proj.weight": (inter, H), p + "mlp.up_proj.weight": (inter, H),
+              p + "mlp.down_proj.weight": (H, inter), p + "input_layernorm.weight": (H,),
+              p + "post_attention_layernorm.weight": (H,), "model.embed_tokens.weight": (V, H),
+              "model.norm.weight": (H,)}
+    if bias:
+        shapes.update({p + "self_attn.q_proj.bias": (nq * d,), p + "self_attn.k_proj.bias": (nkv * d,),
+                       p + "self_attn.v_proj.bias": (nkv * d,)})
+    if not tie:
+        shapes["lm_head.weight"] = (V, H)
+    hf = {k: torch.randn(*s, generator=g) for k, s in shapes.items()}
+    ours = llama_from_hf(hf, cfg)
+    back = llama_to_hf(ours, cfg)
+    assert set(back) == set(hf) | ({"lm_head.weight"} if tie else set())
+    assert all(torch.equal(back[k], v) for k, v in hf.items())
+    fake = _FakeHF(hf)
+    for r in range(tp):
+        local = shard_full_state_dict(ours, cfg, r, tp)
+        for name, full in ours.items():
+            kind = param_kind(name) if tp > 1 else "rep"
+            G = full if full.dim() == 2 else full[None]
+            mine = _tp_local(G, kind, r, tp, nq, nkv, d)
+            loc = local[name] if local[name].dim() == 2 else local[name][None]
+            assert torch.equal(loc, mine), (name, r)
+            if name.endswith("layernorm.weight") or name == "norm.weight":
+                assert torch.equal(_read_rows(fake, name, 0, H, cfg, r, tp), full)
+                continue
+            r0 = data.draw(st.integers(0, loc.shape[0] - 1))
+            r1 = data.draw(st.integers(r0 + 1, loc.shape[0]))
+            got = _read_rows(fake, name, r0, r1, cfg, r, tp)
+            assert torch.equal(got.reshape(r1 - r0, -1), loc[r0:r1]), (name, r, r0, r1)
