@@ -1,8 +1,8 @@
 """GPU twin of tests/test_convergence_cpu.py: chapter 01 on `synthetic:pattern` through the HIP
 kernels (flash attention at head_dim 128, fused norms / SwiGLU / CE / AdamW, hipBLASLt TN GEMMs),
-eager and with the whole step captured in a HIP graph, and chapter 07's FSDP x TP as four ranks
-sharing the GPU (DTG_SHARED_DEVICE=1: real per-rank kernels, gloo collectives): the loss falls
-from ln V far down."""
+eager and with the whole step captured in a HIP graph: the loss falls from ln V far down.  (The
+distributed chapters' convergence runs on CPU ranks, tests/test_convergence_cpu.py; as four ranks
+sharing this GPU over gloo, chapter 07 learned the same way but took 2 minutes of the GPU tier.)"""
 import math
 
 import pytest
@@ -18,10 +18,3 @@ def test_pattern_data_is_learned_on_gpu(cuda, tmp_path, graph):
     assert math.log(1000) * 0.6 < losses[0]  # starts near ln V (V = 1000)
     assert losses[-1] < 1.0 and losses[-1] < losses[0] / 4, losses
 
-
-def test_pattern_data_is_learned_2d_on_gpu(cuda, tmp_path, monkeypatch):
-    monkeypatch.setenv("DTG_SHARED_DEVICE", "1")
-    losses = run_pattern(tmp_path, ("-m", "llama-tiny-d128", "--lr", "1e-3", "-b", "8", "--tp", "2"), steps=200,
-                         timeout=300, chapter="07-2d-parallel", nproc=4)
-    assert math.log(1000) * 0.6 < losses[0]
-    assert losses[-1] < 1.0 and losses[-1] < losses[0] / 4, losses
