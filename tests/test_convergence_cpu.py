@@ -50,3 +50,16 @@ def test_pattern_data_is_learned_fsdp_offload(tmp_path):
     losses = run_pattern(tmp_path, ("-b", "8", "--cpu-offload", "on"), chapter="05-training-llama-405b", nproc=2)
     assert math.log(512) * 0.6 < losses[0]
     assert losses[-1] < 1.5 and losses[-1] < losses[0] / 3, losses
+
+
+def test_pattern_data_is_learned_long_context_cp_and_ulysses(tmp_path):
+    """Context parallel (zig-zag shards, --cp 2) and Ulysses (--sp 2) split every sequence over
+    two ranks: both learn like one process with the same batch (the sequence split changes no
+    value beyond rounding: tests/test_cp_cpu.py, tests/test_ulysses_cpu.py)."""
+    curves = {}
+    for mode in ("cp", "sp"):
+        curves[mode] = run_pattern(tmp_path / mode, ("-b", "8", f"--{mode}", "2"), steps=100, chapter="00-rime", nproc=2)
+    single = run_pattern(tmp_path / "single", ("-b", "8"), steps=100, chapter="00-rime")
+    for mode, losses in curves.items():
+        assert losses[-1] < losses[0] / 1.6, (mode, losses)
+        assert abs(losses[-1] - single[-1]) < 0.1 * single[-1], (mode, losses, single)
