@@ -63,3 +63,12 @@ def test_pattern_data_is_learned_long_context_cp_and_ulysses(tmp_path):
     for mode, losses in curves.items():
         assert losses[-1] < losses[0] / 1.6, (mode, losses)
         assert abs(losses[-1] - single[-1]) < 0.1 * single[-1], (mode, losses, single)
+
+
+def test_pattern_data_is_learned_pipeline(tmp_path):
+    """Pipeline parallel (--pp 2: two decoder-layer stages, 1F1B over 4 micro-batches, chapter
+    02) learns like one process with the same batch."""
+    pp = run_pattern(tmp_path / "pp", ("-b", "8", "--pp", "2"), steps=100, chapter="02-distributed-data-parallel", nproc=2)
+    single = run_pattern(tmp_path / "single", ("-b", "8"), steps=100, chapter="02-distributed-data-parallel", nproc=1)
+    assert pp[-1] < pp[0] / 1.6, pp
+    assert abs(pp[-1] - single[-1]) < 0.1 * single[-1], (pp, single)
