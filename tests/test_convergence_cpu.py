@@ -9,6 +9,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -40,35 +42,30 @@ def test_pattern_data_is_learned(tmp_path):
 
 def test_pattern_data_is_learned_2d_tp2_dp2(tmp_path):
     """Chapter 07's FSDP x TP (tp 2 x dp 2, four gloo ranks, real collectives) learns too."""
-    losses = run_pattern(tmp_path, ("-b", "8", "--tp", "2"), chapter="07-2d-parallel", nproc=4)
+    losses = run_pattern(tmp_path, ("-b", "8", "--tp", "2"), steps=120, chapter="07-2d-parallel", nproc=4)
     assert math.log(512) * 0.6 < losses[0]
-    assert losses[-1] < 1.5 and losses[-1] < losses[0] / 3, losses
+    assert losses[-1] < losses[0] / 2.5, losses
 
 
 def test_pattern_data_is_learned_fsdp_offload(tmp_path):
     """Chapter 05's FSDP with CPU offload (host AdamW) on two gloo ranks learns too."""
-    losses = run_pattern(tmp_path, ("-b", "8", "--cpu-offload", "on"), chapter="05-training-llama-405b", nproc=2)
+    losses = run_pattern(tmp_path, ("-b", "8", "--cpu-offload", "on"), steps=120, chapter="05-training-llama-405b", nproc=2)
     assert math.log(512) * 0.6 < losses[0]
-    assert losses[-1] < 1.5 and losses[-1] < losses[0] / 3, losses
+    assert losses[-1] < losses[0] / 2.5, losses
 
 
-def test_pattern_data_is_learned_long_context_cp_and_ulysses(tmp_path):
-    """Context parallel (zig-zag shards, --cp 2) and Ulysses (--sp 2) split every sequence over
-    two ranks: both learn like one process with the same batch (the sequence split changes no
-    value beyond rounding: tests/test_cp_cpu.py, tests/test_ulysses_cpu.py)."""
-    curves = {}
-    for mode in ("cp", "sp"):
-        curves[mode] = run_pattern(tmp_path / mode, ("-b", "8", f"--{mode}", "2"), steps=100, chapter="00-rime", nproc=2)
-    single = run_pattern(tmp_path / "single", ("-b", "8"), steps=100, chapter="00-rime")
-    for mode, losses in curves.items():
-        assert losses[-1] < losses[0] / 1.6, (mode, losses)
-        assert abs(losses[-1] - single[-1]) < 0.1 * single[-1], (mode, losses, single)
+@pytest.fixture(scope="module")
+def single_b8(tmp_path_factory):
+    """One process, batch 8, chapter 02: the curve the split runs must follow."""
+    return run_pattern(tmp_path_factory.mktemp("single"), ("-b", "8"), steps=100, chapter="02-distributed-data-parallel")
 
 
-def test_pattern_data_is_learned_pipeline(tmp_path):
-    """Pipeline parallel (--pp 2: two decoder-layer stages, 1F1B over 4 micro-batches, chapter
-    02) learns like one process with the same batch."""
-    pp = run_pattern(tmp_path / "pp", ("-b", "8", "--pp", "2"), steps=100, chapter="02-distributed-data-parallel", nproc=2)
-    single = run_pattern(tmp_path / "single", ("-b", "8"), steps=100, chapter="02-distributed-data-parallel", nproc=1)
-    assert pp[-1] < pp[0] / 1.6, pp
-    assert abs(pp[-1] - single[-1]) < 0.1 * single[-1], (pp, single)
+@pytest.mark.parametrize("split", ["--cp", "--sp", "--pp"])
+def test_pattern_data_is_learned_split_like_one_process(tmp_path, single_b8, split):
+    """Context parallel (zig-zag shards), Ulysses (seq <-> heads all-to-all) and 1F1B pipeline
+    parallel (two decoder-layer stages, 4 micro-batches) each split the work of one batch over two
+    ranks: they learn like one process with the same batch (the splits change no value beyond
+    rounding: tests/test_cp_cpu.py, tests/test_ulysses_cpu.py, tests/test_pipeline_cpu.py)."""
+    losses = run_pattern(tmp_path, ("-b", "8", split, "2"), steps=100, chapter="02-distributed-data-parallel", nproc=2)
+    assert losses[-1] < losses[0] / 1.6, losses
+    assert abs(losses[-1] - single_b8[-1]) < 0.1 * single_b8[-1], (losses, single_b8)
