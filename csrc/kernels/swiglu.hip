@@ -58,7 +58,10 @@ __global__ void swiglu_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_
 // halfwords) and stored as 16-byte columns (TT x 2-byte segments of TF feature rows).
 // 64 x 128 is the measured best of the 64/128 x 64/128 tiles and of a register-blocked 8 x 8
 // form (-2.1 ms per 8B step against 64 x 64, profiles/r3/s32; 4.64 vs 4.52 TB/s against the
-// register-blocked one, profiles/r5/transpose/); the others were removed in round 6.
+// register-blocked one, profiles/r5/transpose/); the others were removed in round 6.  Staging the
+// three outputs one after another through a single 16.6 KB buffer doubled the occupancy (6
+// instead of 3 waves per SIMD) and changed nothing: 5.53 vs 5.50 TB/s, step 581.0 vs 580.7 ms
+// (profiles/r6/swiglu_seq/).
 constexpr int kSgTT = 64, kSgTF = 128;
 
 template <int TT, int TF>
